@@ -1,0 +1,207 @@
+/*
+ * drp.h — C ABI of libdrp, the MI355X (gfx950) batch codec for the
+ * dat-replication-protocol hot path: varint-length-prefixed multibuffer
+ * framing + protobuf `Change` decode/encode.
+ *
+ * Reference interface each entry point replaces (mafintosh/dat-replication-protocol v4.1.2):
+ *   drp_decode_batch / drp_decode_device
+ *       -> Decoder._write/_consume/_onheader/_onchangedata/_onchangeend/_onblobdata
+ *          (decode.js:124-133, 144-169, 251-262, 216-249, 205-214, 179-202)
+ *          + messages.Change.decode (messages/index.js:5, schema messages/schema.proto:1-8)
+ *   drp_carry
+ *       -> the decoder's cross-chunk state _header/_ptr/_id/_missing/_buffer/_blob
+ *          (decode.js:75-81)
+ *   drp_encode_size / drp_encode_batch / drp_encode_device
+ *       -> Encoder.change + Encoder._header (encode.js:102-117, 124-137)
+ *          + messages.Change.encode (messages/index.js:5)
+ *   drp_stream_stats + drp_index_scan
+ *       -> no reference counterpart (the reference is single-stream); they build the
+ *          global frame index after the per-GPU stats tables are all-gathered.
+ *
+ * Rules: every function returns DRP_OK (0) or a negative DRP_E_* code and never
+ * throws or aborts across the ABI. All buffers are caller-owned; libdrp never
+ * frees caller memory and never returns heap pointers. Pointers passed to the
+ * *_device entry points must be device (HBM) pointers; drp_decode_batch /
+ * drp_encode_batch accept host or device pointers and stage as needed.
+ * One drp_ctx per device; a ctx must not be used from two threads at once.
+ */
+#ifndef DRP_H
+#define DRP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DRP_ABI_VERSION 1
+
+/* ---- return codes -------------------------------------------------------- */
+#define DRP_OK 0
+#define DRP_E_INVAL (-1)    /* bad argument */
+#define DRP_E_HIP (-2)      /* HIP runtime error */
+#define DRP_E_NOMEM (-3)    /* device/host allocation failed */
+#define DRP_E_CAPACITY (-4) /* output capacity too small */
+#define DRP_E_NODEV (-5)    /* no gfx950 device */
+#define DRP_E_RETRY (-6)    /* internal: speculation failed and strict re-run also failed */
+
+/* ---- frame types (the id byte, decode.js:146-161) ------------------------ */
+#define DRP_TYPE_CHANGE 1
+#define DRP_TYPE_BLOB 2
+/* OR-ed into type[] for a blob whose payload continues past the end of the batch */
+#define DRP_FRAME_PARTIAL 0x80
+
+/* ---- per-Change flags ---------------------------------------------------- */
+#define DRP_F_SUBSET 0x01 /* optional string subset = 1 present */
+#define DRP_F_VALUE 0x02  /* optional bytes value = 6 present (value may be empty) */
+#define DRP_F_BAD 0x04    /* payload is not a well-formed Change (see err codes) */
+
+/* ---- stream error codes (first failing frame, see DESIGN.md "policy") ---- */
+#define DRP_ERR_NONE 0
+#define DRP_ERR_TYPE 1     /* id byte >= 3: 'Protocol error, unknown type: N' (decode.js:159-161) */
+#define DRP_ERR_LEN 2      /* length varint 0 on a change/blob frame (reference is chunk-size dependent) */
+#define DRP_ERR_VARINT 3   /* header varint longer than 10 bytes or >= 2^64 */
+#define DRP_ERR_CHANGE 4   /* malformed Change payload (truncated field, bad wire type, huge varint) */
+#define DRP_ERR_REQUIRED 5 /* Change payload lacks a required field (key/change/from/to) */
+
+/* ---- tail kinds: what the caller must carry into the next batch ---------- */
+#define DRP_TAIL_NONE 0   /* batch ended on a frame boundary */
+#define DRP_TAIL_HEADER 1 /* batch ended inside a frame header: carry bytes [consumed, n) */
+#define DRP_TAIL_CHANGE 2 /* batch ended inside a change payload: carry bytes [consumed, n) */
+#define DRP_TAIL_BLOB 3   /* batch ended inside a blob payload: blob_remaining bytes still to come */
+
+typedef struct drp_ctx drp_ctx;
+
+/* Frame table, one entry per delivered frame (changes and blobs, in stream order). */
+typedef struct drp_frames {
+  uint64_t *payload_off; /* offset of payload byte 0 in the batch buffer */
+  uint32_t *payload_len; /* declared payload length L-1 (saturates at 0xFFFFFFFF) */
+  uint8_t *type;         /* DRP_TYPE_CHANGE / DRP_TYPE_BLOB (| DRP_FRAME_PARTIAL) */
+} drp_frames;
+
+/* Change columns, indexed by frame index (entries of blob frames are left untouched).
+ * Offsets are relative to payload_off of the same frame. */
+typedef struct drp_changes {
+  uint32_t *key_off, *key_len;
+  uint32_t *subset_off, *subset_len;
+  uint32_t *value_off, *value_len;
+  uint64_t *change, *from, *to;
+  uint8_t *flags;
+} drp_changes;
+
+/* Encoder input: one Change per row; offsets are absolute into `heap`. */
+typedef struct drp_change_src {
+  const uint64_t *key_off;
+  const uint32_t *key_len;
+  const uint64_t *subset_off;
+  const uint32_t *subset_len;
+  const uint64_t *value_off;
+  const uint32_t *value_len;
+  const uint64_t *change, *from, *to;
+  const uint8_t *flags; /* DRP_F_SUBSET / DRP_F_VALUE */
+} drp_change_src;
+
+/* Cross-batch carry (mirrors decode.js:75-81). The caller owns the carried bytes:
+ * on return, bytes [consumed, n) of the batch must be prepended to the next batch
+ * (tail HEADER/CHANGE); for tail BLOB the next batch starts with blob_remaining
+ * bytes of blob payload. */
+typedef struct drp_carry {
+  uint64_t blob_remaining; /* in/out */
+  uint64_t consumed;       /* out */
+  uint32_t tail_kind;      /* out: DRP_TAIL_* */
+  uint32_t reserved;
+} drp_carry;
+
+/* Per-stream result of a (multi-)stream decode. */
+typedef struct drp_stream_result {
+  uint64_t frame_begin;    /* index of the stream's first frame in the output columns */
+  uint64_t frames;         /* delivered frames (stop before err_frame) */
+  uint64_t changes;        /* delivered change frames */
+  uint64_t blobs;          /* delivered blob frames (partial included) */
+  uint64_t consumed;       /* stream-relative offset where the carry starts */
+  uint64_t blob_remaining; /* tail BLOB: payload bytes still to come */
+  uint64_t err_frame;      /* UINT64_MAX if no error, else stream-relative index of failing frame */
+  uint32_t err_code;       /* DRP_ERR_* */
+  uint32_t err_detail;     /* DRP_ERR_TYPE: the id byte */
+  uint32_t tail_kind;      /* DRP_TAIL_* */
+  uint32_t reserved;
+} drp_stream_result;
+
+/* The 32-byte per-stream record exchanged by the multi-GPU all-gather. */
+typedef struct drp_stream_stats {
+  uint64_t frames, changes, blobs, wire_bytes;
+} drp_stream_stats;
+
+/* Timing of the last device launch sequence on a ctx (HIP events, milliseconds). */
+typedef struct drp_timing {
+  float decode_ms;   /* main decode kernel */
+  float finalize_ms; /* per-stream finalize kernel */
+  float total_ms;    /* memset + decode + finalize (+ strict re-run if any) */
+  uint32_t strict_reruns;
+  uint32_t reserved;
+} drp_timing;
+
+/* ---- context ------------------------------------------------------------- */
+int drp_abi_version(void);
+int drp_open(int device, drp_ctx **out);
+void drp_close(drp_ctx *ctx);
+/* The hipStream_t (as void*) all kernels of this ctx are launched on. */
+void *drp_stream(drp_ctx *ctx);
+int drp_synchronize(drp_ctx *ctx);
+int drp_last_timing(drp_ctx *ctx, drp_timing *out);
+/* Tunables (0 = default). tile_bytes must be 64*k, k in {64,128,256}. */
+int drp_set_tile(drp_ctx *ctx, uint32_t tile_bytes);
+/* Force every tile to wait for its predecessor's exact exit (no speculation). Test hook. */
+int drp_set_strict(drp_ctx *ctx, int strict);
+/* Device scratch bytes needed to decode `n` bytes split into `nstreams` streams. */
+uint64_t drp_decode_scratch_bytes(drp_ctx *ctx, uint64_t n, uint64_t nstreams);
+
+/* ---- decode -------------------------------------------------------------- */
+/* Decode `nstreams` independent streams laid end to end in `bytes` (device ptr).
+ * stream_off[nstreams+1] (device) gives stream s = bytes[stream_off[s], stream_off[s+1]);
+ * entry[nstreams] (device, may be NULL = all zero) is the stream-relative offset of the
+ * first frame header (skips a blob continuation). Frames of all streams are written to
+ * `frames`/`cols` (device) in stream order; per-stream results go to results[] (device).
+ * Asynchronous on drp_stream(ctx); capacity `cap` frames. */
+int drp_decode_device(drp_ctx *ctx, const uint8_t *bytes, const uint64_t *stream_off,
+                      const uint64_t *entry, uint64_t nstreams, const drp_frames *frames,
+                      const drp_changes *cols, uint64_t cap, drp_stream_result *results);
+
+/* Synchronous single-stream decode of one batch (host or device pointers).
+ * carry->blob_remaining in: leading blob continuation; out: carry for the next batch.
+ * Returns frames delivered in *n_frames, first failing frame in *err_frame
+ * (UINT64_MAX if none) with *err_code and *err_detail. A leading blob continuation is
+ * reported as frame 0 with type DRP_TYPE_BLOB|0x40 (continuation). */
+#define DRP_FRAME_CONT 0x40
+int drp_decode_batch(drp_ctx *ctx, const uint8_t *bytes, uint64_t n, drp_carry *carry,
+                     const drp_frames *frames, const drp_changes *cols, uint64_t cap,
+                     uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code,
+                     uint32_t *err_detail);
+
+/* ---- encode -------------------------------------------------------------- */
+/* Wire size of encoding rows [0,n) as change frames (varint(len+1) 0x01 payload). */
+int drp_encode_size(drp_ctx *ctx, const drp_change_src *src, uint64_t n, uint64_t *wire_bytes);
+/* Device pointers; asynchronous. frame_off[n+1] (device scratch, written) receives the
+ * exclusive prefix of frame sizes; *wire_bytes is written to device memory. */
+int drp_encode_device(drp_ctx *ctx, const drp_change_src *src, const uint8_t *heap, uint64_t n,
+                      uint64_t *frame_off, uint8_t *out, uint64_t cap);
+/* Synchronous; host or device pointers. */
+int drp_encode_batch(drp_ctx *ctx, const drp_change_src *src, const uint8_t *heap,
+                     uint64_t heap_bytes, uint64_t n, uint8_t *out, uint64_t cap,
+                     uint64_t *written);
+
+/* ---- multi-GPU global index ---------------------------------------------- */
+/* stats[nranks*per_rank] (device): all-gathered per-stream tables in rank order.
+ * Writes base[nranks*per_rank] (device): exclusive prefix of frames = global index of
+ * each stream's first frame. Asynchronous. */
+int drp_index_scan(drp_ctx *ctx, const drp_stream_stats *stats, uint64_t count, uint64_t *base);
+/* results[nstreams] (device) -> stats[nstreams] (device), asynchronous. */
+int drp_stream_stats_from_results(drp_ctx *ctx, const drp_stream_result *results,
+                                  const uint64_t *stream_off, uint64_t nstreams,
+                                  drp_stream_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRP_H */
