@@ -1,0 +1,632 @@
+// drp_api.hip — the extern "C" boundary of libdrp (include/drp.h).
+//
+// Owns one HIP stream + scratch per device context, launches the decode / encode kernels,
+// and runs the speculation-repair loop of the decode: after a pass,
+// the first tile whose exact exit differs from its published speculative exit is given its
+// exact exit as an override and every tile from there on is re-run.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <vector>
+
+#include "../../include/drp.h"
+#include "drp_kernels.h"
+
+using drp::DecodeParams;
+using drp::EncodeParams;
+
+namespace {
+
+bool trace_on() {
+  static int v = -1;
+  if (v < 0) v = getenv("DRP_TRACE") ? 1 : 0;
+  return v == 1;
+}
+#define TRACE(...)                                \
+  do {                                            \
+    if (trace_on()) {                             \
+      fprintf(stderr, "[drp] " __VA_ARGS__);      \
+      fputc('\n', stderr);                        \
+      fflush(stderr);                             \
+    }                                             \
+  } while (0)
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t n) {
+    if (n <= cap) return true;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n + n / 4 + 4096;
+    if (hipMalloc(&p, want) != hipSuccess) return false;
+    cap = want;
+    return true;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T *at(size_t off) const {
+    return reinterpret_cast<T *>(static_cast<char *>(p) + off);
+  }
+};
+
+bool is_device_ptr(const void *p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+struct drp_ctx {
+  int device = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t ev[4] = {};
+  uint32_t B = 128;
+  int strict = 0;
+  int cus = 256;
+  DevBuf scratch, in_stage, out_stage, aux;
+  drp_timing timing = {};
+  std::vector<uint64_t> host_tmp;
+};
+
+#define CHK(x)                                                                     \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      if (getenv("DRP_DEBUG")) fprintf(stderr, "drp: %s -> %s\n", #x, hipGetErrorString(e_)); \
+      return DRP_E_HIP;                                                            \
+    }                                                                              \
+  } while (0)
+
+extern "C" {
+
+int drp_abi_version(void) { return DRP_ABI_VERSION; }
+
+int drp_open(int device, drp_ctx **out) {
+  if (!out) return DRP_E_INVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return DRP_E_NODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return DRP_E_NODEV;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return DRP_E_NODEV;
+  drp_ctx *c = new drp_ctx();
+  c->device = device;
+  c->cus = prop.multiProcessorCount;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return DRP_E_HIP;
+  }
+  for (auto &e : c->ev) hipEventCreate(&e);
+  if (const char *t = getenv("DRP_TILE")) {
+    uint32_t tb = (uint32_t)atoi(t);
+    if (tb == 4096 || tb == 8192 || tb == 16384) c->B = tb / 64;
+  }
+  *out = c;
+  return DRP_OK;
+}
+
+void drp_close(drp_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->st);
+  c->scratch.release();
+  c->in_stage.release();
+  c->out_stage.release();
+  c->aux.release();
+  for (auto &e : c->ev) hipEventDestroy(e);
+  hipStreamDestroy(c->st);
+  delete c;
+}
+
+void *drp_stream(drp_ctx *c) { return c ? (void *)c->st : nullptr; }
+
+int drp_synchronize(drp_ctx *c) {
+  if (!c) return DRP_E_INVAL;
+  CHK(hipStreamSynchronize(c->st));
+  return DRP_OK;
+}
+
+int drp_last_timing(drp_ctx *c, drp_timing *out) {
+  if (!c || !out) return DRP_E_INVAL;
+  *out = c->timing;
+  return DRP_OK;
+}
+
+int drp_set_tile(drp_ctx *c, uint32_t tile_bytes) {
+  if (!c) return DRP_E_INVAL;
+  if (tile_bytes == 0) tile_bytes = 8192;
+  if (tile_bytes != 4096 && tile_bytes != 8192 && tile_bytes != 16384) return DRP_E_INVAL;
+  c->B = tile_bytes / 64;
+  return DRP_OK;
+}
+
+int drp_set_strict(drp_ctx *c, int strict) {
+  if (!c) return DRP_E_INVAL;
+  c->strict = strict ? 1 : 0;
+  return DRP_OK;
+}
+
+// scratch layout for a decode of `nbytes` over `ns` streams
+struct DecLayout {
+  uint64_t ntiles_max;
+  size_t tile_prefix, rec, tiles, yover, perr, scount, ctrl, total;
+};
+static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
+  DecLayout L;
+  const uint64_t tile = 64ull * B;
+  L.ntiles_max = nbytes / tile + 2 * ns + 2;
+  size_t o = 0;
+  L.tile_prefix = o; o += al((ns + 1) * 8);
+  L.rec = o; o += al(4 * L.ntiles_max * 8);    // aggx, inclx, aggc, inclc
+  L.tiles = o; o += al(7 * L.ntiles_max * 8);  // x, exit, base, count, nch, nbl, perr
+  L.yover = o; o += al(L.ntiles_max * 8);
+  L.perr = o; o += al(ns * 8);
+  L.scount = o; o += al(2 * ns * 8);
+  L.ctrl = o; o += 256;
+  L.total = o;
+  return L;
+}
+
+uint64_t drp_decode_scratch_bytes(drp_ctx *c, uint64_t n, uint64_t nstreams) {
+  return dec_layout(c ? c->B : 128, n, nstreams).total;
+}
+
+}  // extern "C"
+
+namespace {
+
+__global__ void recount_kernel(const uint64_t *tile_prefix, uint64_t nstreams, const uint64_t *tile_nch,
+                               const uint64_t *tile_nbl, const uint64_t *tile_perr, uint64_t *scount,
+                               uint64_t *perr) {
+  const uint64_t ntiles = tile_prefix[nstreams];
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t lo = 0, hi = nstreams;
+    while (hi - lo > 1) {
+      uint64_t mid = (lo + hi) >> 1;
+      if (tile_prefix[mid] <= t) lo = mid; else hi = mid;
+    }
+    if (tile_nch[t]) atomicAdd((unsigned long long *)&scount[2 * lo], (unsigned long long)tile_nch[t]);
+    if (tile_nbl[t]) atomicAdd((unsigned long long *)&scount[2 * lo + 1], (unsigned long long)tile_nbl[t]);
+    if (tile_perr[t] != ~0ull) atomicMin((unsigned long long *)&perr[lo], (unsigned long long)tile_perr[t]);
+  }
+}
+
+int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
+               const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
+               uint64_t cap, drp_stream_result *res) {
+  if (ns == 0) return DRP_OK;
+  if (((uintptr_t)bytes & 15) != 0) return DRP_E_INVAL;
+  const DecLayout L = dec_layout(c->B, nbytes, ns);
+  if (!c->scratch.ensure(L.total)) return DRP_E_NOMEM;
+  const uint64_t NT = L.ntiles_max;
+  uint64_t *tile_prefix = c->scratch.at<uint64_t>(L.tile_prefix);
+  uint64_t *rec = c->scratch.at<uint64_t>(L.rec);
+  uint64_t *tiles = c->scratch.at<uint64_t>(L.tiles);
+  uint64_t *yover = c->scratch.at<uint64_t>(L.yover);
+  uint64_t *perr = c->scratch.at<uint64_t>(L.perr);
+  uint64_t *scount = c->scratch.at<uint64_t>(L.scount);
+  uint32_t *ctrl = c->scratch.at<uint32_t>(L.ctrl);  // [0] counter [1] misspec [2] overflow
+
+  hipStream_t st = c->st;
+  CHK(hipEventRecord(c->ev[0], st));
+  CHK(hipMemsetAsync(rec, 0, 4 * NT * 8, st));
+  CHK(hipMemsetAsync(yover, 0, NT * 8, st));
+  CHK(hipMemsetAsync(tiles + 6 * NT, 0xFF, NT * 8, st));  // tile_perr
+  CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
+  CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
+  uint32_t ctrl_init[4] = {0, 0xFFFFFFFFu, 0, 0};
+  CHK(hipMemcpyAsync(ctrl, ctrl_init, 16, hipMemcpyHostToDevice, st));
+  CHK(drp_launch_tile_prefix(c->B, stream_off, ns, tile_prefix, st));
+
+  DecodeParams P;
+  memset(&P, 0, sizeof(P));
+  P.bytes = bytes;
+  P.nbytes = nbytes;
+  P.stream_off = stream_off;
+  P.entry = entry;
+  P.nstreams = ns;
+  P.tile_prefix = tile_prefix;
+  P.payload_off = fr->payload_off;
+  P.payload_len = fr->payload_len;
+  P.type = fr->type;
+  P.key_off = co->key_off;
+  P.key_len = co->key_len;
+  P.subset_off = co->subset_off;
+  P.subset_len = co->subset_len;
+  P.value_off = co->value_off;
+  P.value_len = co->value_len;
+  P.change = co->change;
+  P.from = co->from;
+  P.to = co->to;
+  P.flags = co->flags;
+  P.cap = cap;
+  P.aggx = rec;
+  P.inclx = rec + NT;
+  P.aggc = rec + 2 * NT;
+  P.inclc = rec + 3 * NT;
+  P.tile_x = tiles;
+  P.tile_exit = tiles + NT;
+  P.tile_base = tiles + 2 * NT;
+  P.tile_count = tiles + 3 * NT;
+  P.tile_nch = tiles + 4 * NT;
+  P.tile_nbl = tiles + 5 * NT;
+  P.tile_perr = tiles + 6 * NT;
+  P.yover = yover;
+  P.payload_err = perr;
+  P.scount = scount;
+  P.counter = ctrl;
+  P.misspec = ctrl + 1;
+  P.overflow = ctrl + 2;
+  P.strict = (uint32_t)c->strict;
+
+  // persistent grid: enough single-wave blocks to fill every CU several times over
+  const uint32_t tile = 64u * c->B;
+  const uint64_t tiles_needed = nbytes / tile + ns + 1;
+  uint32_t grid = (uint32_t)(c->cus * (c->B >= 256 ? 8 : 12));
+  if (tiles_needed < grid) grid = (uint32_t)tiles_needed;
+  if (grid == 0) grid = 1;
+
+  TRACE("decode: nbytes=%llu ns=%llu B=%u grid=%u NT=%llu", (unsigned long long)nbytes,
+        (unsigned long long)ns, c->B, grid, (unsigned long long)NT);
+  uint32_t *hdbg = nullptr;
+  if (trace_on()) {
+    CHK(hipStreamSynchronize(st));
+    uint64_t tp[2] = {0, 0};
+    CHK(hipMemcpy(tp, tile_prefix + ns, 8, hipMemcpyDeviceToHost));
+    TRACE("ntiles=%llu", (unsigned long long)tp[0]);
+    CHK(hipHostMalloc((void **)&hdbg, grid * 16, hipHostMallocMapped));
+    memset(hdbg, 0, grid * 16);
+    uint32_t *ddbg = nullptr;
+    CHK(hipHostGetDevicePointer((void **)&ddbg, hdbg, 0));
+    P.dbg = ddbg;
+  }
+  CHK(hipEventRecord(c->ev[1], st));
+  CHK(drp_launch_decode(c->B, &P, grid, st));
+  CHK(hipEventRecord(c->ev[2], st));
+  if (trace_on()) {
+    for (int it = 0; it < 100 && hipStreamQuery(st) == hipErrorNotReady; it++) {
+      struct timespec ts = {0, 50 * 1000 * 1000};
+      nanosleep(&ts, nullptr);
+    }
+    for (uint32_t b = 0; b < grid && b < 64; b++)
+      TRACE("block %u: stage=%u tile=%u done=%x", b, hdbg[b * 4], hdbg[b * 4 + 1], hdbg[b * 4 + 2]);
+    if (hipStreamQuery(st) == hipErrorNotReady) {
+      TRACE("decode kernel still running after 5 s: aborting");
+      abort();
+    }
+    TRACE("decode kernel done");
+    P.dbg = nullptr;
+  }
+
+  uint32_t reruns = 0;
+  bool repaired = false;
+  for (;;) {
+    uint32_t h[4];
+    CHK(hipMemcpyAsync(h, ctrl, 16, hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+    TRACE("pass done: counter=%u misspec=%u flags=%u", h[0], h[1], h[2]);
+    if (h[1] == 0xFFFFFFFFu || (h[2] & 2u)) break;
+    // speculation failed at tile m: give it its exact exit and re-run tiles >= m
+    const uint64_t m = h[1];
+    repaired = true;
+    reruns++;
+    if (reruns > 64 && !P.strict) P.strict = 1;  // pathological input: no speculation
+    uint64_t ex_m = 0;
+    CHK(hipMemcpyAsync(&ex_m, P.tile_exit + m, 8, hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+    const uint64_t ov = ex_m + 1;
+    CHK(hipMemcpyAsync(yover + m, &ov, 8, hipMemcpyHostToDevice, st));
+    for (int k = 0; k < 4; k++) CHK(hipMemsetAsync(rec + k * NT + m, 0, (NT - m) * 8, st));
+    uint32_t ctrl_re[4] = {(uint32_t)m, 0xFFFFFFFFu, 0, 0};
+    CHK(hipMemcpyAsync(ctrl, ctrl_re, 12, hipMemcpyHostToDevice, st));
+    CHK(drp_launch_decode(c->B, &P, grid, st));
+  }
+  if (repaired) {
+    CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
+    CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
+    hipLaunchKernelGGL(recount_kernel, dim3(256), dim3(256), 0, st, tile_prefix, ns, P.tile_nch, P.tile_nbl,
+                       P.tile_perr, scount, perr);
+    CHK(hipGetLastError());
+  }
+  CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
+                          scount, fr->type, co->flags, cap, res, st));
+  CHK(hipEventRecord(c->ev[3], st));
+  uint32_t h[4];
+  CHK(hipMemcpyAsync(h, ctrl, 16, hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  float ms = 0;
+  hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
+  c->timing.decode_ms = ms;
+  hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
+  c->timing.total_ms = ms;
+  c->timing.finalize_ms = 0;
+  c->timing.strict_reruns = reruns;
+  if (h[2] & 2u) return DRP_E_HIP;  // bounded wait expired inside the kernel
+  if (h[2]) return DRP_E_CAPACITY;
+  return DRP_OK;
+}
+
+// carve SoA outputs for `cap` frames out of a device buffer
+void carve(DevBuf &b, uint64_t cap, drp_frames &fr, drp_changes &co) {
+  size_t o = 0;
+  auto take = [&](size_t bytes) { void *p = b.at<char>(o); o += al(bytes); return p; };
+  fr.payload_off = (uint64_t *)take(cap * 8);
+  fr.payload_len = (uint32_t *)take(cap * 4);
+  fr.type = (uint8_t *)take(cap);
+  co.key_off = (uint32_t *)take(cap * 4);
+  co.key_len = (uint32_t *)take(cap * 4);
+  co.subset_off = (uint32_t *)take(cap * 4);
+  co.subset_len = (uint32_t *)take(cap * 4);
+  co.value_off = (uint32_t *)take(cap * 4);
+  co.value_len = (uint32_t *)take(cap * 4);
+  co.change = (uint64_t *)take(cap * 8);
+  co.from = (uint64_t *)take(cap * 8);
+  co.to = (uint64_t *)take(cap * 8);
+  co.flags = (uint8_t *)take(cap);
+}
+size_t carve_bytes(uint64_t cap) { return 13 * 256 + cap * 62; }
+
+}  // namespace
+
+extern "C" {
+
+int drp_decode_device(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
+                      const uint64_t *entry, uint64_t nstreams, const drp_frames *frames,
+                      const drp_changes *cols, uint64_t cap, drp_stream_result *results) {
+  if (!c || !stream_off || !frames || !cols || !results || (!bytes && nbytes)) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  return run_decode(c, bytes, nbytes, stream_off, entry, nstreams, frames, cols, cap, results);
+}
+
+int drp_decode_batch(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *carry, const drp_frames *frames,
+                     const drp_changes *cols, uint64_t cap, uint64_t *n_frames, uint64_t *err_frame,
+                     uint32_t *err_code, uint32_t *err_detail) {
+  if (!c || !carry || !frames || !cols || !n_frames || !err_frame || !err_code || !err_detail) return DRP_E_INVAL;
+  if (!bytes && n) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  const bool out_dev = is_device_ptr(frames->payload_off);
+  hipStream_t st = c->st;
+  *err_frame = ~0ull;
+  *err_code = DRP_ERR_NONE;
+  *err_detail = 0;
+  uint64_t nf0 = 0;
+  const uint64_t brem = carry->blob_remaining;
+  // A blob continuation (decode.js _id == 2 with _missing > 0 across _write calls) is frame 0.
+  if (brem) {
+    if (cap < 1) return DRP_E_CAPACITY;
+    uint64_t off0 = 0;
+    uint32_t len0 = brem > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)brem;
+    uint8_t ty0 = DRP_TYPE_BLOB | DRP_FRAME_CONT | (brem > n ? DRP_FRAME_PARTIAL : 0);
+    if (out_dev) {
+      CHK(hipMemcpyAsync(frames->payload_off, &off0, 8, hipMemcpyHostToDevice, st));
+      CHK(hipMemcpyAsync(frames->payload_len, &len0, 4, hipMemcpyHostToDevice, st));
+      CHK(hipMemcpyAsync(frames->type, &ty0, 1, hipMemcpyHostToDevice, st));
+      CHK(hipStreamSynchronize(st));
+    } else {
+      frames->payload_off[0] = off0;
+      frames->payload_len[0] = len0;
+      frames->type[0] = ty0;
+    }
+    nf0 = 1;
+    if (brem >= n) {
+      carry->blob_remaining = brem - n;
+      carry->consumed = n;
+      carry->tail_kind = carry->blob_remaining ? DRP_TAIL_BLOB : DRP_TAIL_NONE;
+      *n_frames = 1;
+      return DRP_OK;
+    }
+  }
+  const uint64_t entry0 = brem;
+  // input: device & aligned, or staged
+  const uint8_t *dbytes = bytes;
+  const size_t stage_meta = 256;
+  if (!c->aux.ensure(stage_meta + sizeof(drp_stream_result) + 64)) return DRP_E_NOMEM;
+  uint64_t *soff = c->aux.at<uint64_t>(0);
+  uint64_t *ent = c->aux.at<uint64_t>(16);
+  drp_stream_result *dres = c->aux.at<drp_stream_result>(stage_meta);
+  if (!is_device_ptr(bytes) || ((uintptr_t)bytes & 15)) {
+    if (!c->in_stage.ensure(n + 64)) return DRP_E_NOMEM;
+    if (n) CHK(hipMemcpyAsync(c->in_stage.p, bytes, n, hipMemcpyDefault, st));
+    dbytes = (const uint8_t *)c->in_stage.p;
+  }
+  uint64_t hv[3] = {0, n, entry0};
+  CHK(hipMemcpyAsync(soff, hv, 16, hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(ent, hv + 2, 8, hipMemcpyHostToDevice, st));
+  const uint64_t cap_rest = cap - nf0;
+  drp_frames dfr;
+  drp_changes dco;
+  if (out_dev) {
+    dfr.payload_off = frames->payload_off + nf0;
+    dfr.payload_len = frames->payload_len + nf0;
+    dfr.type = frames->type + nf0;
+    dco.key_off = cols->key_off + nf0;
+    dco.key_len = cols->key_len + nf0;
+    dco.subset_off = cols->subset_off + nf0;
+    dco.subset_len = cols->subset_len + nf0;
+    dco.value_off = cols->value_off + nf0;
+    dco.value_len = cols->value_len + nf0;
+    dco.change = cols->change + nf0;
+    dco.from = cols->from + nf0;
+    dco.to = cols->to + nf0;
+    dco.flags = cols->flags + nf0;
+  } else {
+    if (!c->out_stage.ensure(carve_bytes(cap_rest))) return DRP_E_NOMEM;
+    carve(c->out_stage, cap_rest, dfr, dco);
+  }
+  int rc = run_decode(c, dbytes, n, soff, ent, 1, &dfr, &dco, cap_rest, dres);
+  if (rc != DRP_OK && rc != DRP_E_CAPACITY) return rc;
+  drp_stream_result r;
+  CHK(hipMemcpyAsync(&r, dres, sizeof(r), hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  const uint64_t nf = r.frames;
+  // keep the failing Change in the table (its flags say why)
+  uint64_t ncopy = nf + ((r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0);
+  if (ncopy > cap_rest) ncopy = cap_rest;
+  if (!out_dev && ncopy) {
+    auto cp = [&](void *dst, const void *src, size_t bytes) {
+      return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+    };
+    CHK(cp(frames->payload_off + nf0, dfr.payload_off, ncopy * 8));
+    CHK(cp(frames->payload_len + nf0, dfr.payload_len, ncopy * 4));
+    CHK(cp(frames->type + nf0, dfr.type, ncopy));
+    CHK(cp(cols->key_off + nf0, dco.key_off, ncopy * 4));
+    CHK(cp(cols->key_len + nf0, dco.key_len, ncopy * 4));
+    CHK(cp(cols->subset_off + nf0, dco.subset_off, ncopy * 4));
+    CHK(cp(cols->subset_len + nf0, dco.subset_len, ncopy * 4));
+    CHK(cp(cols->value_off + nf0, dco.value_off, ncopy * 4));
+    CHK(cp(cols->value_len + nf0, dco.value_len, ncopy * 4));
+    CHK(cp(cols->change + nf0, dco.change, ncopy * 8));
+    CHK(cp(cols->from + nf0, dco.from, ncopy * 8));
+    CHK(cp(cols->to + nf0, dco.to, ncopy * 8));
+    CHK(cp(cols->flags + nf0, dco.flags, ncopy));
+    CHK(hipStreamSynchronize(st));
+  }
+  *n_frames = nf0 + nf;
+  if (r.err_code) {
+    *err_frame = nf0 + r.err_frame;
+    *err_code = r.err_code;
+    *err_detail = r.err_detail;
+  }
+  carry->blob_remaining = r.blob_remaining;
+  carry->consumed = r.consumed;
+  carry->tail_kind = r.tail_kind;
+  return rc;
+}
+
+int drp_encode_device(drp_ctx *c, const drp_change_src *src, const uint8_t *heap, uint64_t n,
+                      uint64_t *frame_off, uint8_t *out, uint64_t cap) {
+  if (!c || !src || !frame_off) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  const uint64_t nblk = (n + 1023) / 1024;
+  if (!c->aux.ensure(4096 + nblk * 8 + 64)) return DRP_E_NOMEM;
+  EncodeParams P;
+  P.src = *src;
+  P.heap = heap;
+  P.n = n;
+  P.frame_off = frame_off;
+  P.out = out;
+  P.cap = cap;
+  P.block_sum = c->aux.at<uint64_t>(4096);
+  P.overflow = c->aux.at<uint32_t>(1024);
+  CHK(hipMemsetAsync(P.overflow, 0, 4, c->st));
+  if (n == 0) {
+    CHK(hipMemsetAsync(frame_off, 0, 8, c->st));
+    return DRP_OK;
+  }
+  CHK(drp_launch_encode(&P, c->st));
+  return DRP_OK;
+}
+
+// stage src columns (+heap) to the device if needed; returns device-side src
+static int stage_src(drp_ctx *c, const drp_change_src *src, const uint8_t *heap, uint64_t heap_bytes, uint64_t n,
+                     drp_change_src &dsrc, const uint8_t *&dheap) {
+  if (is_device_ptr(src->key_off)) {
+    dsrc = *src;
+    dheap = heap;
+    if (!is_device_ptr(heap) && heap_bytes) {
+      if (!c->in_stage.ensure(heap_bytes)) return DRP_E_NOMEM;
+      CHK(hipMemcpyAsync(c->in_stage.p, heap, heap_bytes, hipMemcpyDefault, c->st));
+      dheap = (const uint8_t *)c->in_stage.p;
+    }
+    return DRP_OK;
+  }
+  const size_t need = al(heap_bytes + 16) + 10 * al(n * 8 + 8);
+  if (!c->in_stage.ensure(need)) return DRP_E_NOMEM;
+  size_t o = 0;
+  auto put = [&](const void *h, size_t bytes) -> void * {
+    void *d = c->in_stage.at<char>(o);
+    o += al(bytes + 8);
+    if (bytes) hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->st);
+    return d;
+  };
+  dheap = (const uint8_t *)put(heap, heap_bytes);
+  dsrc.key_off = (const uint64_t *)put(src->key_off, n * 8);
+  dsrc.key_len = (const uint32_t *)put(src->key_len, n * 4);
+  dsrc.subset_off = (const uint64_t *)put(src->subset_off, n * 8);
+  dsrc.subset_len = (const uint32_t *)put(src->subset_len, n * 4);
+  dsrc.value_off = (const uint64_t *)put(src->value_off, n * 8);
+  dsrc.value_len = (const uint32_t *)put(src->value_len, n * 4);
+  dsrc.change = (const uint64_t *)put(src->change, n * 8);
+  dsrc.from = (const uint64_t *)put(src->from, n * 8);
+  dsrc.to = (const uint64_t *)put(src->to, n * 8);
+  dsrc.flags = (const uint8_t *)put(src->flags, n);
+  CHK(hipGetLastError());
+  return DRP_OK;
+}
+
+int drp_encode_size(drp_ctx *c, const drp_change_src *src, uint64_t n, uint64_t *wire_bytes) {
+  if (!c || !src || !wire_bytes) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  drp_change_src dsrc;
+  const uint8_t *dheap;
+  int rc = stage_src(c, src, nullptr, 0, n, dsrc, dheap);
+  if (rc) return rc;
+  if (!c->out_stage.ensure((n + 1) * 8)) return DRP_E_NOMEM;
+  uint64_t *foff = c->out_stage.at<uint64_t>(0);
+  rc = drp_encode_device(c, &dsrc, dheap, n, foff, nullptr, ~0ull);
+  if (rc) return rc;
+  CHK(hipMemcpyAsync(wire_bytes, foff + n, 8, hipMemcpyDeviceToHost, c->st));
+  CHK(hipStreamSynchronize(c->st));
+  return DRP_OK;
+}
+
+int drp_encode_batch(drp_ctx *c, const drp_change_src *src, const uint8_t *heap, uint64_t heap_bytes, uint64_t n,
+                     uint8_t *out, uint64_t cap, uint64_t *written) {
+  if (!c || !src || !written || (!out && cap)) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  drp_change_src dsrc;
+  const uint8_t *dheap;
+  int rc = stage_src(c, src, heap, heap_bytes, n, dsrc, dheap);
+  if (rc) return rc;
+  const bool odev = is_device_ptr(out);
+  const size_t fo_bytes = al((n + 1) * 8);
+  if (!c->out_stage.ensure(fo_bytes + (odev ? 0 : cap + 64))) return DRP_E_NOMEM;
+  uint64_t *foff = c->out_stage.at<uint64_t>(0);
+  uint8_t *dout = odev ? out : c->out_stage.at<uint8_t>(fo_bytes);
+  rc = drp_encode_device(c, &dsrc, dheap, n, foff, dout, cap);
+  if (rc) return rc;
+  uint64_t total = 0;
+  CHK(hipMemcpyAsync(&total, foff + n, 8, hipMemcpyDeviceToHost, c->st));
+  CHK(hipStreamSynchronize(c->st));
+  *written = total;
+  if (total > cap) return DRP_E_CAPACITY;
+  if (!odev && total) {
+    CHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, c->st));
+    CHK(hipStreamSynchronize(c->st));
+  }
+  return DRP_OK;
+}
+
+int drp_index_scan(drp_ctx *c, const drp_stream_stats *stats, uint64_t count, uint64_t *base) {
+  if (!c || (!stats && count) || (!base && count)) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  CHK(drp_launch_index_scan(stats, count, base, c->st));
+  return DRP_OK;
+}
+
+int drp_stream_stats_from_results(drp_ctx *c, const drp_stream_result *results, const uint64_t *stream_off,
+                                  uint64_t nstreams, drp_stream_stats *stats) {
+  if (!c || (!results && nstreams) || (!stats && nstreams)) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  CHK(drp_launch_stats_from_results(results, stream_off, nstreams, stats, c->st));
+  return DRP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,233 @@
+// drp_encode.hip — gfx950 batched Change encode: Encoder.change + Encoder._header
+// (encode.js:102-117, 124-137) + messages.Change.encode (messages/index.js:5) for n rows.
+//
+// Three passes over the rows: (1) frame sizes, (2) exclusive scan of the sizes
+// (per-block sums, then a single-block scan of the block sums), (3) one wave per frame
+// assembles its bytes: lane 0 writes the header and field prefixes, all 64 lanes copy the
+// key / subset / value bytes. Also the per-stream stats and global index scan used by the
+// multi-GPU all-gather path.
+#include "drp_device.h"
+#include "drp_kernels.h"
+
+namespace drp {
+
+__device__ __forceinline__ uint32_t vlen64(uint64_t v) {
+  uint32_t n = 1;
+  while (v >= 0x80) {
+    v >>= 7;
+    n++;
+  }
+  return n;
+}
+__device__ __forceinline__ uint32_t venc(uint64_t v, uint8_t *o) {
+  uint32_t n = 0;
+  while (v >= 0x80) {
+    o[n++] = (uint8_t)(v | 0x80);
+    v >>= 7;
+  }
+  o[n++] = (uint8_t)v;
+  return n;
+}
+
+// payload length of row i (protocol-buffers@2 field order: subset?, key, change, from, to, value?)
+__device__ __forceinline__ uint64_t payload_len(const drp_change_src &s, uint64_t i) {
+  const uint32_t fl = s.flags[i];
+  uint64_t n = 0;
+  if (fl & DRP_F_SUBSET) n += 1 + vlen64(s.subset_len[i]) + s.subset_len[i];
+  n += 1 + vlen64(s.key_len[i]) + s.key_len[i];
+  n += 1 + vlen64(s.change[i]) + 1 + vlen64(s.from[i]) + 1 + vlen64(s.to[i]);
+  if (fl & DRP_F_VALUE) n += 1 + vlen64(s.value_len[i]) + s.value_len[i];
+  return n;
+}
+
+constexpr uint32_t SCAN_BLK = 1024;
+
+__global__ __launch_bounds__(SCAN_BLK) void enc_size_kernel(EncodeParams P) {
+  __shared__ uint64_t part[SCAN_BLK];
+  const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLK + threadIdx.x;
+  uint64_t sz = 0;
+  if (i < P.n) {
+    const uint64_t pl = payload_len(P.src, i);
+    sz = vlen64(pl + 1) + 1 + pl;
+  }
+  part[threadIdx.x] = sz;
+  __syncthreads();
+  for (uint32_t d = 1; d < SCAN_BLK; d <<= 1) {
+    uint64_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  if (i < P.n) P.frame_off[i] = part[threadIdx.x] - sz;  // block-local exclusive
+  if (threadIdx.x == SCAN_BLK - 1) P.block_sum[blockIdx.x] = part[SCAN_BLK - 1];
+}
+
+__global__ __launch_bounds__(SCAN_BLK) void enc_blocksum_kernel(EncodeParams P, uint64_t nblk) {
+  __shared__ uint64_t part[SCAN_BLK];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint64_t c0 = 0; c0 < nblk; c0 += SCAN_BLK) {
+    const uint64_t b = c0 + threadIdx.x;
+    const uint64_t v0 = b < nblk ? P.block_sum[b] : 0;
+    part[threadIdx.x] = v0;
+    __syncthreads();
+    for (uint32_t d = 1; d < SCAN_BLK; d <<= 1) {
+      uint64_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+    }
+    if (b < nblk) P.block_sum[b] = carry + part[threadIdx.x] - v0;
+    __syncthreads();
+    if (threadIdx.x == SCAN_BLK - 1) carry += part[SCAN_BLK - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    P.frame_off[P.n] = carry;
+    if (carry > P.cap) atomicOr(P.overflow, 1u);
+  }
+}
+
+__global__ __launch_bounds__(SCAN_BLK) void enc_addbase_kernel(EncodeParams P) {
+  const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLK + threadIdx.x;
+  if (i < P.n) P.frame_off[i] += P.block_sum[blockIdx.x];
+}
+
+__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t lane) {
+  for (uint64_t k = lane; k < n; k += 64) dst[k] = src[k];
+}
+
+// one wave per frame (grid-stride over frames)
+__global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
+  const uint32_t lane = lane_id();
+  const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  if (P.frame_off[P.n] > P.cap) return;
+  const drp_change_src &s = P.src;
+  for (uint64_t i = wid; i < P.n; i += nw) {
+    uint8_t *o = P.out + P.frame_off[i];
+    const uint32_t fl = s.flags[i];
+    const uint64_t pl = payload_len(s, i);
+    // header + subset prefix
+    uint8_t pre[32];
+    uint32_t h = venc(pl + 1, pre);
+    pre[h++] = DRP_TYPE_CHANGE;
+    uint64_t off = 0;
+    if (lane == 0)
+      for (uint32_t k = 0; k < h; k++) o[k] = pre[k];
+    off = h;
+    if (fl & DRP_F_SUBSET) {
+      uint8_t t[12];
+      uint32_t m = 0;
+      t[m++] = 0x0a;
+      m += venc(s.subset_len[i], t + m);
+      if (lane == 0)
+        for (uint32_t k = 0; k < m; k++) o[off + k] = t[k];
+      off += m;
+      wave_copy(o + off, P.heap + s.subset_off[i], s.subset_len[i], lane);
+      off += s.subset_len[i];
+    }
+    {
+      uint8_t t[12];
+      uint32_t m = 0;
+      t[m++] = 0x12;
+      m += venc(s.key_len[i], t + m);
+      if (lane == 0)
+        for (uint32_t k = 0; k < m; k++) o[off + k] = t[k];
+      off += m;
+      wave_copy(o + off, P.heap + s.key_off[i], s.key_len[i], lane);
+      off += s.key_len[i];
+    }
+    {
+      uint8_t t[36];
+      uint32_t m = 0;
+      t[m++] = 0x18;
+      m += venc(s.change[i], t + m);
+      t[m++] = 0x20;
+      m += venc(s.from[i], t + m);
+      t[m++] = 0x28;
+      m += venc(s.to[i], t + m);
+      if (fl & DRP_F_VALUE) {
+        t[m++] = 0x32;
+        m += venc(s.value_len[i], t + m);
+      }
+      if (lane == 0)
+        for (uint32_t k = 0; k < m; k++) o[off + k] = t[k];
+      off += m;
+    }
+    if (fl & DRP_F_VALUE) wave_copy(o + off, P.heap + s.value_off[i], s.value_len[i], lane);
+  }
+}
+
+// exclusive prefix of stats[i].frames (single block)
+__global__ __launch_bounds__(1024) void index_scan_kernel(const drp_stream_stats *stats, uint64_t count,
+                                                          uint64_t *base) {
+  __shared__ uint64_t part[1024];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint64_t c0 = 0; c0 < count; c0 += 1024) {
+    const uint64_t i = c0 + threadIdx.x;
+    const uint64_t v0 = i < count ? stats[i].frames : 0;
+    part[threadIdx.x] = v0;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+      uint64_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+    }
+    if (i < count) base[i] = carry + part[threadIdx.x] - v0;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += part[1023];
+    __syncthreads();
+  }
+}
+
+__global__ void stats_kernel(const drp_stream_result *res, const uint64_t *stream_off, uint64_t n,
+                             drp_stream_stats *stats) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  drp_stream_stats o;
+  o.frames = res[s].frames;
+  o.changes = res[s].changes;
+  o.blobs = res[s].blobs;
+  o.wire_bytes = res[s].consumed;
+  (void)stream_off;
+  stats[s] = o;
+}
+
+}  // namespace drp
+
+using namespace drp;
+
+extern "C" hipError_t drp_launch_encode(const EncodeParams *Pp, hipStream_t st) {
+  EncodeParams P = *Pp;
+  if (P.n == 0) return hipSuccess;
+  const uint64_t nblk = (P.n + SCAN_BLK - 1) / SCAN_BLK;
+  hipLaunchKernelGGL(enc_size_kernel, dim3((uint32_t)nblk), dim3(SCAN_BLK), 0, st, P);
+  hipLaunchKernelGGL(enc_blocksum_kernel, dim3(1), dim3(SCAN_BLK), 0, st, P, nblk);
+  hipLaunchKernelGGL(enc_addbase_kernel, dim3((uint32_t)nblk), dim3(SCAN_BLK), 0, st, P);
+  if (P.out) {
+    uint64_t waves = P.n < 65536 ? P.n : 65536;
+    uint32_t grid = (uint32_t)((waves * 64 + 255) / 256);
+    hipLaunchKernelGGL(enc_write_kernel, dim3(grid), dim3(256), 0, st, P);
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t drp_launch_index_scan(const drp_stream_stats *stats, uint64_t count, uint64_t *base,
+                                            hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(index_scan_kernel, dim3(1), dim3(1024), 0, st, stats, count, base);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t drp_launch_stats_from_results(const drp_stream_result *res, const uint64_t *stream_off,
+                                                    uint64_t nstreams, drp_stream_stats *stats, hipStream_t st) {
+  if (nstreams == 0) return hipSuccess;
+  const uint32_t grid = (uint32_t)((nstreams + 255) / 256);
+  hipLaunchKernelGGL(stats_kernel, dim3(grid), dim3(256), 0, st, res, stream_off, nstreams, stats);
+  return hipGetLastError();
+}

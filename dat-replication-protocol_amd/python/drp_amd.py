@@ -1,0 +1,231 @@
+"""ctypes binding of libdrp (include/drp.h) for the Python test suite and bench.py.
+
+The product host layer is the Node module in this package (index.js / decode.js /
+encode.js over the N-API addon); this module exposes the same C ABI to Python so the
+parity tests and the benchmark call exactly the code the addon calls. It loads the
+in-tree lib/libdrp.so and raises if it is missing: there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG, "lib", "libdrp.so")
+
+DRP_OK, DRP_E_INVAL, DRP_E_HIP, DRP_E_NOMEM, DRP_E_CAPACITY, DRP_E_NODEV = 0, -1, -2, -3, -4, -5
+TYPE_CHANGE, TYPE_BLOB, FRAME_CONT, FRAME_PARTIAL = 1, 2, 0x40, 0x80
+F_SUBSET, F_VALUE, F_BAD, F_MISSING = 1, 2, 4, 8
+ERR_NONE, ERR_TYPE, ERR_LEN, ERR_VARINT, ERR_CHANGE, ERR_REQUIRED = 0, 1, 2, 3, 4, 5
+TAIL_NONE, TAIL_HEADER, TAIL_CHANGE, TAIL_BLOB = 0, 1, 2, 3
+
+EXPORTS = [
+    "drp_abi_version", "drp_open", "drp_close", "drp_stream", "drp_synchronize",
+    "drp_last_timing", "drp_set_tile", "drp_set_strict", "drp_decode_scratch_bytes",
+    "drp_decode_device", "drp_decode_batch", "drp_encode_size", "drp_encode_device",
+    "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results",
+]
+
+P = C.c_void_p
+U64, U32 = C.c_uint64, C.c_uint32
+
+
+class Frames(C.Structure):
+    _fields_ = [("payload_off", P), ("payload_len", P), ("type", P)]
+
+
+class Changes(C.Structure):
+    _fields_ = [(k, P) for k in ["key_off", "key_len", "subset_off", "subset_len", "value_off",
+                                 "value_len", "change", "from_", "to", "flags"]]
+
+
+class ChangeSrc(C.Structure):
+    _fields_ = [(k, P) for k in ["key_off", "key_len", "subset_off", "subset_len", "value_off",
+                                 "value_len", "change", "from_", "to", "flags"]]
+
+
+class Carry(C.Structure):
+    _fields_ = [("blob_remaining", U64), ("consumed", U64), ("tail_kind", U32), ("reserved", U32)]
+
+
+class StreamResult(C.Structure):
+    _fields_ = [("frame_begin", U64), ("frames", U64), ("changes", U64), ("blobs", U64),
+                ("consumed", U64), ("blob_remaining", U64), ("err_frame", U64), ("err_code", U32),
+                ("err_detail", U32), ("tail_kind", U32), ("reserved", U32)]
+
+
+class StreamStats(C.Structure):
+    _fields_ = [("frames", U64), ("changes", U64), ("blobs", U64), ("wire_bytes", U64)]
+
+
+class Timing(C.Structure):
+    _fields_ = [("decode_ms", C.c_float), ("finalize_ms", C.c_float), ("total_ms", C.c_float),
+                ("strict_reruns", U32), ("reserved", U32)]
+
+
+_lib = None
+
+
+def lib():
+    """Load lib/libdrp.so (raises OSError if it was not built: no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"libdrp not built: {LIB_PATH} missing (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        L.drp_abi_version.restype = C.c_int
+        L.drp_open.argtypes = [C.c_int, C.POINTER(P)]
+        L.drp_close.argtypes = [P]
+        L.drp_close.restype = None
+        L.drp_stream.argtypes = [P]
+        L.drp_stream.restype = P
+        L.drp_synchronize.argtypes = [P]
+        L.drp_last_timing.argtypes = [P, C.POINTER(Timing)]
+        L.drp_set_tile.argtypes = [P, U32]
+        L.drp_set_strict.argtypes = [P, C.c_int]
+        L.drp_decode_scratch_bytes.argtypes = [P, U64, U64]
+        L.drp_decode_scratch_bytes.restype = U64
+        L.drp_decode_device.argtypes = [P, P, U64, P, P, U64, C.POINTER(Frames),
+                                        C.POINTER(Changes), U64, P]
+        L.drp_decode_batch.argtypes = [P, P, U64, C.POINTER(Carry), C.POINTER(Frames),
+                                       C.POINTER(Changes), U64, C.POINTER(U64), C.POINTER(U64),
+                                       C.POINTER(U32), C.POINTER(U32)]
+        L.drp_encode_size.argtypes = [P, C.POINTER(ChangeSrc), U64, C.POINTER(U64)]
+        L.drp_encode_device.argtypes = [P, C.POINTER(ChangeSrc), P, U64, P, P, U64]
+        L.drp_encode_batch.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, U64,
+                                       C.POINTER(U64)]
+        L.drp_index_scan.argtypes = [P, P, U64, P]
+        L.drp_stream_stats_from_results.argtypes = [P, P, P, U64, P]
+        for f in ["drp_open", "drp_synchronize", "drp_last_timing", "drp_set_tile",
+                  "drp_set_strict", "drp_decode_device", "drp_decode_batch", "drp_encode_size",
+                  "drp_encode_device", "drp_encode_batch", "drp_index_scan",
+                  "drp_stream_stats_from_results"]:
+            getattr(L, f).restype = C.c_int
+        _lib = L
+    return _lib
+
+
+class DrpError(RuntimeError):
+    def __init__(self, fn, rc):
+        super().__init__(f"{fn} failed with {rc}")
+        self.rc = rc
+
+
+def _chk(fn, rc):
+    if rc != DRP_OK:
+        raise DrpError(fn, rc)
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+COLS32 = ["key_off", "key_len", "subset_off", "subset_len", "value_off", "value_len"]
+COLS64 = ["change", "from", "to"]
+
+
+def alloc_host_outputs(cap):
+    o = {"payload_off": np.zeros(cap, np.uint64), "payload_len": np.zeros(cap, np.uint32),
+         "type": np.zeros(cap, np.uint8), "flags": np.zeros(cap, np.uint8)}
+    for k in COLS32:
+        o[k] = np.zeros(cap, np.uint32)
+    for k in COLS64:
+        o[k] = np.zeros(cap, np.uint64)
+    return o
+
+
+def _structs(o, ptr):
+    fr = Frames(ptr(o["payload_off"]), ptr(o["payload_len"]), ptr(o["type"]))
+    co = Changes(*[ptr(o[k]) for k in COLS32], ptr(o["change"]), ptr(o["from"]), ptr(o["to"]),
+                 ptr(o["flags"]))
+    return fr, co
+
+
+class Ctx:
+    """One libdrp context (device + HIP stream + scratch)."""
+
+    def __init__(self, device=0, tile=0):
+        self.L = lib()
+        h = P()
+        _chk("drp_open", self.L.drp_open(device, C.byref(h)))
+        self.h = h
+        if tile:
+            _chk("drp_set_tile", self.L.drp_set_tile(self.h, tile))
+
+    def close(self):
+        if self.h:
+            self.L.drp_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def stream(self):
+        return self.L.drp_stream(self.h)
+
+    def set_strict(self, on):
+        _chk("drp_set_strict", self.L.drp_set_strict(self.h, 1 if on else 0))
+
+    def set_tile(self, tile):
+        _chk("drp_set_tile", self.L.drp_set_tile(self.h, tile))
+
+    def timing(self):
+        t = Timing()
+        _chk("drp_last_timing", self.L.drp_last_timing(self.h, C.byref(t)))
+        return t
+
+    # ---- host-buffer batch decode (the N-API addon's path) -----------------------------
+    def decode_batch(self, wire, blob_remaining=0, cap=None):
+        w = np.frombuffer(bytes(wire), np.uint8) if not isinstance(wire, np.ndarray) else wire
+        n = int(w.size)
+        if cap is None:
+            cap = n // 2 + 2
+        o = alloc_host_outputs(cap)
+        fr, co = _structs(o, _p)
+        carry = Carry(blob_remaining, 0, 0, 0)
+        nf, ef, ec, ed = U64(), U64(), U32(), U32()
+        buf = w if n else np.zeros(16, np.uint8)
+        rc = self.L.drp_decode_batch(self.h, _p(buf), n, C.byref(carry), C.byref(fr), C.byref(co),
+                                     cap, C.byref(nf), C.byref(ef), C.byref(ec), C.byref(ed))
+        _chk("drp_decode_batch", rc)
+        nframes = int(nf.value)
+        keep = nframes + (1 if ec.value in (ERR_CHANGE, ERR_REQUIRED) else 0)
+        res = {k: v[:keep] for k, v in o.items()}
+        res.update(nframes=nframes, err_frame=int(ef.value), err_code=int(ec.value),
+                   err_detail=int(ed.value), consumed=int(carry.consumed),
+                   tail=int(carry.tail_kind), blob_remaining=int(carry.blob_remaining))
+        return res
+
+    # ---- device decode over torch tensors (bench path) --------------------------------
+    def decode_device(self, wire_t, stream_off_t, entry_t, outs, cap, results_t):
+        """All arguments are torch CUDA tensors (uint8 wire, int64 offsets); outs is a dict
+        of column tensors; results_t is a uint8 tensor of nstreams*sizeof(StreamResult)."""
+        tp = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
+        fr, co = _structs(outs, tp)
+        ns = stream_off_t.numel() - 1
+        rc = self.L.drp_decode_device(self.h, tp(wire_t), wire_t.numel(), tp(stream_off_t),
+                                      tp(entry_t), ns, C.byref(fr), C.byref(co), cap, tp(results_t))
+        _chk("drp_decode_device", rc)
+
+    # ---- encode -----------------------------------------------------------------------
+    def encode_batch(self, heap, cols):
+        n = len(cols["key_len"])
+        h = np.frombuffer(bytes(heap), np.uint8) if not isinstance(heap, np.ndarray) else heap
+        arrs = {k: np.ascontiguousarray(cols[k]) for k in
+                ["key_off", "key_len", "subset_off", "subset_len", "value_off", "value_len",
+                 "change", "from", "to", "flags"]}
+        src = ChangeSrc(*[_p(arrs[k]) for k in ["key_off", "key_len", "subset_off", "subset_len",
+                                                  "value_off", "value_len", "change", "from", "to",
+                                                  "flags"]])
+        total = U64()
+        _chk("drp_encode_size", self.L.drp_encode_size(self.h, C.byref(src), n, C.byref(total)))
+        out = np.zeros(max(16, int(total.value)), np.uint8)
+        written = U64()
+        hb = h if h.size else np.zeros(16, np.uint8)
+        _chk("drp_encode_batch", self.L.drp_encode_batch(self.h, C.byref(src), _p(hb), int(h.size), n,
+                                                         _p(out), int(total.value), C.byref(written)))
+        return out[:int(written.value)].tobytes()

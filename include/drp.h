@@ -56,6 +56,7 @@ extern "C" {
 #define DRP_F_SUBSET 0x01 /* optional string subset = 1 present */
 #define DRP_F_VALUE 0x02  /* optional bytes value = 6 present (value may be empty) */
 #define DRP_F_BAD 0x04    /* payload is not a well-formed Change (see err codes) */
+#define DRP_F_MISSING 0x08 /* with DRP_F_BAD: a required field (key/change/from/to) is missing */
 
 /* ---- stream error codes (first failing frame, see DESIGN.md "policy") ---- */
 #define DRP_ERR_NONE 0
@@ -158,15 +159,18 @@ int drp_set_strict(drp_ctx *ctx, int strict);
 uint64_t drp_decode_scratch_bytes(drp_ctx *ctx, uint64_t n, uint64_t nstreams);
 
 /* ---- decode -------------------------------------------------------------- */
-/* Decode `nstreams` independent streams laid end to end in `bytes` (device ptr).
+/* Decode `nstreams` independent streams laid end to end in `bytes` (device ptr, 16-byte
+ * aligned, `nbytes` long).
  * stream_off[nstreams+1] (device) gives stream s = bytes[stream_off[s], stream_off[s+1]);
  * entry[nstreams] (device, may be NULL = all zero) is the stream-relative offset of the
  * first frame header (skips a blob continuation). Frames of all streams are written to
  * `frames`/`cols` (device) in stream order; per-stream results go to results[] (device).
- * Asynchronous on drp_stream(ctx); capacity `cap` frames. */
-int drp_decode_device(drp_ctx *ctx, const uint8_t *bytes, const uint64_t *stream_off,
-                      const uint64_t *entry, uint64_t nstreams, const drp_frames *frames,
-                      const drp_changes *cols, uint64_t cap, drp_stream_result *results);
+ * Runs on drp_stream(ctx) and returns after completion (the speculation check needs the
+ * result); capacity `cap` frames (DRP_E_CAPACITY if more were found). */
+int drp_decode_device(drp_ctx *ctx, const uint8_t *bytes, uint64_t nbytes,
+                      const uint64_t *stream_off, const uint64_t *entry, uint64_t nstreams,
+                      const drp_frames *frames, const drp_changes *cols, uint64_t cap,
+                      drp_stream_result *results);
 
 /* Synchronous single-stream decode of one batch (host or device pointers).
  * carry->blob_remaining in: leading blob continuation; out: carry for the next batch.

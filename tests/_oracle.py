@@ -77,12 +77,14 @@ def alloc_outputs(cap):
     return o
 
 
-def decode_batch(wire: bytes, chunk=0, blob_remaining=0, cap=None):
+def decode_batch(wire, chunk=0, blob_remaining=0, cap=None, outs=None):
     """Run the decode.js restatement over `wire` written in `chunk`-byte pieces."""
+    if outs is not None:
+        cap = len(outs["type"])
     if cap is None:
         cap = len(wire) // 2 + 2
     w = np.frombuffer(wire, np.uint8) if len(wire) else np.zeros(1, np.uint8)
-    o = alloc_outputs(cap)
+    o = outs if outs is not None else alloc_outputs(cap)
     meta = np.zeros(9, np.uint64)
     p = lambda a: a.ctypes.data_as(C.c_void_p)
     rc = lib().oracle_decode_batch(p(w), len(wire), chunk, blob_remaining, cap, p(o["payload_off"]),

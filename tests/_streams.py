@@ -1,0 +1,93 @@
+"""Synthetic replication streams shaped like BASELINE.json's configs (seeded)."""
+import random  # noqa: F401  (callers pass random.Random instances)
+
+import numpy as np
+
+
+def varint(n):
+    out = bytearray()
+    while n >= 0x80:
+        out.append((n & 0x7F) | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def change_payload(key, change, frm, to, value=None, subset=None):
+    """protocol-buffers@2 field order (schema.proto:1-8): subset?, key, change, from, to, value?"""
+    p = bytearray()
+    if subset is not None:
+        p += b"\x0a" + varint(len(subset)) + subset
+    p += b"\x12" + varint(len(key)) + key
+    p += b"\x18" + varint(change) + b"\x20" + varint(frm) + b"\x28" + varint(to)
+    if value is not None:
+        p += b"\x32" + varint(len(value)) + value
+    return bytes(p)
+
+
+def frame(payload, typ=1):
+    return varint(len(payload) + 1) + bytes([typ]) + payload
+
+
+def c2_stream(nframes, seed=1, start=0):
+    """C2: exactly 86 B/frame: key = 10-digit i, change=(i%100)+1, from=i%128, to=(i+1)%128,
+    64 random value bytes."""
+    i = np.arange(start, start + nframes, dtype=np.int64)
+    a = np.zeros((nframes, 86), np.uint8)
+    a[:, 0] = 85
+    a[:, 1] = 1
+    a[:, 2] = 0x12
+    a[:, 3] = 10
+    for k in range(10):
+        a[:, 4 + k] = 48 + (i // 10 ** (9 - k)) % 10
+    a[:, 14] = 0x18
+    a[:, 15] = (i % 100) + 1
+    a[:, 16] = 0x20
+    a[:, 17] = i % 128
+    a[:, 18] = 0x28
+    a[:, 19] = (i + 1) % 128
+    a[:, 20] = 0x32
+    a[:, 21] = 64
+    rng = np.random.default_rng(seed)
+    a[:, 22:] = rng.integers(0, 256, size=(nframes, 64), dtype=np.uint8)
+    return a.reshape(-1)
+
+
+def random_stream(rng, nframes, blob_p=0.05, blob_max=3000, zero_p=0.01, big_key_p=0.05,
+                  subset_p=0.2, value_max=300):
+    parts = []
+    for _ in range(nframes):
+        r = rng.random()
+        if r < blob_p:
+            b = rng.randbytes(rng.randint(0, blob_max))
+            parts.append(frame(b, 2))
+        elif r < blob_p + zero_p:
+            parts.append(varint(rng.randint(0, 300)) + b"\x00")  # id 0: header only
+        else:
+            klen = rng.randint(128, 300) if rng.random() < big_key_p else rng.randint(0, 40)
+            key = bytes(rng.choice(b"abcdefghijklmnopqrstuvwxyz0123456789") for _ in range(klen))
+            val = None if rng.random() < 0.1 else rng.randbytes(rng.randint(0, value_max))
+            sub = rng.randbytes(rng.randint(0, 8)) if rng.random() < subset_p else None
+            nums = [rng.choice([rng.randint(0, 127), rng.randint(0, 2**21), rng.randint(0, 2**32 - 1),
+                                rng.randint(0, 2**53 - 1)]) for _ in range(3)]
+            parts.append(frame(change_payload(key, *nums, value=val, subset=sub)))
+    return b"".join(parts)
+
+
+def c5_stream(rng, nframes):
+    """C5-shaped: 4096 B values, key length U[1,256], change/from/to U[0,2^32)."""
+    parts = []
+    for _ in range(nframes):
+        key = rng.randbytes(rng.randint(1, 256))
+        nums = [rng.randint(0, 2**32 - 1) for _ in range(3)]
+        parts.append(frame(change_payload(key, *nums, value=rng.randbytes(4096))))
+    return b"".join(parts)
+
+
+def c3_stream(rng, units, frames_per_unit=1000, blob_len=1 << 20, seed=3):
+    """C3-shaped: repeating [frames_per_unit C2 frames + one blob of blob_len random bytes]."""
+    out = []
+    for u in range(units):
+        out.append(c2_stream(frames_per_unit, seed=seed + u, start=u * frames_per_unit).tobytes())
+        out.append(frame(rng.randbytes(blob_len), 2))
+    return b"".join(out)

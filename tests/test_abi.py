@@ -1,0 +1,53 @@
+"""CPU: libdrp.so loads and exports exactly the C ABI declared in include/drp.h."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "dat-replication-protocol_amd", "lib", "libdrp.so")
+HDR = os.path.join(ROOT, "include", "drp.h")
+
+
+def declared():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|uint64_t|void \*)\s*\*?\s*(drp_\w+)\(", src, re.M)))
+
+
+def test_header_declares_entry_points():
+    d = declared()
+    assert "drp_decode_batch" in d and "drp_encode_batch" in d and "drp_index_scan" in d
+    assert len(d) >= 15
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(LIB):
+        pytest.fail("lib/libdrp.so not built; run __graft_entry__.build()")
+    lib = ctypes.CDLL(LIB)
+    for name in declared():
+        assert hasattr(lib, name), name
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB], text=True)
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert set(declared()) <= exported
+
+
+def test_binding_matches_header():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "dat-replication-protocol_amd", "python"))
+    import drp_amd
+    assert sorted(drp_amd.EXPORTS) == declared()
+    assert drp_amd.lib().drp_abi_version() == 1
+
+
+def test_open_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "dat-replication-protocol_amd", "python"))
+    import drp_amd
+    with pytest.raises(drp_amd.DrpError) as e:
+        drp_amd.Ctx(0)
+    assert e.value.rc == drp_amd.DRP_E_NODEV

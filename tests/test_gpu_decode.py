@@ -1,0 +1,157 @@
+"""GPU parity: libdrp's gfx950 decode/encode vs the oracle (decode.js / encode.js
+restatement), bit-exact on every column.
+
+Run on an MI355X:  python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import _streams as S
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from _gpu import drp_amd
+    c = drp_amd.Ctx(0)
+    yield c
+    c.close()
+
+
+def test_golden_streams(ctx):
+    from _gpu import assert_same
+    vecs = json.load(open(os.path.join(GOLD, "streams.json")))["vectors"]
+    for v in vecs:
+        wire = bytes.fromhex(v["wire"])
+        assert_same(ctx.decode_batch(wire), O.decode_batch(wire), v["source"])
+
+
+@pytest.mark.parametrize("tile", [4096, 8192, 16384])
+@pytest.mark.parametrize("seed", range(4))
+def test_random_streams(ctx, tile, seed):
+    from _gpu import assert_same
+    ctx.set_tile(tile)
+    try:
+        rng = random.Random(seed)
+        wire = S.random_stream(rng, 3000)
+        wire = wire[:rng.randint(len(wire) // 2, len(wire))]
+        assert_same(ctx.decode_batch(wire), O.decode_batch(wire), f"seed{seed}/tile{tile}")
+    finally:
+        ctx.set_tile(0)
+
+
+def test_strict_equals_speculative(ctx):
+    from _gpu import assert_same
+    rng = random.Random(11)
+    wire = S.random_stream(rng, 4000, blob_p=0.1, blob_max=20000)
+    ref = O.decode_batch(wire)
+    ctx.set_strict(True)
+    try:
+        assert_same(ctx.decode_batch(wire), ref, "strict")
+    finally:
+        ctx.set_strict(False)
+    assert_same(ctx.decode_batch(wire), ref, "speculative")
+
+
+def test_c2_shape(ctx):
+    from _gpu import assert_same
+    wire = S.c2_stream(200_000, seed=5).tobytes()
+    g = ctx.decode_batch(wire)
+    assert g["nframes"] == 200_000 and g["err_code"] == 0 and g["tail"] == 0
+    assert_same(g, O.decode_batch(wire, chunk=65536), "c2")
+
+
+def test_c5_shape(ctx):
+    from _gpu import assert_same
+    wire = S.c5_stream(random.Random(9), 3000)
+    assert_same(ctx.decode_batch(wire), O.decode_batch(wire, chunk=65536), "c5")
+
+
+def test_c3_shape(ctx):
+    from _gpu import assert_same
+    wire = S.c3_stream(random.Random(4), 3, frames_per_unit=1000)
+    g = ctx.decode_batch(wire)
+    assert g["nframes"] == 3003
+    assert_same(g, O.decode_batch(wire, chunk=65536), "c3")
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_errors_and_tails(ctx, seed):
+    """Protocol errors (decode.js:159-161) and policy errors injected at frame boundaries."""
+    from _gpu import assert_same
+    rng = random.Random(100 + seed)
+    base = S.random_stream(rng, 800)
+    bad = [b"\x03\x07ab", b"\x00\x01", b"\x80" * 10 + b"\x01\x01", b"\x01\x01",
+           S.frame(b"\x12\x05k"), S.frame(b"\x12\x01k\x18\x01\x20\x02\x28\x03\x3b")]
+    for b in bad:
+        cut = rng.randint(0, len(base))
+        r0 = O.decode_batch(base[:cut])
+        if r0["tail"] == 3:
+            continue
+        cut = r0["consumed"]
+        wire = base[:cut] + b + base
+        assert_same(ctx.decode_batch(wire), O.decode_batch(wire), repr(b))
+
+
+def test_batches_with_carry(ctx):
+    """Split a stream into batches at random points and carry state like the JS layer."""
+    rng = random.Random(21)
+    wire = S.random_stream(rng, 2000, blob_p=0.1, blob_max=5000)
+    ref = O.decode_batch(wire)
+    pos, carry_bytes, blob_rem = 0, b"", 0
+    frames = []
+    while pos < len(wire):
+        step = rng.choice([1, 7, 100, 4096, 30000])
+        chunk = wire[pos:pos + step]
+        batch = carry_bytes + chunk
+        base = pos - len(carry_bytes)
+        g = ctx.decode_batch(batch, blob_remaining=blob_rem)
+        assert g["err_code"] == 0
+        for k in range(g["nframes"]):
+            frames.append((int(g["type"][k]) & 0x7F, base + int(g["payload_off"][k])))
+        carry_bytes = batch[g["consumed"]:] if g["tail"] in (1, 2) else b""
+        blob_rem = g["blob_remaining"]
+        pos += len(chunk)
+    merged = [(t & 0x3F, o) for t, o in frames if not (t & 0x40)]
+    exp = [(int(t) & 0x3F, int(o)) for t, o in zip(ref["type"], ref["payload_off"])]
+    assert merged == exp
+
+
+def _random_cols(rng, n):
+    heap = bytearray()
+    cols = {k: [] for k in ["key_off", "key_len", "subset_off", "subset_len", "value_off",
+                            "value_len", "change", "from", "to", "flags"]}
+    for _ in range(n):
+        for name, b in [("key", rng.randbytes(rng.randint(0, 300))),
+                        ("value", rng.randbytes(rng.choice([0, 3, 64, 4096]))),
+                        ("subset", rng.randbytes(rng.randint(0, 4)))]:
+            cols[name + "_off"].append(len(heap))
+            cols[name + "_len"].append(len(b))
+            heap += b
+        cols["change"].append(rng.randint(0, 2**53 - 1))
+        cols["from"].append(rng.randint(0, 2**32 - 1))
+        cols["to"].append(rng.randint(0, 127))
+        cols["flags"].append((1 if rng.random() < 0.3 else 0) | (2 if rng.random() < 0.9 else 0))
+    dt = {"key_off": np.uint64, "subset_off": np.uint64, "value_off": np.uint64,
+          "key_len": np.uint32, "subset_len": np.uint32, "value_len": np.uint32,
+          "change": np.uint64, "from": np.uint64, "to": np.uint64, "flags": np.uint8}
+    return bytes(heap), {k: np.array(v, dtype=dt[k]) for k, v in cols.items()}
+
+
+def test_encode_matches_oracle(ctx):
+    heap, c = _random_cols(random.Random(3), 3000)
+    g = ctx.encode_batch(heap, c)
+    assert g == O.encode_changes(heap, c)
+    d = ctx.decode_batch(g)
+    assert d["nframes"] == 3000 and d["err_code"] == 0
+    np.testing.assert_array_equal(d["change"], c["change"])
+    np.testing.assert_array_equal(d["from"], c["from"])
+    np.testing.assert_array_equal(d["flags"], c["flags"])
