@@ -285,34 +285,48 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
 
   TRACE("decode: nbytes=%llu ns=%llu B=%u grid=%u NT=%llu", (unsigned long long)nbytes,
         (unsigned long long)ns, c->B, grid, (unsigned long long)NT);
-  uint32_t *hdbg = nullptr;
-  if (trace_on()) {
-    CHK(hipStreamSynchronize(st));
-    uint64_t tp[2] = {0, 0};
-    CHK(hipMemcpy(tp, tile_prefix + ns, 8, hipMemcpyDeviceToHost));
-    TRACE("ntiles=%llu", (unsigned long long)tp[0]);
-    CHK(hipHostMalloc((void **)&hdbg, grid * 16, hipHostMallocMapped));
-    memset(hdbg, 0, grid * 16);
-    uint32_t *ddbg = nullptr;
-    CHK(hipHostGetDevicePointer((void **)&ddbg, hdbg, 0));
+  uint32_t *ddbg = nullptr;
+  if (getenv("DRP_WATCH")) {
+    CHK(hipMalloc((void **)&ddbg, grid * 16));
+    CHK(hipMemsetAsync(ddbg, 0, grid * 16, st));
     P.dbg = ddbg;
   }
   CHK(hipEventRecord(c->ev[1], st));
   CHK(drp_launch_decode(c->B, &P, grid, st));
   CHK(hipEventRecord(c->ev[2], st));
-  if (trace_on()) {
-    for (int it = 0; it < 100 && hipStreamQuery(st) == hipErrorNotReady; it++) {
+  if (getenv("DRP_WATCH")) {  // watchdog: snapshot device state of a stuck decode (no kernel change)
+    int it = 0;
+    for (; it < 100 && hipStreamQuery(st) == hipErrorNotReady; it++) {
       struct timespec ts = {0, 50 * 1000 * 1000};
       nanosleep(&ts, nullptr);
     }
-    for (uint32_t b = 0; b < grid && b < 64; b++)
-      TRACE("block %u: stage=%u tile=%u done=%x", b, hdbg[b * 4], hdbg[b * 4 + 1], hdbg[b * 4 + 2]);
     if (hipStreamQuery(st) == hipErrorNotReady) {
-      TRACE("decode kernel still running after 5 s: aborting");
+      hipStream_t s2;
+      hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+      const uint64_t nshow = NT < 8 ? NT : 8;
+      std::vector<uint64_t> recs(4 * nshow), tl(7 * nshow);
+      uint32_t h[4] = {0, 0, 0, 0};
+      hipMemcpyAsync(h, ctrl, 16, hipMemcpyDeviceToHost, s2);
+      for (int k = 0; k < 4; k++) hipMemcpyAsync(recs.data() + k * nshow, rec + k * NT, nshow * 8, hipMemcpyDeviceToHost, s2);
+      for (int k = 0; k < 7; k++) hipMemcpyAsync(tl.data() + k * nshow, tiles + k * NT, nshow * 8, hipMemcpyDeviceToHost, s2);
+      uint32_t *hd = nullptr;
+      hipHostMalloc((void **)&hd, grid * 16, hipHostMallocMapped);
+      uint32_t *hdd = nullptr;
+      hipHostGetDevicePointer((void **)&hdd, hd, 0);
+      if (ddbg) drp_launch_peek(ddbg, grid * 4, hdd, s2);
+      hipStreamSynchronize(s2);
+      for (uint32_t b = 0; b < grid && b < 32; b++)
+        fprintf(stderr, "[drp-watch] block %u: tile=%u stage=%u done=%x\n", b, hd[b * 4] >> 8, hd[b * 4] & 255, hd[b * 4 + 1]);
+      fprintf(stderr, "[drp-watch] stuck: counter=%u misspec=%u flags=%u\n", h[0], h[1], h[2]);
+      for (uint64_t t = 0; t < nshow; t++)
+        fprintf(stderr, "[drp-watch] tile %llu aggx=%llx inclx=%llx aggc=%llx inclc=%llx x=%llx exit=%llx base=%llu cnt=%llu\n",
+                (unsigned long long)t, (unsigned long long)recs[t], (unsigned long long)recs[nshow + t],
+                (unsigned long long)recs[2 * nshow + t], (unsigned long long)recs[3 * nshow + t],
+                (unsigned long long)tl[t], (unsigned long long)tl[nshow + t], (unsigned long long)tl[2 * nshow + t],
+                (unsigned long long)tl[3 * nshow + t]);
+      fflush(stderr);
       abort();
     }
-    TRACE("decode kernel done");
-    P.dbg = nullptr;
   }
 
   uint32_t reruns = 0;
@@ -358,7 +372,7 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
   c->timing.total_ms = ms;
   c->timing.finalize_ms = 0;
   c->timing.strict_reruns = reruns;
-  if (h[2] & 2u) return DRP_E_HIP;  // bounded wait expired inside the kernel
+  if (h[2] & 6u) return DRP_E_HIP;  // bounded wait expired / inconsistent walk inside the kernel
   if (h[2]) return DRP_E_CAPACITY;
   return DRP_OK;
 }

@@ -39,20 +39,100 @@ __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < 
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 
 #ifdef DRP_KERNEL_TRACE
-#define MARK(stage)                                                              \
-  do {                                                                           \
-    if (P.dbg && lane == 0) {                                                    \
-      volatile uint32_t *d_ = P.dbg + blockIdx.x * 4;                            \
-      d_[0] = (stage);                                                           \
-      d_[1] = (uint32_t)t;                                                       \
-      __threadfence_system();                                                    \
-    }                                                                            \
+#define MARK(stage)                                                                   \
+  do {                                                                                \
+    if (lane == 0 && P.dbg)                                                           \
+      __hip_atomic_store(P.dbg + blockIdx.x * 4, ((uint32_t)t << 8) | (uint32_t)(stage), \
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                  \
   } while (0)
 #else
 #define MARK(stage) \
   do {              \
   } while (0)
 #endif
+
+// Per-lane chain functions F(p) for the live positions of the lane's B bytes.
+struct LaneFns {
+  uint32_t meta[LMAX];  // tile-relative pos (14b) | nodes (9b) << 14 | delivered (9b) << 23
+  uint64_t ex[LMAX];    // first chain position past the lane, or MARK_TERM | terminal node
+  uint32_t cnt, ovf;
+};
+
+struct TileCtx {
+  const uint8_t *buf;  // LDS image of [A, A + TILE + HALO)
+  uint64_t A, ve, se;
+};
+
+// F(E) for a wave-uniform E inside the tile: read from the owning lane's list by readlane;
+// lanes that dropped positions (list full) are walked directly (uniform).
+template <int B>
+__device__ __forceinline__ void lane_lookup(const LaneFns &F, const TileCtx &T, uint64_t E, uint64_t &xo,
+                                            uint32_t &ndo, uint32_t &dlo) {
+  E = uniform64(E);
+  const uint32_t prel = (uint32_t)(E - T.A);
+  const uint32_t l = uniform32(prel / B);
+  bool hit = false;
+  uint64_t hx = 0;
+  uint32_t hm = 0;
+#pragma unroll
+  for (int k = 0; k < LMAX; k++)
+    if ((uint32_t)k < F.cnt && (F.meta[k] & 0x3FFFu) == prel) { hit = true; hx = F.ex[k]; hm = F.meta[k]; }
+  const uint64_t hb = __ballot(hit);
+  if ((hb >> l) & 1ull) {
+    xo = readlane64(hx, l);
+    const uint32_t m = readlane32(hm, l);
+    ndo = (m >> 14) & 0x1FFu;
+    dlo = m >> 23;
+    return;
+  }
+  if (readlane32(F.ovf, l)) {
+    const uint64_t le = umin64(T.A + (uint64_t)(l + 1) * B, T.ve);
+    uint64_t cur = E;
+    uint32_t nd = 0, dl = 0;
+    for (;;) {
+      Hdr h = parse_hdr_lds(T.buf, T.A, cur, T.se);
+      nd++;
+      if (h.kind != H_VALID) {
+        dl += (h.kind == H_TAIL_BLOB) ? 1u : 0u;
+        xo = MARK_TERM | cur;
+        break;
+      }
+      dl += h.id != 0 ? 1u : 0u;
+      cur = uniform64(h.succ);
+      if (cur >= le) { xo = cur; break; }
+    }
+    ndo = uniform32(nd);
+    dlo = uniform32(dl);
+    return;
+  }
+  xo = MARK_TERM | E;  // not a live header: the chain ends here (error or tail)
+  ndo = 1;
+  dlo = 0;
+}
+
+// Walk the frame chain from the wave-uniform entry E through the tile, one lane per step.
+// rec: lanes on the chain remember their entry (ent) and delivered count (mydl).
+template <int B>
+__device__ __forceinline__ uint64_t chain_walk(const LaneFns &F, const TileCtx &T, uint64_t E, bool rec,
+                                               uint32_t lane, int32_t &ent, uint32_t &mydl, uint32_t &nodes,
+                                               uint32_t &del) {
+  nodes = 0;
+  del = 0;
+  E = uniform64(E);
+  while (E < T.ve) {
+    uint64_t x;
+    uint32_t nd, dl;
+    lane_lookup<B>(F, T, E, x, nd, dl);
+    if (rec) {
+      const uint32_t l = uniform32((uint32_t)((E - T.A) / B));
+      if (lane == l) { ent = (int32_t)(E - T.A); mydl = dl; }
+    }
+    nodes = uniform32(nodes + nd);
+    del = uniform32(del + dl);
+    E = uniform64(x);
+  }
+  return E;
+}
 
 template <int B>
 __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
@@ -69,10 +149,12 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
 
   for (;;) {
-    uint32_t tt = 0;
-    if (lane == 0) tt = atomicAdd(P.counter, 1u);
-    const uint64_t t = readlane32(tt, 0);
-    if (t >= ntiles) break;
+    // Grab the next tile. Every lane executes the atomic (addend 1 on lane 0, 0 elsewhere):
+    // a grab under `if (lane == 0)` let the structurizer split this loop so that its inner
+    // back-edge skipped the grab and re-processed the same tile forever.
+    const uint32_t tt = atomicAdd(P.counter, lane == 0 ? 1u : 0u);
+    const uint64_t t = uniform32(readlane32(tt, 0));
+    if (t >= ntiles) return;
     MARK(1);
 
     // ---- which stream / tile ---------------------------------------------------------
@@ -123,11 +205,14 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
     // ---- lane-local live positions and chain functions ----------------------------------
     const uint64_t ls = A + (uint64_t)lane * B;
     const uint64_t lvs = umax64(ls, vs), lend = umin64(ls + B, ve);
-    uint32_t meta[LMAX];  // tile-relative pos (14b) | nodes (9b) << 14 | delivered (9b) << 23
-    uint64_t ex[LMAX];
+    LaneFns F;
 #pragma unroll
-    for (int k = 0; k < LMAX; k++) { meta[k] = 0; ex[k] = 0; }
-    uint32_t cnt = 0, ovf = 0;
+    for (int k = 0; k < LMAX; k++) { F.meta[k] = 0; F.ex[k] = 0; }
+    F.cnt = 0;
+    F.ovf = 0;
+    uint32_t &cnt = F.cnt, &ovf = F.ovf;
+    uint32_t *meta = F.meta;
+    uint64_t *ex = F.ex;
     if (lvs < lend) {
       uint64_t M[NW], S[NW];
 #pragma unroll
@@ -220,64 +305,7 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
     // ---- chain walker: one lane per step ---------------------------------------------
     int32_t ent = -1;     // this lane's entry (tile-relative) on the recorded chain
     uint32_t mydl = 0;    // delivered frames of the recorded chain inside this lane
-    auto lookup = [&](uint64_t E, uint64_t &xo, uint32_t &ndo, uint32_t &dlo) {
-      const uint32_t prel = (uint32_t)(E - A);
-      const uint32_t l = prel / B;
-      bool hit = false;
-      uint64_t hx = 0;
-      uint32_t hm = 0;
-#pragma unroll
-      for (int k = 0; k < LMAX; k++)
-        if ((uint32_t)k < cnt && (meta[k] & 0x3FFFu) == prel) { hit = true; hx = ex[k]; hm = meta[k]; }
-      const uint64_t hb = __ballot(hit);
-      if ((hb >> l) & 1ull) {
-        xo = readlane64(hx, l);
-        const uint32_t m = readlane32(hm, l);
-        ndo = (m >> 14) & 0x1FFu;
-        dlo = m >> 23;
-        return;
-      }
-      if (readlane32(ovf, l)) {  // lane l dropped positions: walk it directly (uniform)
-        const uint64_t le = umin64(A + (uint64_t)(l + 1) * B, ve);
-        uint64_t cur = E;
-        uint32_t nd = 0, dl = 0;
-        for (;;) {
-          Hdr h = parse_hdr_lds(buf, A, cur, se);
-          nd++;
-          if (h.kind != H_VALID) {
-            dl += (h.kind == H_TAIL_BLOB) ? 1u : 0u;
-            xo = MARK_TERM | cur;
-            break;
-          }
-          dl += h.id != 0 ? 1u : 0u;
-          cur = h.succ;
-          if (cur >= le) { xo = cur; break; }
-        }
-        ndo = nd;
-        dlo = dl;
-        return;
-      }
-      xo = MARK_TERM | E;  // not a live header: the chain ends here (error or tail)
-      ndo = 1;
-      dlo = 0;
-    };
-    auto walk = [&](uint64_t E, bool rec, uint32_t &nodes, uint32_t &del) -> uint64_t {
-      nodes = 0;
-      del = 0;
-      while (E < ve) {
-        uint64_t x;
-        uint32_t nd, dl;
-        lookup(E, x, nd, dl);
-        if (rec) {
-          const uint32_t l = (uint32_t)((E - A) / B);
-          if (lane == l) { ent = (int32_t)(E - A); mydl = dl; }
-        }
-        nodes += nd;
-        del += dl;
-        E = x;
-      }
-      return E;
-    };
+    const TileCtx TC{buf, A, ve, se};
     auto term_is_tail = [&](uint64_t x) -> bool {
       const uint64_t q = x & POS_MASK;
       if (q >= A + TILE) return false;
@@ -308,14 +336,14 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
         while (lanes_with && !done) {
           const uint32_t l = (uint32_t)__builtin_ctzll(lanes_with);
           lanes_with &= lanes_with - 1;
-          const uint32_t cl = readlane32(cnt, l);
+          const uint32_t cl = uniform32(readlane32(cnt, l));
           for (int32_t k = (int32_t)cl - 1; k >= 0 && !done; k--) {
             uint32_t msel = 0;
 #pragma unroll
             for (int kk = 0; kk < LMAX; kk++) if (kk == k) msel = meta[kk];
-            const uint64_t g = A + (readlane32(msel, l) & 0x3FFFu);
+            const uint64_t g = uniform64(A + (readlane32(msel, l) & 0x3FFFu));
             uint32_t nodes, del;
-            const uint64_t xe = walk(g, false, nodes, del);
+            const uint64_t xe = chain_walk<B>(F, TC, g, false, lane, ent, mydl, nodes, del);
             const bool survived = xe < MARK_TERM || (ve == se && term_is_tail(xe));
             if (survived) {
               bool validated = false;
@@ -373,13 +401,21 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
 
     MARK(5);
     // ---- exact chain through this tile ---------------------------------------------------
+    x = uniform64(x);
+    y = uniform64(y);
     uint64_t exit_t;
     uint32_t count_t = 0;
     if (x >= ve) {
       exit_t = x;  // pass-through (inside a long frame) or the chain already ended
     } else {
       uint32_t nodes;
-      exit_t = walk(x, true, nodes, count_t);
+      exit_t = chain_walk<B>(F, TC, x, true, lane, ent, mydl, nodes, count_t);
+    }
+    exit_t = uniform64(exit_t);
+    count_t = uniform32(count_t);
+    if (count_t > TILE) {  // impossible for a consistent walk: flag instead of looping on it
+      if (lane == 0) atomicOr(P.overflow, 4u);
+      count_t = 0;
     }
     if (published && y != MARK_NONE && exit_t != y && x < ve) {
       if (lane == 0) atomicMin(P.misspec, (uint32_t)t);
@@ -421,12 +457,15 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
         __builtin_amdgcn_s_sleep(1);
       }
     }
+    base = uniform64(base);
     if (lane == 0) st_agent(&P.inclc[t], base + count_t + 1);
     if (base + count_t > P.cap && lane == 0) atomicOr(P.overflow, 1u);
 
     MARK(7);
     // ---- emit frames ---------------------------------------------------------------------
+    MARK(10);
     const uint32_t myoff = wave_incl_scan32(mydl) - mydl;
+    MARK(11);
     uint32_t nch = 0, nbl = 0;
     uint64_t badf = ~0ull;
     for (uint32_t r0 = 0; r0 < count_t; r0 += FL_CAP) {
@@ -445,7 +484,9 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
           if (cur >= lend) break;
         }
       }
+      MARK(12);
       __syncthreads();
+      MARK(13);
       const uint32_t nr = (count_t - r0) < FL_CAP ? (count_t - r0) : FL_CAP;
       for (uint32_t k = lane; k < nr; k += 64) {
         const uint64_t pos = A + flist[k];
@@ -485,7 +526,9 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
           }
         }
       }
+      MARK(14);
       __syncthreads();
+      MARK(15);
     }
     MARK(8);
     nch = wave_sum32(nch);
@@ -509,11 +552,15 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
     MARK(9);
   }
 #ifdef DRP_KERNEL_TRACE
-  if (P.dbg && lane == 0) {
-    P.dbg[blockIdx.x * 4 + 2] = 0xD0E;
-    __threadfence_system();
-  }
+  if (P.dbg && lane == 0)
+    __hip_atomic_store(P.dbg + blockIdx.x * 4 + 1, 0xD0Eu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
+}
+
+// Debug: copy the agent-scope progress words of a running decode to host-mapped memory.
+__global__ void peek_kernel(const uint32_t *dbg, uint32_t n, uint32_t *out) {
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    out[i] = __hip_atomic_load(dbg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // tile_prefix[s] = number of tiles of streams < s; tile_prefix[nstreams] = total.
@@ -602,9 +649,10 @@ __global__ void finalize_kernel(const uint8_t *bytes, const uint64_t *stream_off
         r.consumed = se - so;
         r.blob_remaining = (q + h.vlen + h.L) - se;
         break;
-      case H_ERR_TYPE: r.err_code = DRP_ERR_TYPE; r.err_detail = h.id; r.err_frame = chain; r.consumed = q - so; break;
-      case H_ERR_LEN: r.err_code = DRP_ERR_LEN; r.err_detail = h.id; r.err_frame = chain; r.consumed = q - so; break;
-      default: r.err_code = DRP_ERR_VARINT; r.err_frame = chain; r.consumed = q - so; break;
+      // an error ends the stream: nothing is carried (consumed = stream length)
+      case H_ERR_TYPE: r.err_code = DRP_ERR_TYPE; r.err_detail = h.id; r.err_frame = chain; break;
+      case H_ERR_LEN: r.err_code = DRP_ERR_LEN; r.err_detail = h.id; r.err_frame = chain; break;
+      default: r.err_code = DRP_ERR_VARINT; r.err_frame = chain; break;
     }
   } else {
     r.consumed = (ex >= se ? se : ex) - so;
@@ -616,6 +664,7 @@ __global__ void finalize_kernel(const uint8_t *bytes, const uint64_t *stream_off
     r.err_detail = 0;
     r.tail_kind = DRP_TAIL_NONE;
     r.blob_remaining = 0;
+    r.consumed = se - so;
   }
   if (r.err_frame < frames) frames = r.err_frame;
   r.frames = frames;
@@ -656,6 +705,11 @@ extern "C" hipError_t drp_launch_decode(uint32_t B, const DecodeParams *P, uint3
     case 256: hipLaunchKernelGGL(decode_tiles<256>, dim3(grid), dim3(64), 0, st, *P); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t drp_launch_peek(const uint32_t *dbg, uint32_t n, uint32_t *out, hipStream_t st) {
+  hipLaunchKernelGGL(peek_kernel, dim3(1), dim3(256), 0, st, dbg, n, out);
   return hipGetLastError();
 }
 

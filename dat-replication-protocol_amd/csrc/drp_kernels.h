@@ -61,6 +61,7 @@ hipError_t drp_launch_finalize(const uint8_t *bytes, const uint64_t *stream_off,
                                const uint64_t *payload_err, const uint64_t *scount,
                                const uint8_t *type, const uint8_t *flags, uint64_t cap,
                                drp_stream_result *res, hipStream_t st);
+hipError_t drp_launch_peek(const uint32_t *dbg, uint32_t n, uint32_t *out, hipStream_t st);
 hipError_t drp_launch_encode(const drp::EncodeParams *P, hipStream_t st);
 hipError_t drp_launch_index_scan(const drp_stream_stats *stats, uint64_t count, uint64_t *base,
                                  hipStream_t st);

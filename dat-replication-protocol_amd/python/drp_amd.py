@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG, "lib", "libdrp.so")
+LIB_PATH = os.environ.get("DRP_LIB") or os.path.join(PKG, "lib", "libdrp.so")
 
 DRP_OK, DRP_E_INVAL, DRP_E_HIP, DRP_E_NOMEM, DRP_E_CAPACITY, DRP_E_NODEV = 0, -1, -2, -3, -4, -5
 TYPE_CHANGE, TYPE_BLOB, FRAME_CONT, FRAME_PARTIAL = 1, 2, 0x40, 0x80

@@ -152,7 +152,7 @@ ORACLE_API int oracle_change_decode(const uint8_t *p, uint64_t len, oracle_chang
   }
   if (found != 15) {
     c->err = DRP_ERR_REQUIRED;
-    c->flags |= DRP_F_BAD;
+    c->flags |= DRP_F_BAD | DRP_F_MISSING;
   }
   return (int)c->err;
 bad:
