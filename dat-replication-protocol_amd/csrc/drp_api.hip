@@ -1,9 +1,8 @@
 // drp_api.hip — the extern "C" boundary of libdrp (include/drp.h).
 //
-// Owns one HIP stream + scratch per device context, launches the decode / encode kernels,
-// and runs the speculation-repair loop of the decode: after a pass,
-// the first tile whose exact exit differs from its published speculative exit is given its
-// exact exit as an override and every tile from there on is re-run.
+// Owns one HIP stream + scratch per device context and launches the decode / encode
+// kernels. A decode is one pass: the kernel resolves every tile's entry exactly
+// (DESIGN.md §decode), so there is no host-side repair loop.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -76,9 +75,10 @@ struct drp_ctx {
   int device = 0;
   hipStream_t st = nullptr;
   hipEvent_t ev[4] = {};
-  uint32_t B = 128;
+  uint32_t B = 64;
   int strict = 0;
   int cus = 256;
+  uint32_t waves_per_cu = 16;
   DevBuf scratch, in_stage, out_stage, aux;
   drp_timing timing = {};
   std::vector<uint64_t> host_tmp;
@@ -115,7 +115,11 @@ int drp_open(int device, drp_ctx **out) {
   for (auto &e : c->ev) hipEventCreate(&e);
   if (const char *t = getenv("DRP_TILE")) {
     uint32_t tb = (uint32_t)atoi(t);
-    if (tb == 4096 || tb == 8192 || tb == 16384) c->B = tb / 64;
+    if (tb == 4096 || tb == 8192) c->B = tb / 64;
+  }
+  if (const char *w = getenv("DRP_WAVES_PER_CU")) {
+    int v = atoi(w);
+    if (v > 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
   }
   *out = c;
   return DRP_OK;
@@ -150,8 +154,8 @@ int drp_last_timing(drp_ctx *c, drp_timing *out) {
 
 int drp_set_tile(drp_ctx *c, uint32_t tile_bytes) {
   if (!c) return DRP_E_INVAL;
-  if (tile_bytes == 0) tile_bytes = 8192;
-  if (tile_bytes != 4096 && tile_bytes != 8192 && tile_bytes != 16384) return DRP_E_INVAL;
+  if (tile_bytes == 0) tile_bytes = 4096;
+  if (tile_bytes != 4096 && tile_bytes != 8192) return DRP_E_INVAL;
   c->B = tile_bytes / 64;
   return DRP_OK;
 }
@@ -165,7 +169,7 @@ int drp_set_strict(drp_ctx *c, int strict) {
 // scratch layout for a decode of `nbytes` over `ns` streams
 struct DecLayout {
   uint64_t ntiles_max;
-  size_t tile_prefix, rec, tiles, yover, perr, scount, ctrl, total;
+  size_t tile_prefix, rec, tiles, perr, scount, ctrl, total;
 };
 static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   DecLayout L;
@@ -173,9 +177,8 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.ntiles_max = nbytes / tile + 2 * ns + 2;
   size_t o = 0;
   L.tile_prefix = o; o += al((ns + 1) * 8);
-  L.rec = o; o += al(4 * L.ntiles_max * 8);    // aggx, inclx, aggc, inclc
-  L.tiles = o; o += al(7 * L.ntiles_max * 8);  // x, exit, base, count, nch, nbl, perr
-  L.yover = o; o += al(L.ntiles_max * 8);
+  L.rec = o; o += al(5 * L.ntiles_max * 8);    // ywd, aggv, inclx, aggc, inclc (zeroed per call)
+  L.tiles = o; o += al(3 * L.ntiles_max * 8);  // exit, base, count
   L.perr = o; o += al(ns * 8);
   L.scount = o; o += al(2 * ns * 8);
   L.ctrl = o; o += 256;
@@ -191,23 +194,6 @@ uint64_t drp_decode_scratch_bytes(drp_ctx *c, uint64_t n, uint64_t nstreams) {
 
 namespace {
 
-__global__ void recount_kernel(const uint64_t *tile_prefix, uint64_t nstreams, const uint64_t *tile_nch,
-                               const uint64_t *tile_nbl, const uint64_t *tile_perr, uint64_t *scount,
-                               uint64_t *perr) {
-  const uint64_t ntiles = tile_prefix[nstreams];
-  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ntiles;
-       t += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t lo = 0, hi = nstreams;
-    while (hi - lo > 1) {
-      uint64_t mid = (lo + hi) >> 1;
-      if (tile_prefix[mid] <= t) lo = mid; else hi = mid;
-    }
-    if (tile_nch[t]) atomicAdd((unsigned long long *)&scount[2 * lo], (unsigned long long)tile_nch[t]);
-    if (tile_nbl[t]) atomicAdd((unsigned long long *)&scount[2 * lo + 1], (unsigned long long)tile_nbl[t]);
-    if (tile_perr[t] != ~0ull) atomicMin((unsigned long long *)&perr[lo], (unsigned long long)tile_perr[t]);
-  }
-}
-
 int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
                const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
                uint64_t cap, drp_stream_result *res) {
@@ -219,20 +205,16 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
   uint64_t *tile_prefix = c->scratch.at<uint64_t>(L.tile_prefix);
   uint64_t *rec = c->scratch.at<uint64_t>(L.rec);
   uint64_t *tiles = c->scratch.at<uint64_t>(L.tiles);
-  uint64_t *yover = c->scratch.at<uint64_t>(L.yover);
   uint64_t *perr = c->scratch.at<uint64_t>(L.perr);
   uint64_t *scount = c->scratch.at<uint64_t>(L.scount);
-  uint32_t *ctrl = c->scratch.at<uint32_t>(L.ctrl);  // [0] counter [1] misspec [2] overflow
+  uint32_t *ctrl = c->scratch.at<uint32_t>(L.ctrl);  // [0] tile counter [1] overflow flags
 
   hipStream_t st = c->st;
   CHK(hipEventRecord(c->ev[0], st));
-  CHK(hipMemsetAsync(rec, 0, 4 * NT * 8, st));
-  CHK(hipMemsetAsync(yover, 0, NT * 8, st));
-  CHK(hipMemsetAsync(tiles + 6 * NT, 0xFF, NT * 8, st));  // tile_perr
+  CHK(hipMemsetAsync(rec, 0, 5 * NT * 8, st));
   CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
   CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
-  uint32_t ctrl_init[4] = {0, 0xFFFFFFFFu, 0, 0};
-  CHK(hipMemcpyAsync(ctrl, ctrl_init, 16, hipMemcpyHostToDevice, st));
+  CHK(hipMemsetAsync(ctrl, 0, 16, st));
   CHK(drp_launch_tile_prefix(c->B, stream_off, ns, tile_prefix, st));
 
   DecodeParams P;
@@ -257,113 +239,43 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
   P.to = co->to;
   P.flags = co->flags;
   P.cap = cap;
-  P.aggx = rec;
-  P.inclx = rec + NT;
-  P.aggc = rec + 2 * NT;
-  P.inclc = rec + 3 * NT;
-  P.tile_x = tiles;
-  P.tile_exit = tiles + NT;
-  P.tile_base = tiles + 2 * NT;
-  P.tile_count = tiles + 3 * NT;
-  P.tile_nch = tiles + 4 * NT;
-  P.tile_nbl = tiles + 5 * NT;
-  P.tile_perr = tiles + 6 * NT;
-  P.yover = yover;
+  P.ywd = rec;
+  P.aggv = rec + NT;
+  P.inclx = rec + 2 * NT;
+  P.aggc = rec + 3 * NT;
+  P.inclc = rec + 4 * NT;
+  P.tile_exit = tiles;
+  P.tile_base = tiles + NT;
+  P.tile_count = tiles + 2 * NT;
   P.payload_err = perr;
   P.scount = scount;
   P.counter = ctrl;
-  P.misspec = ctrl + 1;
-  P.overflow = ctrl + 2;
+  P.overflow = ctrl + 1;
   P.strict = (uint32_t)c->strict;
+  unsigned long long *dstats = nullptr;
+  if (getenv("DRP_STATS")) {
+    CHK(hipMalloc((void **)&dstats, 64 * 8));
+    CHK(hipMemsetAsync(dstats, 0, 64 * 8, st));
+    P.stats = dstats;
+  }
 
-  // persistent grid: enough single-wave blocks to fill every CU several times over
+  // persistent grid: single-wave blocks, several per CU; tiles are handed out in stream
+  // order by an atomic counter, so a tile only ever waits on tiles already taken.
   const uint32_t tile = 64u * c->B;
   const uint64_t tiles_needed = nbytes / tile + ns + 1;
-  uint32_t grid = (uint32_t)(c->cus * (c->B >= 256 ? 8 : 12));
+  uint32_t grid = (uint32_t)(c->cus * c->waves_per_cu);
   if (tiles_needed < grid) grid = (uint32_t)tiles_needed;
   if (grid == 0) grid = 1;
-
   TRACE("decode: nbytes=%llu ns=%llu B=%u grid=%u NT=%llu", (unsigned long long)nbytes,
         (unsigned long long)ns, c->B, grid, (unsigned long long)NT);
-  uint32_t *ddbg = nullptr;
-  if (getenv("DRP_WATCH")) {
-    CHK(hipMalloc((void **)&ddbg, grid * 16));
-    CHK(hipMemsetAsync(ddbg, 0, grid * 16, st));
-    P.dbg = ddbg;
-  }
   CHK(hipEventRecord(c->ev[1], st));
   CHK(drp_launch_decode(c->B, &P, grid, st));
   CHK(hipEventRecord(c->ev[2], st));
-  if (getenv("DRP_WATCH")) {  // watchdog: snapshot device state of a stuck decode (no kernel change)
-    int it = 0;
-    for (; it < 100 && hipStreamQuery(st) == hipErrorNotReady; it++) {
-      struct timespec ts = {0, 50 * 1000 * 1000};
-      nanosleep(&ts, nullptr);
-    }
-    if (hipStreamQuery(st) == hipErrorNotReady) {
-      hipStream_t s2;
-      hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
-      const uint64_t nshow = NT < 8 ? NT : 8;
-      std::vector<uint64_t> recs(4 * nshow), tl(7 * nshow);
-      uint32_t h[4] = {0, 0, 0, 0};
-      hipMemcpyAsync(h, ctrl, 16, hipMemcpyDeviceToHost, s2);
-      for (int k = 0; k < 4; k++) hipMemcpyAsync(recs.data() + k * nshow, rec + k * NT, nshow * 8, hipMemcpyDeviceToHost, s2);
-      for (int k = 0; k < 7; k++) hipMemcpyAsync(tl.data() + k * nshow, tiles + k * NT, nshow * 8, hipMemcpyDeviceToHost, s2);
-      uint32_t *hd = nullptr;
-      hipHostMalloc((void **)&hd, grid * 16, hipHostMallocMapped);
-      uint32_t *hdd = nullptr;
-      hipHostGetDevicePointer((void **)&hdd, hd, 0);
-      if (ddbg) drp_launch_peek(ddbg, grid * 4, hdd, s2);
-      hipStreamSynchronize(s2);
-      for (uint32_t b = 0; b < grid && b < 32; b++)
-        fprintf(stderr, "[drp-watch] block %u: tile=%u stage=%u done=%x\n", b, hd[b * 4] >> 8, hd[b * 4] & 255, hd[b * 4 + 1]);
-      fprintf(stderr, "[drp-watch] stuck: counter=%u misspec=%u flags=%u\n", h[0], h[1], h[2]);
-      for (uint64_t t = 0; t < nshow; t++)
-        fprintf(stderr, "[drp-watch] tile %llu aggx=%llx inclx=%llx aggc=%llx inclc=%llx x=%llx exit=%llx base=%llu cnt=%llu\n",
-                (unsigned long long)t, (unsigned long long)recs[t], (unsigned long long)recs[nshow + t],
-                (unsigned long long)recs[2 * nshow + t], (unsigned long long)recs[3 * nshow + t],
-                (unsigned long long)tl[t], (unsigned long long)tl[nshow + t], (unsigned long long)tl[2 * nshow + t],
-                (unsigned long long)tl[3 * nshow + t]);
-      fflush(stderr);
-      abort();
-    }
-  }
-
-  uint32_t reruns = 0;
-  bool repaired = false;
-  for (;;) {
-    uint32_t h[4];
-    CHK(hipMemcpyAsync(h, ctrl, 16, hipMemcpyDeviceToHost, st));
-    CHK(hipStreamSynchronize(st));
-    TRACE("pass done: counter=%u misspec=%u flags=%u", h[0], h[1], h[2]);
-    if (h[1] == 0xFFFFFFFFu || (h[2] & 2u)) break;
-    // speculation failed at tile m: give it its exact exit and re-run tiles >= m
-    const uint64_t m = h[1];
-    repaired = true;
-    reruns++;
-    if (reruns > 64 && !P.strict) P.strict = 1;  // pathological input: no speculation
-    uint64_t ex_m = 0;
-    CHK(hipMemcpyAsync(&ex_m, P.tile_exit + m, 8, hipMemcpyDeviceToHost, st));
-    CHK(hipStreamSynchronize(st));
-    const uint64_t ov = ex_m + 1;
-    CHK(hipMemcpyAsync(yover + m, &ov, 8, hipMemcpyHostToDevice, st));
-    for (int k = 0; k < 4; k++) CHK(hipMemsetAsync(rec + k * NT + m, 0, (NT - m) * 8, st));
-    uint32_t ctrl_re[4] = {(uint32_t)m, 0xFFFFFFFFu, 0, 0};
-    CHK(hipMemcpyAsync(ctrl, ctrl_re, 12, hipMemcpyHostToDevice, st));
-    CHK(drp_launch_decode(c->B, &P, grid, st));
-  }
-  if (repaired) {
-    CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
-    CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
-    hipLaunchKernelGGL(recount_kernel, dim3(256), dim3(256), 0, st, tile_prefix, ns, P.tile_nch, P.tile_nbl,
-                       P.tile_perr, scount, perr);
-    CHK(hipGetLastError());
-  }
   CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
                           scount, fr->type, co->flags, cap, res, st));
   CHK(hipEventRecord(c->ev[3], st));
-  uint32_t h[4];
-  CHK(hipMemcpyAsync(h, ctrl, 16, hipMemcpyDeviceToHost, st));
+  uint32_t h[2];
+  CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
   float ms = 0;
   hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
@@ -371,9 +283,21 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
   hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
   c->timing.total_ms = ms;
   c->timing.finalize_ms = 0;
-  c->timing.strict_reruns = reruns;
-  if (h[2] & 6u) return DRP_E_HIP;  // bounded wait expired / inconsistent walk inside the kernel
-  if (h[2]) return DRP_E_CAPACITY;
+  c->timing.strict_reruns = 0;
+  TRACE("decode done: tiles=%u flags=%u", h[0], h[1]);
+  if (dstats) {
+    unsigned long long hs[32];
+    CHK(hipMemcpy(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost));
+    static const char *nm[] = {"lb_iters", "lb_noincl", "lb_noagg", "lb_keymiss", "lb_vunk", "lb_ok0", "lb_okn",
+                               "y_spins", "serial", "cnt_spins", "y_count", "agg_unk", "tiles", "pass", "ovf_pos",
+                               "t_grab", "t_stage", "t_dp", "t_y", "t_lb", "t_path", "t_cnt", "t_emit"};
+    fprintf(stderr, "[drp-stats]");
+    for (int i = 0; i < 23; i++) fprintf(stderr, " %s=%llu", nm[i], hs[i]);
+    fprintf(stderr, " decode_ms=%.3f\n", c->timing.decode_ms);
+    hipFree(dstats);
+  }
+  if (h[1] & 6u) return DRP_E_HIP;  // bounded wait expired / inconsistent walk inside the kernel
+  if (h[1]) return DRP_E_CAPACITY;
   return DRP_OK;
 }
 

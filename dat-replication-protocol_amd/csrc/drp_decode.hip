@@ -3,168 +3,161 @@
 // (Decoder._consume / _onheader / _onchangedata / _onchangeend / _onblobdata,
 // decode.js:144-262) and messages.Change.decode (messages/index.js:5).
 //
-// Algorithm:
-//   * One wave (64 lanes) owns one tile of 64*B stream bytes, staged once into LDS.
-//     Tiles are handed out by an atomic counter, so every tile a wave waits on has
-//     already been taken by a running wave (no deadlock, any grid size).
-//   * Lane l owns B bytes. It finds every position whose bytes form a complete header
-//     with id <= 2 (bit masks over its bytes), and for each such "live" position computes
-//     the lane-local chain function F(p) = (first chain position past the lane, #nodes,
-//     #delivered frames) by one descending pass.
-//   * A frame chain through the tile is then walked one LANE per step (<= 64 steps),
-//     with the per-lane functions read by readlane.
-//   * The tile's entry depends on the previous tile's chain (frames have no sync marker).
-//     Each tile publishes a speculative exit y (the chain of its best-evidenced candidate
-//     entry) and looks back over predecessors: x_t = f_{t-1}(...f_k(x_k)) with
-//     f_k(x) = x >= end_k ? x : y_k. With x known it walks its exact chain, checks it
-//     against its own y (a mismatch is recorded; the host re-runs from the first such
-//     tile with the corrected exit), publishes its exact exit and its frame count, and a
-//     second look-back over counts gives its first output slot.
-//   * Frames are listed in LDS and decoded round-robin over lanes, so each column store
-//     of a wave is one contiguous run.
+// One wave owns one tile of 64*B stream bytes (B bytes per lane), read from HBM once and
+// kept in LDS. Frames carry no sync marker, so a tile cannot know where its first frame
+// starts until its predecessors are resolved; the kernel therefore splits the work into
+// an entry-independent part (almost all of it) and an O(1) entry-dependent part:
+//
+//   1. live mask   Every byte position whose bytes could start a header with id <= 2
+//                  (varint terminator followed by a byte <= 2) — bit-parallel per lane.
+//   2. lane DP     Descending over its live positions, each lane sorts every position of
+//                  its B bytes into: dead (the chain from it ends inside the lane: error,
+//                  tail or non-header) or one of <= 3 "classes" = the distinct positions at
+//                  which chains leave the lane. One header parse per live position.
+//   3. lane graph  Node (lane, class) -> node holding that class exit in a later lane (or
+//                  EXIT / DEAD / UNKNOWN); 6 rounds of pointer doubling in LDS give every
+//                  node its tile exit. The tile's transfer function is now known for EVERY
+//                  entry position.
+//   4. look-back  Tile t publishes Y_t (the distinct exits landing in tile t+1) as soon as
+//                  step 3 is done, then agg_t = f_t evaluated on Y_{t-1} (exact, no
+//                  speculation). Tile t finds its entry x_t by reading predecessors'
+//                  inclusive exits / aggs and composing forward; a miss waits for that
+//                  predecessor's exact inclusive exit.
+//   5. emit        Marking over the doubling levels gives each lane its entry on the true
+//                  chain; lanes walk their own bytes, a second (count) look-back gives the
+//                  output slot, and frames are decoded from LDS into the SoA columns.
+//
+// DESIGN.md §decode has the derivation and the cost model.
 #include "drp_device.h"
 #include "drp_kernels.h"
 
 namespace drp {
 
-constexpr int LMAX = 8;      // live positions per lane kept in registers
-constexpr int CMAX = 48;     // speculative candidates tried per tile
-constexpr uint32_t EVID = 8; // chain nodes that count as strong evidence
-constexpr uint32_t HALO = 256;
-constexpr uint32_t SPIN_MAX = 1u << 22;  // bounded waits: ~seconds, then flag and give up
+constexpr int NC = 3;                 // surviving exit classes per lane
+constexpr uint32_t N_DEAD = 3;        // special graph nodes (class slot 3 of lanes 0 / 1)
+constexpr uint32_t N_UNK = 7;
+constexpr int LEV = 7;                // doubling levels 0..6 (2^6 = 64 lane hops)
+constexpr uint32_t HALO = 512;        // bytes past the tile kept in LDS (straddling frames)
+constexpr uint32_t SPIN_MAX = 1u << 22;
+constexpr uint64_t READY = 1ull << 63;
+constexpr uint32_t V_UNK = 0xFFFFu;   // agg value: not expressible -> wait for inclusive
 
-
+// Optional per-wave event counters and phase cycle counts (DRP_STATS=1): accumulated in
+// registers and flushed with one atomic per counter when the wave exits.
+enum : uint32_t {
+  ST_LB_ITERS = 0, ST_LB_NOINCL, ST_LB_NOAGG, ST_LB_KEYMISS, ST_LB_VUNK, ST_LB_OK0, ST_LB_OKN,
+  ST_Y_SPINS, ST_SERIAL, ST_CNT_SPINS, ST_Y_COUNT, ST_AGG_UNK, ST_TILES, ST_PASS, ST_OVF_LANES,
+  ST_T_GRAB, ST_T_STAGE, ST_T_DP, ST_T_Y, ST_T_LB, ST_T_PATH, ST_T_CNT, ST_T_EMIT,
+  ST_NSTATS
+};
+#define STAT(k, v)                        \
+  do {                                    \
+    if (P.stats) acc[k] += (uint64_t)(v); \
+  } while (0)
+#define TMARK(k)                             \
+  do {                                       \
+    if (P.stats) {                           \
+      const uint64_t now_ = clock64();       \
+      acc[k] += now_ - tclk;                 \
+      tclk = now_;                           \
+    }                                        \
+  } while (0)
 
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 
-#ifdef DRP_KERNEL_TRACE
-#define MARK(stage)                                                                   \
-  do {                                                                                \
-    if (lane == 0 && P.dbg)                                                           \
-      __hip_atomic_store(P.dbg + blockIdx.x * 4, ((uint32_t)t << 8) | (uint32_t)(stage), \
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                  \
-  } while (0)
-#else
-#define MARK(stage) \
-  do {              \
-  } while (0)
-#endif
-
-// Per-lane chain functions F(p) for the live positions of the lane's B bytes.
-struct LaneFns {
-  uint32_t meta[LMAX];  // tile-relative pos (14b) | nodes (9b) << 14 | delivered (9b) << 23
-  uint64_t ex[LMAX];    // first chain position past the lane, or MARK_TERM | terminal node
-  uint32_t cnt, ovf;
-};
-
-struct TileCtx {
-  const uint8_t *buf;  // LDS image of [A, A + TILE + HALO)
-  uint64_t A, ve, se;
-};
-
-// F(E) for a wave-uniform E inside the tile: read from the owning lane's list by readlane;
-// lanes that dropped positions (list full) are walked directly (uniform).
-template <int B>
-__device__ __forceinline__ void lane_lookup(const LaneFns &F, const TileCtx &T, uint64_t E, uint64_t &xo,
-                                            uint32_t &ndo, uint32_t &dlo) {
-  E = uniform64(E);
-  const uint32_t prel = (uint32_t)(E - T.A);
-  const uint32_t l = uniform32(prel / B);
-  bool hit = false;
-  uint64_t hx = 0;
-  uint32_t hm = 0;
+// ---- bit arrays of NW 64-bit words (lane-private, fully unrolled) ---------------------
+template <int NW>
+__device__ __forceinline__ bool tbit(const uint64_t (&m)[NW], uint32_t o) {
+  uint64_t w = m[0];
 #pragma unroll
-  for (int k = 0; k < LMAX; k++)
-    if ((uint32_t)k < F.cnt && (F.meta[k] & 0x3FFFu) == prel) { hit = true; hx = F.ex[k]; hm = F.meta[k]; }
-  const uint64_t hb = __ballot(hit);
-  if ((hb >> l) & 1ull) {
-    xo = readlane64(hx, l);
-    const uint32_t m = readlane32(hm, l);
-    ndo = (m >> 14) & 0x1FFu;
-    dlo = m >> 23;
-    return;
-  }
-  if (readlane32(F.ovf, l)) {
-    const uint64_t le = umin64(T.A + (uint64_t)(l + 1) * B, T.ve);
-    uint64_t cur = E;
-    uint32_t nd = 0, dl = 0;
-    for (;;) {
-      Hdr h = parse_hdr_lds(T.buf, T.A, cur, T.se);
-      nd++;
-      if (h.kind != H_VALID) {
-        dl += (h.kind == H_TAIL_BLOB) ? 1u : 0u;
-        xo = MARK_TERM | cur;
-        break;
-      }
-      dl += h.id != 0 ? 1u : 0u;
-      cur = uniform64(h.succ);
-      if (cur >= le) { xo = cur; break; }
-    }
-    ndo = uniform32(nd);
-    dlo = uniform32(dl);
-    return;
-  }
-  xo = MARK_TERM | E;  // not a live header: the chain ends here (error or tail)
-  ndo = 1;
-  dlo = 0;
+  for (int i = 1; i < NW; i++)
+    if ((o >> 6) == (uint32_t)i) w = m[i];
+  return (w >> (o & 63)) & 1ull;
+}
+template <int NW>
+__device__ __forceinline__ void sbit(uint64_t (&m)[NW], uint32_t o) {
+#pragma unroll
+  for (int i = 0; i < NW; i++)
+    if ((o >> 6) == (uint32_t)i) m[i] |= 1ull << (o & 63);
+}
+// right shift (toward lower positions) of an N-word array by d < 64
+template <int N>
+__device__ __forceinline__ void shr(const uint64_t (&a)[N], uint32_t d, uint64_t (&o)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; i++) o[i] = (a[i] >> d) | (i + 1 < N ? (a[i + 1] << (64 - d)) : 0ull);
 }
 
-// Walk the frame chain from the wave-uniform entry E through the tile, one lane per step.
-// rec: lanes on the chain remember their entry (ent) and delivered count (mydl).
-template <int B>
-__device__ __forceinline__ uint64_t chain_walk(const LaneFns &F, const TileCtx &T, uint64_t E, bool rec,
-                                               uint32_t lane, int32_t &ent, uint32_t &mydl, uint32_t &nodes,
-                                               uint32_t &del) {
-  nodes = 0;
-  del = 0;
-  E = uniform64(E);
-  while (E < T.ve) {
-    uint64_t x;
-    uint32_t nd, dl;
-    lane_lookup<B>(F, T, E, x, nd, dl);
-    if (rec) {
-      const uint32_t l = uniform32((uint32_t)((E - T.A) / B));
-      if (lane == l) { ent = (int32_t)(E - T.A); mydl = dl; }
-    }
-    nodes = uniform32(nodes + nd);
-    del = uniform32(del + dl);
-    E = uniform64(x);
-  }
-  return E;
+// bit k of the result = MSB of byte k of x
+__device__ __forceinline__ uint32_t msb4(uint32_t x) {
+  return (((x >> 7) & 0x01010101u) * 0x01020408u) >> 24;
+}
+// MSB of each byte set iff that byte <= 2
+__device__ __forceinline__ uint32_t le2(uint32_t x) {
+  return ~(((x & 0x7F7F7F7Fu) + 0x7D7D7D7Du) | x) & 0x80808080u;
+}
+__device__ __forceinline__ void gather16(const uint4 v, uint32_t &m16, uint32_t &s16) {
+  m16 = msb4(v.x) | (msb4(v.y) << 4) | (msb4(v.z) << 8) | (msb4(v.w) << 12);
+  s16 = msb4(le2(v.x)) | (msb4(le2(v.y)) << 4) | (msb4(le2(v.z)) << 8) | (msb4(le2(v.w)) << 12);
+}
+
+__device__ __forceinline__ uint4 load16(const uint8_t *g, uint64_t p, uint64_t se) {
+  if (p + 16 <= se) return *reinterpret_cast<const uint4 *>(g + p);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (uint32_t k = 0; k < 16; k++)
+    if (p + k < se) w[k >> 2] |= (uint32_t)g[p + k] << (8 * (k & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 template <int B>
 __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
   constexpr uint32_t TILE = 64u * B;
+  constexpr int NW = B / 64;           // mask words per lane
+  constexpr int NV = B / 16;           // 16-byte loads per lane
   constexpr uint32_t LBUF = TILE + HALO + 32;
-  constexpr uint32_t FL_CAP = TILE / 8;
-  constexpr int NW = (B + 16 + 63) / 64;  // 64-bit mask words per lane
+  constexpr int NM = NC + 2;           // per lane: class masks, dead mask, live mask
   __shared__ __attribute__((aligned(16))) uint8_t buf[LBUF];
-  constexpr uint32_t NBW = (TILE + HALO) / 64 + 2;  // bitmap words (+2 zero pad)
-  __shared__ uint16_t flist[FL_CAP];
-  __shared__ uint64_t mbits[NBW], sbits[NBW];
+  __shared__ uint64_t lm[64 * NM * NW];
+  __shared__ uint64_t exv[256];
+  __shared__ uint8_t jmp[LEV][256];
+  __shared__ uint8_t mark[256];
+  __shared__ int32_t entry[64];
 
   const uint32_t lane = lane_id();
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
 
+  // lm accessors: lane m, mask k (0..NC-1 class, NC dead, NC+1 live), word w
+  auto LM = [&](uint32_t m, uint32_t k, uint32_t w) -> uint64_t & { return lm[(m * NM + k) * NW + w]; };
+
+  uint64_t acc[ST_NSTATS];
+#pragma unroll
+  for (int i = 0; i < (int)ST_NSTATS; i++) acc[i] = 0;
+  uint64_t tclk = P.stats ? clock64() : 0;
+  uint32_t novf = 0;
+
   for (;;) {
-    // Grab the next tile. Every lane executes the atomic (addend 1 on lane 0, 0 elsewhere):
-    // a grab under `if (lane == 0)` let the structurizer split this loop so that its inner
-    // back-edge skipped the grab and re-processed the same tile forever.
+    // Every lane executes the atomic (addend 1 on lane 0): a grab under `if (lane == 0)`
+    // let the structurizer split this loop so its inner back-edge skipped the grab.
     const uint32_t tt = atomicAdd(P.counter, lane == 0 ? 1u : 0u);
     const uint64_t t = uniform32(readlane32(tt, 0));
-    if (t >= ntiles) return;
-    MARK(1);
+    if (t >= ntiles) {
+      if (P.stats) {
+        acc[ST_OVF_LANES] = wave_sum32(novf);
+        if (lane == 0)
+#pragma unroll
+          for (int i = 0; i < (int)ST_NSTATS; i++) atomicAdd(P.stats + i, (unsigned long long)acc[i]);
+      }
+      return;
+    }
 
     // ---- which stream / tile ---------------------------------------------------------
     uint64_t lo = 0, hi = P.nstreams;
     while (hi - lo > 1) {
-      uint64_t mid = (lo + hi) >> 1;
+      const uint64_t mid = (lo + hi) >> 1;
       if (P.tile_prefix[mid] <= t) lo = mid; else hi = mid;
     }
     const uint64_t s = uniform64(lo);
-    const uint64_t tf = P.tile_prefix[s];
+    const uint64_t tf = P.tile_prefix[s], tl = P.tile_prefix[s + 1];
     const uint64_t so = P.stream_off[s], se = P.stream_off[s + 1];
     const uint64_t A0 = so & ~(uint64_t)(TILE - 1);
     const uint64_t A = A0 + (t - tf) * TILE;
@@ -172,339 +165,530 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
     const bool first = (t == tf);
     const uint64_t e0 = so + (P.entry ? P.entry[s] : 0ull);
 
-    // ---- stage the tile (+halo) in LDS; build MSB / (byte <= 2) bitmaps on the way -------
-    for (uint32_t i = lane * 16; i < TILE + HALO; i += 64 * 16) {
-      const uint64_t p = A + i;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (p + 16 <= se) {
-        v = *reinterpret_cast<const uint4 *>(P.bytes + p);
-      } else if (p < se) {
-        uint32_t w[4] = {0, 0, 0, 0};
-        for (uint32_t k = 0; k < 16 && p + k < se; k++) w[k >> 2] |= (uint32_t)P.bytes[p + k] << (8 * (k & 3));
-        v = make_uint4(w[0], w[1], w[2], w[3]);
-      }
-      *reinterpret_cast<uint4 *>(buf + i) = v;
-      const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
-      uint32_t hm16 = 0, sm16 = 0;
+    TMARK(ST_T_GRAB);
+    __syncthreads();  // previous tile's LDS reads are done
+    // ---- stage: own B bytes (+ the halo) into LDS --------------------------------------
+    const uint64_t lb = A + (uint64_t)lane * B;
+    uint4 v[NV];
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t x = xs[j];
-        const uint32_t hm = (x >> 7) & 0x01010101u;                                       // MSB set
-        const uint32_t sm = (~((x & 0x7F7F7F7Fu) + 0x7D7D7D7Du) & ~x & 0x80808080u) >> 7;  // byte <= 2
-        hm16 |= (((hm * 0x01020408u) >> 24) & 0xFu) << (4 * j);
-        sm16 |= (((sm * 0x01020408u) >> 24) & 0xFu) << (4 * j);
-      }
-      reinterpret_cast<uint16_t *>(mbits)[i / 16] = (uint16_t)hm16;
-      reinterpret_cast<uint16_t *>(sbits)[i / 16] = (uint16_t)sm16;
-    }
+    for (int k = 0; k < NV; k++) v[k] = load16(P.bytes, lb + 16 * k, se);
+#pragma unroll
+    for (int k = 0; k < NV; k++) *reinterpret_cast<uint4 *>(buf + lane * B + 16 * k) = v[k];
+    if (lane < HALO / 16)
+      *reinterpret_cast<uint4 *>(buf + TILE + lane * 16) = load16(P.bytes, A + TILE + lane * 16, se);
     if (lane < 2) *reinterpret_cast<uint4 *>(buf + TILE + HALO + lane * 16) = make_uint4(0, 0, 0, 0);
-    if (lane < 2) { mbits[NBW - 2 + lane] = 0; sbits[NBW - 2 + lane] = 0; }
+    entry[lane] = -1;
     __syncthreads();
 
-    MARK(2);
-    // ---- lane-local live positions and chain functions ----------------------------------
-    const uint64_t ls = A + (uint64_t)lane * B;
-    const uint64_t lvs = umax64(ls, vs), lend = umin64(ls + B, ve);
-    LaneFns F;
+    // ---- 1. live mask over the lane's B bytes ----------------------------------------------
+    const uint32_t plo = (uint32_t)(vs > lb ? umin64(vs - lb, B) : 0);
+    const uint32_t phi = (uint32_t)(ve > lb ? umin64(ve - lb, B) : 0);
+    const uint64_t lhi = lb + phi;  // lane's valid end (absolute)
+    uint64_t lvm[NW];
+    {
+      uint64_t M[NW + 1], S[NW + 1];
 #pragma unroll
-    for (int k = 0; k < LMAX; k++) { F.meta[k] = 0; F.ex[k] = 0; }
-    F.cnt = 0;
-    F.ovf = 0;
-    uint32_t &cnt = F.cnt, &ovf = F.ovf;
-    uint32_t *meta = F.meta;
-    uint64_t *ex = F.ex;
-    if (lvs < lend) {
-      uint64_t M[NW], S[NW];
+      for (int w = 0; w <= NW; w++) { M[w] = 0; S[w] = 0; }
 #pragma unroll
-      for (int w = 0; w < NW; w++) {
-        M[w] = mbits[lane * (B / 64) + w];
-        S[w] = sbits[lane * (B / 64) + w];
+      for (int k = 0; k < NV; k++) {
+        uint32_t m16, s16;
+        gather16(v[k], m16, s16);
+        M[k >> 2] |= (uint64_t)m16 << (16 * (k & 3));
+        S[k >> 2] |= (uint64_t)s16 << (16 * (k & 3));
       }
-      // terminator t: MSB clear at t and byte t+1 <= 2  (bit t of ~M & (S >> 1))
-      uint64_t T[NW];
-#pragma unroll
-      for (int w = 0; w < NW; w++) {
-        uint64_t sh = (S[w] >> 1) | (w + 1 < NW ? (S[w + 1] << 63) : 0ull);
-        T[w] = ~M[w] & sh;
+      {
+        const uint4 x = *reinterpret_cast<const uint4 *>(buf + lane * B + B);
+        uint32_t m16, s16;
+        gather16(x, m16, s16);
+        M[NW] = m16;
+        S[NW] = s16;
       }
-      // only terminators that can end a varint starting in [plo, phi)
-      const uint32_t plo = (uint32_t)(lvs - ls), phi = (uint32_t)(lend - ls);
-      const uint32_t tmax = phi + 9;  // exclusive
+      // terminator q: MSB clear at q and byte q+1 <= 2
+      uint64_t S1[NW + 1], X[NW + 1], tmp[NW + 1], Mk[NW + 1];
+      shr<NW + 1>(S, 1, S1);
 #pragma unroll
-      for (int w = 0; w < NW; w++) {
-        int b0 = w * 64;
-        if ((uint32_t)b0 >= tmax) T[w] = 0;
-        else if ((uint32_t)(b0 + 64) > tmax) T[w] &= (1ull << (tmax - b0)) - 1;
-      }
-      // descending over terminators, then over varint start positions
+      for (int w = 0; w <= NW; w++) X[w] = ~M[w] & S1[w];
+      // p is live if the run of MSB-set bytes from p ends at a terminator (<= 15 bytes)
 #pragma unroll
-      for (int w = NW - 1; w >= 0; w--) {
-        uint64_t tw = T[w];
-        while (tw) {
-          const int tb = 63 - __builtin_clzll(tw);
-          tw &= ~(1ull << tb);
-          const uint32_t tpos = (uint32_t)(w * 64 + tb);
-          uint32_t p = tpos;
-          for (;;) {
-            if (p < phi && p >= plo && !ovf) {
-              const uint64_t abs = ls + p;
-              Hdr h = parse_hdr_lds(buf, A, abs, se);
-              if (h.kind == H_VALID || h.kind == H_TAIL_BLOB || h.kind == H_TAIL_CHANGE ||
-                  h.kind == H_ERR_LEN) {
-                uint64_t exv;
-                uint32_t nd, dl;
-                if (h.kind != H_VALID) {
-                  exv = MARK_TERM | abs;
-                  nd = 1;
-                  dl = (h.kind == H_TAIL_BLOB) ? 1u : 0u;
-                } else {
-                  dl = h.id != 0 ? 1u : 0u;
-                  const uint64_t nx = h.succ;
-                  if (nx >= lend) {
-                    exv = nx;
-                    nd = 1;
-                  } else {
-                    const uint32_t nrel = (uint32_t)(nx - A);
-                    bool f = false;
-                    uint64_t fx = 0;
-                    uint32_t fm = 0;
+      for (int w = 0; w <= NW; w++) Mk[w] = M[w];
 #pragma unroll
-                    for (int k = 0; k < LMAX; k++)
-                      if ((uint32_t)k < cnt && (meta[k] & 0x3FFFu) == nrel) { f = true; fx = ex[k]; fm = meta[k]; }
-                    if (f) {
-                      exv = fx;
-                      nd = 1 + ((fm >> 14) & 0x1FFu);
-                      dl += fm >> 23;
-                    } else {  // successor is a dead / incomplete header inside this lane
-                      exv = MARK_TERM | nx;
-                      nd = 2;
-                    }
-                  }
-                }
-                if (cnt < (uint32_t)LMAX) {
-                  const uint32_t m = (uint32_t)(abs - A) | (umin64(nd, 511) << 14) | (umin64(dl, 511) << 23);
+      for (int d = 1; d <= 8; d <<= 1) {
+        shr<NW + 1>(X, d, tmp);
 #pragma unroll
-                  for (int k = 0; k < LMAX; k++)
-                    if ((uint32_t)k == cnt) { meta[k] = m; ex[k] = exv; }
-                  cnt++;
-                } else {
-                  ovf = 1;
-                }
-              }
-            }
-            if (p == 0 || p <= plo) break;
-            const uint32_t q = p - 1;
-            if (!((M[q >> 6] >> (q & 63)) & 1ull) || tpos - q + 1 > 10) break;
-            p = q;
-          }
+        for (int w = 0; w <= NW; w++) X[w] |= Mk[w] & tmp[w];
+        if (d < 8) {
+          shr<NW + 1>(Mk, d, tmp);
+#pragma unroll
+          for (int w = 0; w <= NW; w++) Mk[w] &= tmp[w];
         }
+      }
+#pragma unroll
+      for (int w = 0; w < NW; w++) {
+        const uint32_t b0 = 64u * w;
+        uint64_t r = ~0ull;
+        if (phi <= b0) r = 0;
+        else if (phi < b0 + 64) r = (1ull << (phi - b0)) - 1;
+        if (plo >= b0 + 64) r = 0;
+        else if (plo > b0) r &= ~((1ull << (plo - b0)) - 1);
+        lvm[w] = X[w] & r;
       }
     }
 
-    MARK(3);
-    // ---- chain walker: one lane per step ---------------------------------------------
-    int32_t ent = -1;     // this lane's entry (tile-relative) on the recorded chain
-    uint32_t mydl = 0;    // delivered frames of the recorded chain inside this lane
-    const TileCtx TC{buf, A, ve, se};
-    auto term_is_tail = [&](uint64_t x) -> bool {
-      const uint64_t q = x & POS_MASK;
-      if (q >= A + TILE) return false;
-      Hdr h = parse_hdr_lds(buf, A, q, se);
-      return h.kind == H_TAIL_HDR || h.kind == H_TAIL_CHANGE || h.kind == H_TAIL_BLOB;
+    TMARK(ST_T_STAGE);
+    // live masks go to LDS first: an exit that lands on a non-live position of a later lane
+    // is a dead end and must not take one of the lane's NC exit classes
+#pragma unroll
+    for (int w = 0; w < NW; w++) LM(lane, NC + 1, w) = lvm[w];
+    __syncthreads();
+
+    // ---- 2. lane DP: classify every live position, descending --------------------------
+    uint64_t cm[NC][NW], dm[NW];
+    uint64_t cex[NC];
+    uint32_t ncls = 0;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      cex[c] = 0;
+#pragma unroll
+      for (int w = 0; w < NW; w++) cm[c][w] = 0;
+    }
+#pragma unroll
+    for (int w = 0; w < NW; w++) dm[w] = 0;
+#pragma unroll
+    for (int w = NW - 1; w >= 0; w--) {
+      uint64_t bits = lvm[w];
+      while (bits) {
+        const uint32_t o = 64u * w + (63u - (uint32_t)__builtin_clzll(bits));
+        bits &= ~(1ull << (o & 63));
+        const Hdr h = parse_hdr_lds(buf, A, lb + o, se);
+        int cls = -1;  // -1 dead, -2 unresolved (class overflow)
+        if (h.kind == H_VALID) {
+          const uint64_t nx = h.succ;
+          bool exit_dead = false;
+          if (nx >= lhi && nx < ve) {
+            const uint32_t r2 = (uint32_t)(nx - A);
+            exit_dead = !((LM(r2 / B, NC + 1, (r2 % B) >> 6) >> (r2 & 63)) & 1ull);
+          } else if (nx >= ve && nx < se && nx + 16 <= A + TILE + HALO) {
+            const Hdr h2 = parse_hdr_lds(buf, A, nx, se);  // exit into the halo: error header there?
+            exit_dead = h2.kind >= H_ERR_VARINT;
+          }
+          if (exit_dead) {
+            cls = -1;
+          } else if (nx >= lhi) {
+            cls = -2;
+#pragma unroll
+            for (int c = 0; c < NC; c++)
+              if ((uint32_t)c < ncls && cex[c] == nx) cls = c;
+            if (cls == -2 && ncls < (uint32_t)NC) {
+#pragma unroll
+              for (int c = 0; c < NC; c++)
+                if ((uint32_t)c == ncls) cex[c] = nx;
+              cls = (int)ncls;
+              ncls++;
+            } else if (cls == -2) {
+              // table full: evict the farthest exit if this one is nearer. Near exits are
+              // checked against live / halo headers; far ones are mostly the 2-byte "shadow"
+              // varints that end on a frame's first header byte. Evicted positions become
+              // unresolved (a path through them takes the serial walk).
+              int far = 0;
+#pragma unroll
+              for (int c = 1; c < NC; c++)
+                if (cex[c] > cex[far]) far = c;
+              uint64_t fx = cex[0];
+#pragma unroll
+              for (int c = 1; c < NC; c++)
+                if (c == far) fx = cex[c];
+              if (nx < fx) {
+#pragma unroll
+                for (int c = 0; c < NC; c++)
+                  if (c == far) {
+                    cex[c] = nx;
+#pragma unroll
+                    for (int w = 0; w < NW; w++) cm[c][w] = 0;
+                  }
+                cls = far;
+              }
+            }
+          } else {
+            const uint32_t o2 = (uint32_t)(nx - lb);
+            if (tbit<NW>(dm, o2) || !tbit<NW>(lvm, o2)) {
+              cls = -1;
+            } else {
+              cls = -2;
+#pragma unroll
+              for (int c = 0; c < NC; c++)
+                if (tbit<NW>(cm[c], o2)) cls = c;
+            }
+          }
+        }
+        if (cls == -2) novf++;
+        if (cls == -1) sbit<NW>(dm, o);
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+          if (cls == c) sbit<NW>(cm[c], o);
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+#pragma unroll
+      for (int c = 0; c < NC; c++) LM(lane, c, w) = cm[c][w];
+      LM(lane, NC, w) = dm[w];
+    }
+    __syncthreads();
+
+    // node of an in-tile position q (vs <= q < ve): class node, N_DEAD or N_UNK
+    auto resolve = [&](uint64_t q) -> uint32_t {
+      const uint32_t r = (uint32_t)(q - A);
+      const uint32_t m = r / B, o = r % B;
+      const uint32_t w = o >> 6, b = o & 63;
+#pragma unroll
+      for (int c = 0; c < NC; c++)
+        if ((LM(m, c, w) >> b) & 1ull) return m * 4 + c;
+      if ((LM(m, NC, w) >> b) & 1ull) return N_DEAD;
+      if (!((LM(m, NC + 1, w) >> b) & 1ull)) return N_DEAD;
+      return N_UNK;
     };
 
-    // ---- entry: known, looked up early, overridden, or speculated -----------------------
-    uint64_t x = 0, y = MARK_NONE;
-    bool have_x = false, published = false;
-    if (first) {
-      x = e0;
-      have_x = true;
-    } else if (!P.strict) {
-      const uint64_t v = ld_agent(&P.inclx[t - 1]);
-      if (v) { x = v - 1; have_x = true; }
-    }
-    if (!have_x && !P.strict) {
-      const uint64_t ov = P.yover ? P.yover[t] : 0ull;
-      if (ov) {
-        y = ov - 1;
-      } else {
-        // candidates in ascending position order; best = most evidence, earliest on ties
-        uint64_t lanes_with = __ballot(cnt > 0);
-        int64_t best = -1;
-        uint32_t tried = 0;
-        bool done = false;
-        while (lanes_with && !done) {
-          const uint32_t l = (uint32_t)__builtin_ctzll(lanes_with);
-          lanes_with &= lanes_with - 1;
-          const uint32_t cl = uniform32(readlane32(cnt, l));
-          for (int32_t k = (int32_t)cl - 1; k >= 0 && !done; k--) {
-            uint32_t msel = 0;
+    // ---- 3. lane graph + pointer doubling ------------------------------------------------
+    uint32_t J[4];
 #pragma unroll
-            for (int kk = 0; kk < LMAX; kk++) if (kk == k) msel = meta[kk];
-            const uint64_t g = uniform64(A + (readlane32(msel, l) & 0x3FFFu));
-            uint32_t nodes, del;
-            const uint64_t xe = chain_walk<B>(F, TC, g, false, lane, ent, mydl, nodes, del);
-            const bool survived = xe < MARK_TERM || (ve == se && term_is_tail(xe));
-            if (survived) {
-              bool validated = false;
-              Hdr h = parse_hdr_lds(buf, A, g, se);
-              if (h.kind == H_VALID && h.id == 1) {
-                LdsReader rd{buf, A, umin64(A + TILE + HALO, se)};
-                ChangeCols c = decode_change(rd, g + h.vlen + 1, h.L - 1);
-                validated = (c.err == 0);
-              }
-              const int64_t score = (int64_t)nodes + (validated ? 1000 : 0);
-              if (score > best) { best = score; y = xe; }
-              if (nodes >= EVID || validated) done = true;
-            }
-            if (++tried >= (uint32_t)CMAX) done = true;
-          }
+    for (int c = 0; c < 4; c++) {
+      const uint32_t n = lane * 4 + c;
+      uint32_t j = n;  // self loop: EXIT node, unused slot, or the special nodes 3 / 7
+      if ((uint32_t)c < ncls) {
+        const uint64_t e = cex[c];
+        exv[n] = e;
+        if (e < ve) j = resolve(e);
+      }
+      J[c] = j;
+      jmp[0][n] = (uint8_t)j;
+    }
+    for (int r = 1; r < LEV; r++) {
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        J[c] = jmp[r - 1][J[c]];
+        jmp[r][lane * 4 + c] = (uint8_t)J[c];
+      }
+    }
+    __syncthreads();
+    // J[c] = final node of my class c
+
+    TMARK(ST_T_DP);
+    // ---- 4a. Y_t: distinct exits of my classes that land in the next tile ----------------
+    const bool has_next = (t + 1 < tl);
+    if (has_next) {
+      uint64_t cand[NC];
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        cand[c] = ~0ull;
+        if ((uint32_t)c < ncls && J[c] != N_DEAD && J[c] != N_UNK) {
+          const uint64_t e = exv[J[c]];
+          if (e >= A + TILE && e < A + 2 * TILE && e < se) cand[c] = e;
         }
       }
-      if (lane == 0) st_agent(&P.aggx[t], y + 1);
-      published = true;
+      uint64_t yw = READY;
+      for (int k = 0; k < 3; k++) {
+        bool any = false;
+        uint64_t mine = ~0ull;
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+          if (cand[c] != ~0ull && !any) { any = true; mine = cand[c]; }
+        const uint64_t bm = __ballot(any);
+        if (!bm) break;
+        const uint64_t y = readlane64(mine, (uint32_t)__builtin_ctzll(bm));
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+          if (cand[c] == y) cand[c] = ~0ull;
+        yw |= (y - (A + TILE) + 1) << (16 * k);
+        STAT(ST_Y_COUNT, 1);
+      }
+      if (lane == 0) st_agent(&P.ywd[t], yw);
     }
 
-    MARK(4);
-    // ---- exit look-back ----------------------------------------------------------------
-    if (!have_x) {
+    // ---- 4b. agg_t = f_t on Y_{t-1} (exact); published for successors' look-back --------
+    if (!first && !P.strict) {
+      uint64_t yk = 0;
       for (uint32_t spin = 0;; spin++) {
-        const int64_t pi = (int64_t)t - 1 - (int64_t)lane;
-        const bool inr = pi >= (int64_t)tf;
-        const uint64_t vi = inr ? ld_agent(&P.inclx[pi]) : 0ull;
-        const uint64_t va = (inr && !P.strict) ? ld_agent(&P.aggx[pi]) : 0ull;
-        const uint64_t im = __ballot(vi != 0);
-        if (im) {
-          const uint32_t ist = (uint32_t)__builtin_ctzll(im);
-          const uint64_t am = __ballot(va != 0 && (va - 1) != MARK_NONE);
-          const uint64_t need = (ist >= 64) ? ~0ull : ((1ull << ist) - 1);
-          if ((am & need) == need) {
-            uint64_t xv = readlane64(vi, ist) - 1;
-            for (int32_t i = (int32_t)ist - 1; i >= 0; i--) {
-              const uint64_t k = t - 1 - (uint64_t)i;
-              const uint64_t ce_k = umin64(A0 + (k - tf + 1) * TILE, se);
-              const uint64_t yk = readlane64(va, (uint32_t)i) - 1;
-              if (xv < ce_k) xv = yk;
+        yk = ld_agent(&P.ywd[t - 1]);
+        if (yk & READY) break;
+        if (spin > SPIN_MAX) { yk = READY; if (lane == 0) atomicOr(P.overflow, 2u); break; }
+        STAT(ST_Y_SPINS, 1);
+        __builtin_amdgcn_s_sleep(1);
+      }
+      yk = uniform64(yk);
+      uint64_t aw = READY;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const uint32_t rel = (uint32_t)(yk >> (16 * k)) & 0xFFFFu;
+        uint32_t code = V_UNK;
+        if (rel) {
+          const uint64_t q = A + rel - 1;
+          if (q >= vs && q < ve) {
+            const uint32_t n = resolve(q);
+            if (n != N_DEAD && n != N_UNK) {
+              const uint32_t f = jmp[LEV - 1][n];
+              if (f != N_DEAD && f != N_UNK) {
+                const uint64_t e = exv[f];
+                if (e - (A + TILE) < 0xFFF0ull) code = (uint32_t)(e - (A + TILE));
+              }
             }
-            x = xv;
-            break;
           }
         }
-        if (spin > SPIN_MAX) {  // a predecessor never published: flag, end the chain here
+        if (rel && code == V_UNK) STAT(ST_AGG_UNK, 1);
+        aw |= (uint64_t)code << (16 * k);
+      }
+      if (lane == 0) st_agent(&P.aggv[t], aw);
+    }
+
+    TMARK(ST_T_Y);
+    // ---- 4c. look-back: the entry x of this tile ----------------------------------------
+    // Poll only the inclusive exits of the 64 predecessors; the agg / Y words are read only
+    // for the tiles between the nearest inclusive and this one, when composing.
+    uint64_t x = e0;
+    if (!first) {
+      uint32_t nap = 1;
+      for (uint32_t spin = 0;; spin++) {
+        const int64_t j = (int64_t)t - 1 - (int64_t)lane;
+        const bool inr = j >= (int64_t)tf;
+        const uint64_t vi = inr ? ld_agent(&P.inclx[j]) : 0ull;
+        const uint64_t im = __ballot(vi != 0);
+        bool ok = false;
+        STAT(ST_LB_ITERS, 1);
+        if (!im) STAT(ST_LB_NOINCL, 1);
+        if (im) {
+          const uint32_t ist = (uint32_t)__builtin_ctzll(im);
+          uint64_t av = 0, yk = 0;
+          if (lane < ist && j > (int64_t)tf && !P.strict) {
+            av = ld_agent(&P.aggv[j]);
+            if (av & READY) yk = ld_agent(&P.ywd[j - 1]);
+          }
+          uint64_t xv = readlane64(vi, ist) - 1;
+          ok = true;
+          for (int32_t i = (int32_t)ist - 1; i >= 0 && ok; i--) {
+            const uint64_t Aj = A - (uint64_t)(i + 1) * TILE;
+            if (xv >= Aj + TILE) continue;  // passes over tile j (also: chain already ended)
+            const uint64_t ai = readlane64(av, (uint32_t)i), yi = readlane64(yk, (uint32_t)i);
+            if (!(ai & READY) || !(yi & READY)) { ok = false; STAT(ST_LB_NOAGG, 1); break; }
+            const uint64_t rel = xv - Aj + 1;
+            uint32_t code = V_UNK;
+            bool hit = false;
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+              if (((yi >> (16 * k)) & 0xFFFFu) == rel) { code = (uint32_t)(ai >> (16 * k)) & 0xFFFFu; hit = true; }
+            if (code == V_UNK) {
+              STAT(hit ? ST_LB_VUNK : ST_LB_KEYMISS, 1);
+              ok = false;
+              break;
+            }
+            xv = Aj + TILE + code;
+          }
+          if (ok) { x = xv; STAT(ist ? ST_LB_OKN : ST_LB_OK0, 1); }
+        }
+        if (ok) break;
+        if (spin > SPIN_MAX) {
           if (lane == 0) atomicOr(P.overflow, 2u);
           x = MARK_TERM | vs;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(2);
+        nap = nap < 8 ? nap * 2 : 8;
       }
     }
-
-    MARK(5);
-    // ---- exact chain through this tile ---------------------------------------------------
     x = uniform64(x);
-    y = uniform64(y);
-    uint64_t exit_t;
-    uint32_t count_t = 0;
+    STAT(ST_TILES, 1);
+    if (x >= ve) STAT(ST_PASS, 1);
+
+    TMARK(ST_T_LB);
+    // the exact exit is known right away unless the path ends inside the tile / is serial:
+    // publish it before the lane walks so successors' look-backs advance sooner
+    bool early = false;
+    uint32_t n0 = N_DEAD;
     if (x >= ve) {
-      exit_t = x;  // pass-through (inside a long frame) or the chain already ended
+      early = true;
     } else {
-      uint32_t nodes;
-      exit_t = chain_walk<B>(F, TC, x, true, lane, ent, mydl, nodes, count_t);
+      n0 = uniform32(resolve(x));
+      if (n0 != N_DEAD && n0 != N_UNK) {
+        const uint32_t f = jmp[LEV - 1][n0];
+        early = (f != N_DEAD && f != N_UNK);
+        if (early && lane == 0) st_agent(&P.inclx[t], exv[f] + 1);
+      }
+    }
+    if (x >= ve && lane == 0) st_agent(&P.inclx[t], x + 1);
+
+    // ---- 5a. this tile's path: entries per lane -------------------------------------------
+    bool graph_exit = false;
+    uint64_t gexit = 0;
+    if (x < ve) {
+      if (lane == 0) entry[(uint32_t)(x - A) / B] = (int32_t)(x - A);
+      bool serial = (n0 == N_UNK);
+      if (n0 != N_DEAD && n0 != N_UNK) {
+        const uint32_t f = jmp[LEV - 1][n0];
+        if (f == N_UNK) serial = true;
+        if (f != N_DEAD && f != N_UNK) { graph_exit = true; gexit = exv[f]; }
+        if (!serial) {
+          // mark the path: after level r the marked set is {J^k(n0) : k < 2^(r+1)}
+#pragma unroll
+          for (int c = 0; c < 4; c++) mark[lane * 4 + c] = 0;
+          __syncthreads();
+          if (lane == 0) mark[n0] = 1;
+          for (int r = 0; r < LEV - 1; r++) {
+            __syncthreads();
+            uint32_t tg[4];
+            bool mk[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+              mk[c] = mark[lane * 4 + c] != 0;
+              tg[c] = jmp[r][lane * 4 + c];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+              if (mk[c]) mark[tg[c]] = 1;
+          }
+          __syncthreads();
+#pragma unroll
+          for (int c = 0; c < NC; c++) {
+            const uint32_t n = lane * 4 + c;
+            if ((uint32_t)c < ncls && mark[n]) {
+              const uint32_t nx = jmp[0][n];
+              const uint64_t e = cex[c];
+              if (e < ve && nx != n) {  // the path continues in a later lane (class or death)
+                const uint32_t r = (uint32_t)(e - A);
+                entry[r / B] = (int32_t)r;
+              }
+            }
+          }
+        }
+      }
+      if (serial) STAT(ST_SERIAL, 1);
+      if (serial) {  // class overflow on the path: walk it frame by frame (rare)
+        uint64_t cur = x;
+        for (;;) {
+          if (cur >= ve) break;
+          const uint32_t r = (uint32_t)(cur - A);
+          if (lane == 0 && entry[r / B] < 0) entry[r / B] = (int32_t)r;
+          const Hdr h = parse_hdr_lds(buf, A, cur, se);
+          if (h.kind != H_VALID) break;
+          cur = uniform64(h.succ);
+        }
+      }
+      __syncthreads();
+    }
+
+    // ---- 5b. lane walks: delivered frames of the path inside my bytes --------------------
+    // The path leaves the last entered lane at wend; if that is still inside the tile (a
+    // path that dies at a dead-end exit), the lane holding it walks next.
+    int32_t myent = entry[lane];
+    uint64_t dmask[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) dmask[w] = 0;
+    uint32_t cnt = 0;
+    uint64_t wend = 0;
+    uint64_t exit_t = x;
+    uint32_t count_t = 0;
+    if (x < ve) {
+      bool walk = myent >= 0;
+      for (;;) {
+        if (walk) {
+          uint64_t cur = A + (uint32_t)myent;
+          for (;;) {
+            if (cur >= lhi) { wend = cur; break; }
+            const Hdr h = parse_hdr_lds(buf, A, cur, se);
+            if (hdr_delivered(h)) { sbit<NW>(dmask, (uint32_t)(cur - lb)); cnt++; }
+            if (h.kind != H_VALID) { wend = MARK_TERM | cur; break; }
+            cur = h.succ;
+          }
+        }
+        const uint64_t em = __ballot(myent >= 0);
+        const uint32_t last = 63u - (uint32_t)__builtin_clzll(em);
+        exit_t = uniform64(readlane64(wend, last));
+        if (exit_t >= ve) break;
+        const uint32_t r = (uint32_t)(exit_t - A);
+        walk = lane == r / B;
+        if (walk) myent = (int32_t)r;
+      }
+      count_t = wave_sum32(cnt);
+      if (graph_exit && exit_t != gexit && lane == 0) atomicOr(P.overflow, 4u);
     }
     exit_t = uniform64(exit_t);
     count_t = uniform32(count_t);
-    if (count_t > TILE) {  // impossible for a consistent walk: flag instead of looping on it
-      if (lane == 0) atomicOr(P.overflow, 4u);
-      count_t = 0;
-    }
-    if (published && y != MARK_NONE && exit_t != y && x < ve) {
-      if (lane == 0) atomicMin(P.misspec, (uint32_t)t);
-    }
     if (lane == 0) {
-      st_agent(&P.inclx[t], exit_t + 1);
+      if (!early) st_agent(&P.inclx[t], exit_t + 1);
       st_agent(&P.aggc[t], (uint64_t)count_t + 1);
     }
 
-    MARK(6);
-    // ---- count look-back -> first output slot ------------------------------------------
+    TMARK(ST_T_PATH);
+    // ---- 5c. count look-back -> first output slot ------------------------------------------
+    // Decoupled look-back over sums: windows of 64 predecessors, moving back while a whole
+    // window has counts but no inclusive prefix.
     uint64_t base = 0;
     if (t > 0) {
+      uint64_t csum = 0;
+      int64_t top = (int64_t)t - 1;
+      uint32_t nap = 1;
       for (uint32_t spin = 0;;) {
-        const int64_t pi = (int64_t)t - 1 - (int64_t)lane;
+        const int64_t pi = top - (int64_t)lane;
         uint64_t vi = 0, va = 0;
         if (pi >= 0) {
           vi = ld_agent(&P.inclc[pi]);
-          va = ld_agent(&P.aggc[pi]);
+          if (!vi) va = ld_agent(&P.aggc[pi]);
         } else if (pi == -1) {
           vi = 1;  // virtual inclusive prefix 0 before tile 0
         }
         const uint64_t im = __ballot(vi != 0);
-        if (im) {
-          const uint32_t ist = (uint32_t)__builtin_ctzll(im);
-          const uint64_t am = __ballot(va != 0);
-          const uint64_t need = (1ull << ist) - 1;
-          if ((am & need) == need) {
-            const uint64_t part = (lane < ist) ? va - 1 : 0ull;
-            base = readlane64(vi, ist) - 1 + wave_sum64(part);
-            base = uniform64(base);
+        const uint32_t ist = im ? (uint32_t)__builtin_ctzll(im) : 64u;
+        const uint64_t am = __ballot(va != 0);
+        const uint64_t need = ist >= 64 ? ~0ull : ((1ull << ist) - 1);
+        if ((am & need) == need) {
+          csum += wave_sum64(lane < ist ? va - 1 : 0ull);
+          if (ist < 64) {
+            base = csum + readlane64(vi, ist) - 1;
             break;
           }
+          top -= 64;
+          continue;
         }
         if (++spin > SPIN_MAX) {
           if (lane == 0) atomicOr(P.overflow, 2u);
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        STAT(ST_CNT_SPINS, 1);
+        for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(2);
+        nap = nap < 8 ? nap * 2 : 8;
       }
     }
     base = uniform64(base);
     if (lane == 0) st_agent(&P.inclc[t], base + count_t + 1);
     if (base + count_t > P.cap && lane == 0) atomicOr(P.overflow, 1u);
 
-    MARK(7);
-    // ---- emit frames ---------------------------------------------------------------------
-    MARK(10);
-    const uint32_t myoff = wave_incl_scan32(mydl) - mydl;
-    MARK(11);
-    uint32_t nch = 0, nbl = 0;
+    TMARK(ST_T_CNT);
+    // ---- 5d. emit ------------------------------------------------------------------------
+    const uint32_t myoff = wave_incl_scan32(cnt) - cnt;
+    uint32_t nch = 0, nbl = 0, k = 0;
     uint64_t badf = ~0ull;
-    for (uint32_t r0 = 0; r0 < count_t; r0 += FL_CAP) {
-      if (ent >= 0 && mydl) {
-        uint64_t cur = A + (uint32_t)ent;
-        uint32_t k = 0;
-        for (;;) {
-          Hdr h = parse_hdr_lds(buf, A, cur, se);
-          if (hdr_delivered(h)) {
-            const uint32_t rank = myoff + k;
-            if (rank >= r0 && rank < r0 + FL_CAP) flist[rank - r0] = (uint16_t)(cur - A);
-            k++;
-          }
-          if (h.kind != H_VALID) break;
-          cur = h.succ;
-          if (cur >= lend) break;
-        }
-      }
-      MARK(12);
-      __syncthreads();
-      MARK(13);
-      const uint32_t nr = (count_t - r0) < FL_CAP ? (count_t - r0) : FL_CAP;
-      for (uint32_t k = lane; k < nr; k += 64) {
-        const uint64_t pos = A + flist[k];
-        Hdr h = parse_hdr_lds(buf, A, pos, se);
-        const uint64_t f = base + r0 + k;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      uint64_t bits = dmask[w];
+      while (bits) {
+        const uint32_t o = 64u * w + (uint32_t)__builtin_ctzll(bits);
+        bits &= bits - 1;
+        const uint64_t pos = lb + o;
+        const Hdr h = parse_hdr_lds(buf, A, pos, se);
+        const uint64_t f = base + myoff + k;
+        k++;
         const uint64_t po = pos + h.vlen + 1;
         const uint64_t pl = h.L - 1;
-        uint32_t ty = h.id | (h.kind == H_TAIL_BLOB ? DRP_FRAME_PARTIAL : 0u);
+        const uint32_t ty = h.id | (h.kind == H_TAIL_BLOB ? DRP_FRAME_PARTIAL : 0u);
         if (h.id == 1) nch++; else nbl++;
         if (f < P.cap) {
           P.payload_off[f] = po;
           P.payload_len[f] = pl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pl;
           P.type[f] = (uint8_t)ty;
           if (h.id == 1) {
-            LdsReader rd{buf, A, umin64(A + TILE + HALO, se)};
+            const LdsReader rd{buf, A, umin64(A + TILE + HALO, se)};
             ChangeCols c = decode_change(rd, po, pl);
             if (c.err == ERR_UNREACHABLE) {
-              GlobalReader gr{P.bytes, se};
+              const GlobalReader gr{P.bytes, se};
               c = decode_change(gr, po, pl);
             }
             P.key_off[f] = c.key_off;
@@ -519,18 +703,11 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
             uint32_t fl = c.flags;
             if (c.err == DRP_ERR_REQUIRED) fl |= DRP_F_MISSING;
             P.flags[f] = (uint8_t)fl;
-            if (c.err) {
-              atomicMin((unsigned long long *)&P.payload_err[s], (unsigned long long)f);
-              badf = f < badf ? f : badf;
-            }
+            if (c.err) badf = f < badf ? f : badf;
           }
         }
       }
-      MARK(14);
-      __syncthreads();
-      MARK(15);
     }
-    MARK(8);
     nch = wave_sum32(nch);
     nbl = wave_sum32(nbl);
 #pragma unroll
@@ -541,26 +718,13 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
     if (lane == 0) {
       if (nch) atomicAdd((unsigned long long *)&P.scount[2 * s], (unsigned long long)nch);
       if (nbl) atomicAdd((unsigned long long *)&P.scount[2 * s + 1], (unsigned long long)nbl);
-      P.tile_x[t] = x;
+      if (badf != ~0ull) atomicMin((unsigned long long *)&P.payload_err[s], (unsigned long long)badf);
       P.tile_exit[t] = exit_t;
       P.tile_base[t] = base;
       P.tile_count[t] = count_t;
-      P.tile_nch[t] = nch;
-      P.tile_nbl[t] = nbl;
-      P.tile_perr[t] = badf;
     }
-    MARK(9);
+    TMARK(ST_T_EMIT);
   }
-#ifdef DRP_KERNEL_TRACE
-  if (P.dbg && lane == 0)
-    __hip_atomic_store(P.dbg + blockIdx.x * 4 + 1, 0xD0Eu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-}
-
-// Debug: copy the agent-scope progress words of a running decode to host-mapped memory.
-__global__ void peek_kernel(const uint32_t *dbg, uint32_t n, uint32_t *out) {
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
-    out[i] = __hip_atomic_load(dbg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // tile_prefix[s] = number of tiles of streams < s; tile_prefix[nstreams] = total.
@@ -692,7 +856,6 @@ extern "C" hipError_t drp_launch_tile_prefix(uint32_t B, const uint64_t *stream_
   switch (B) {
     case 64: hipLaunchKernelGGL(tile_prefix_kernel<64>, dim3(1), dim3(1024), 0, st, stream_off, nstreams, tile_prefix); break;
     case 128: hipLaunchKernelGGL(tile_prefix_kernel<128>, dim3(1), dim3(1024), 0, st, stream_off, nstreams, tile_prefix); break;
-    case 256: hipLaunchKernelGGL(tile_prefix_kernel<256>, dim3(1), dim3(1024), 0, st, stream_off, nstreams, tile_prefix); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -702,14 +865,8 @@ extern "C" hipError_t drp_launch_decode(uint32_t B, const DecodeParams *P, uint3
   switch (B) {
     case 64: hipLaunchKernelGGL(decode_tiles<64>, dim3(grid), dim3(64), 0, st, *P); break;
     case 128: hipLaunchKernelGGL(decode_tiles<128>, dim3(grid), dim3(64), 0, st, *P); break;
-    case 256: hipLaunchKernelGGL(decode_tiles<256>, dim3(grid), dim3(64), 0, st, *P); break;
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
-}
-
-extern "C" hipError_t drp_launch_peek(const uint32_t *dbg, uint32_t n, uint32_t *out, hipStream_t st) {
-  hipLaunchKernelGGL(peek_kernel, dim3(1), dim3(256), 0, st, dbg, n, out);
   return hipGetLastError();
 }
 

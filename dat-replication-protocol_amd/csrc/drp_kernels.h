@@ -22,20 +22,21 @@ struct DecodeParams {
   uint64_t *change, *from, *to;
   uint8_t *flags;
   uint64_t cap;
-  // per-tile scratch
-  uint64_t *aggx, *inclx, *aggc, *inclc;  // look-back granules (value + 1; 0 = not yet)
-  uint64_t *tile_x, *tile_exit, *tile_base, *tile_count;
-  uint64_t *tile_nch, *tile_nbl, *tile_perr;  // per-tile change / blob counts, min bad frame
-  const uint64_t *yover;  // per-tile corrected speculative exit (value + 1; 0 = none)
+  // per-tile look-back words (value + 1, or READY-tagged; 0 = not yet published)
+  uint64_t *ywd;    // Y_t: <= 3 distinct exits landing in tile t+1 (16-bit rel + 1) | READY
+  uint64_t *aggv;   // agg_t: f_t on the slots of Y_{t-1} (16-bit codes) | READY
+  uint64_t *inclx;  // exact exit of tile t + 1
+  uint64_t *aggc;   // delivered frames of tile t + 1
+  uint64_t *inclc;  // frames of tiles <= t + 1
+  uint64_t *tile_exit, *tile_base, *tile_count;  // per-tile records for finalize
   // per-stream scratch
   uint64_t *payload_err;  // min absolute index of a malformed Change
   uint64_t *scount;       // [2*s] changes, [2*s+1] blobs
   // control
   uint32_t *counter;
-  uint32_t *misspec;
-  uint32_t *overflow;
-  uint32_t strict;
-  uint32_t *dbg;  // optional host-mapped progress markers (DRP_TRACE)
+  uint32_t *overflow;  // bit 0 capacity, bit 1 bounded wait expired, bit 2 inconsistent walk
+  uint32_t strict;     // look-back uses exact inclusive exits only (test hook)
+  unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
 };
 
 struct EncodeParams {
@@ -61,7 +62,6 @@ hipError_t drp_launch_finalize(const uint8_t *bytes, const uint64_t *stream_off,
                                const uint64_t *payload_err, const uint64_t *scount,
                                const uint8_t *type, const uint8_t *flags, uint64_t cap,
                                drp_stream_result *res, hipStream_t st);
-hipError_t drp_launch_peek(const uint32_t *dbg, uint32_t n, uint32_t *out, hipStream_t st);
 hipError_t drp_launch_encode(const drp::EncodeParams *P, hipStream_t st);
 hipError_t drp_launch_index_scan(const drp_stream_stats *stats, uint64_t count, uint64_t *base,
                                  hipStream_t st);

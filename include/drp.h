@@ -151,9 +151,9 @@ void drp_close(drp_ctx *ctx);
 void *drp_stream(drp_ctx *ctx);
 int drp_synchronize(drp_ctx *ctx);
 int drp_last_timing(drp_ctx *ctx, drp_timing *out);
-/* Tunables (0 = default). tile_bytes must be 64*k, k in {64,128,256}. */
+/* Tunables (0 = default 4096). tile_bytes is 4096 or 8192 (64 lanes x 64 or 128 bytes). */
 int drp_set_tile(drp_ctx *ctx, uint32_t tile_bytes);
-/* Force every tile to wait for its predecessor's exact exit (no speculation). Test hook. */
+/* Look-back composes exact inclusive exits only, never the per-tile maps agg_t. Test hook. */
 int drp_set_strict(drp_ctx *ctx, int strict);
 /* Device scratch bytes needed to decode `n` bytes split into `nstreams` streams. */
 uint64_t drp_decode_scratch_bytes(drp_ctx *ctx, uint64_t n, uint64_t nstreams);
