@@ -169,7 +169,8 @@ int drp_set_strict(drp_ctx *c, int strict) {
 // scratch layout for a decode of `nbytes` over `ns` streams
 struct DecLayout {
   uint64_t ntiles_max;
-  size_t tile_prefix, rec, tiles, perr, scount, ctrl, total;
+  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, total;
+  uint64_t nsg;
 };
 static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   DecLayout L;
@@ -178,6 +179,8 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   size_t o = 0;
   L.tile_prefix = o; o += al((ns + 1) * 8);
   L.rec = o; o += al(5 * L.ntiles_max * 8);    // ywd, aggv, inclx, aggc, inclc (zeroed per call)
+  L.nsg = L.ntiles_max / 64 + 2;
+  L.sgrp = o; o += al(L.nsg * 24);             // sgc_agg+sgc_cnt (u32 x2), sagg, scnt (zeroed)
   L.tiles = o; o += al(3 * L.ntiles_max * 8);  // exit, base, count
   L.perr = o; o += al(ns * 8);
   L.scount = o; o += al(2 * ns * 8);
@@ -212,6 +215,8 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
   hipStream_t st = c->st;
   CHK(hipEventRecord(c->ev[0], st));
   CHK(hipMemsetAsync(rec, 0, 5 * NT * 8, st));
+  uint8_t *sgrp = c->scratch.at<uint8_t>(L.sgrp);
+  CHK(hipMemsetAsync(sgrp, 0, L.nsg * 24, st));
   CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
   CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
   CHK(hipMemsetAsync(ctrl, 0, 16, st));
@@ -244,6 +249,10 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
   P.inclx = rec + 2 * NT;
   P.aggc = rec + 3 * NT;
   P.inclc = rec + 4 * NT;
+  P.sgc_agg = reinterpret_cast<uint32_t *>(sgrp);
+  P.sgc_cnt = P.sgc_agg + L.nsg;
+  P.sagg = reinterpret_cast<uint64_t *>(sgrp + L.nsg * 8);
+  P.scnt = P.sagg + L.nsg;
   P.tile_exit = tiles;
   P.tile_base = tiles + NT;
   P.tile_count = tiles + 2 * NT;
@@ -262,9 +271,10 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
   // persistent grid: single-wave blocks, several per CU; tiles are handed out in stream
   // order by an atomic counter, so a tile only ever waits on tiles already taken.
   const uint32_t tile = 64u * c->B;
-  const uint64_t tiles_needed = nbytes / tile + ns + 1;
-  uint32_t grid = (uint32_t)(c->cus * c->waves_per_cu);
-  if (tiles_needed < grid) grid = (uint32_t)tiles_needed;
+  const uint32_t wpg = drp_decode_waves_per_group();
+  const uint64_t groups_needed = (nbytes / tile + ns + 1 + wpg - 1) / wpg;
+  uint32_t grid = (uint32_t)(c->cus * ((c->waves_per_cu + wpg - 1) / wpg));
+  if (groups_needed < grid) grid = (uint32_t)groups_needed;
   if (grid == 0) grid = 1;
   TRACE("decode: nbytes=%llu ns=%llu B=%u grid=%u NT=%llu", (unsigned long long)nbytes,
         (unsigned long long)ns, c->B, grid, (unsigned long long)NT);

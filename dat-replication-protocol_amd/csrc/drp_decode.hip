@@ -50,13 +50,13 @@ enum : uint32_t {
   ST_T_GRAB, ST_T_STAGE, ST_T_DP, ST_T_Y, ST_T_LB, ST_T_PATH, ST_T_CNT, ST_T_EMIT,
   ST_NSTATS
 };
-#define STAT(k, v)                        \
-  do {                                    \
-    if (P.stats) acc[k] += (uint64_t)(v); \
+#define STAT(k, v)                         \
+  do {                                     \
+    if (PROF) acc[k] += (uint64_t)(v);     \
   } while (0)
 #define TMARK(k)                             \
   do {                                       \
-    if (P.stats) {                           \
+    if (PROF) {                              \
       const uint64_t now_ = clock64();       \
       acc[k] += now_ - tclk;                 \
       tclk = now_;                           \
@@ -109,46 +109,75 @@ __device__ __forceinline__ uint4 load16(const uint8_t *g, uint64_t p, uint64_t s
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// LDS of one wave (one tile).
 template <int B>
-__global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
+struct WaveLds {
+  static constexpr uint32_t TILE = 64u * B;
+  static constexpr int NW = B / 64;
+  static constexpr int NM = NC + 2;
+  uint8_t buf[TILE + HALO + 32] __attribute__((aligned(16)));
+  uint64_t lm[64 * NM * NW];  // per lane: class masks, dead mask, live mask
+  uint64_t exv[256];          // node -> its class exit
+  uint8_t jmp[LEV][256];      // doubling levels of the lane graph
+  uint8_t mark[256];
+  int32_t entry[64];          // per lane: entry of the tile's path (tile-relative), -1 none
+};
+
+// Orders this wave's LDS accesses (a wave's DS instructions execute in order; this keeps
+// the compiler from moving them and drains outstanding LDS traffic).
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+}
+
+constexpr int WPG = 4;  // waves (= consecutive tiles) per workgroup: one grab per group
+constexpr int64_t SG = 64;  // tiles per super-group (second look-back level)
+#ifndef DRP_MIN_WAVES
+#define DRP_MIN_WAVES 3  // waves per SIMD the register allocation must allow
+#endif
+
+template <int B, bool PROF>
+__global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodeParams P) {
   constexpr uint32_t TILE = 64u * B;
   constexpr int NW = B / 64;           // mask words per lane
   constexpr int NV = B / 16;           // 16-byte loads per lane
-  constexpr uint32_t LBUF = TILE + HALO + 32;
   constexpr int NM = NC + 2;           // per lane: class masks, dead mask, live mask
-  __shared__ __attribute__((aligned(16))) uint8_t buf[LBUF];
-  __shared__ uint64_t lm[64 * NM * NW];
-  __shared__ uint64_t exv[256];
-  __shared__ uint8_t jmp[LEV][256];
-  __shared__ uint8_t mark[256];
-  __shared__ int32_t entry[64];
+  __shared__ WaveLds<B> wl[WPG];
+  __shared__ uint32_t grp_slot;
 
   const uint32_t lane = lane_id();
+  const uint32_t wid = threadIdx.x >> 6;
+  uint8_t *const buf = wl[wid].buf;
+  uint64_t *const lm = wl[wid].lm;
+  uint64_t *const exv = wl[wid].exv;
+  uint8_t(*const jmp)[256] = wl[wid].jmp;
+  uint8_t *const mark = wl[wid].mark;
+  int32_t *const entry = wl[wid].entry;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
 
   // lm accessors: lane m, mask k (0..NC-1 class, NC dead, NC+1 live), word w
   auto LM = [&](uint32_t m, uint32_t k, uint32_t w) -> uint64_t & { return lm[(m * NM + k) * NW + w]; };
 
-  uint64_t acc[ST_NSTATS];
+  uint64_t acc[PROF ? ST_NSTATS : 1];
 #pragma unroll
-  for (int i = 0; i < (int)ST_NSTATS; i++) acc[i] = 0;
-  uint64_t tclk = P.stats ? clock64() : 0;
+  for (int i = 0; i < (PROF ? (int)ST_NSTATS : 1); i++) acc[i] = 0;
+  uint64_t tclk = PROF ? clock64() : 0;
   uint32_t novf = 0;
 
   for (;;) {
-    // Every lane executes the atomic (addend 1 on lane 0): a grab under `if (lane == 0)`
-    // let the structurizer split this loop so its inner back-edge skipped the grab.
-    const uint32_t tt = atomicAdd(P.counter, lane == 0 ? 1u : 0u);
-    const uint64_t t = uniform32(readlane32(tt, 0));
-    if (t >= ntiles) {
-      if (P.stats) {
-        acc[ST_OVF_LANES] = wave_sum32(novf);
-        if (lane == 0)
-#pragma unroll
-          for (int i = 0; i < (int)ST_NSTATS; i++) atomicAdd(P.stats + i, (unsigned long long)acc[i]);
-      }
-      return;
+    // one atomic grab per group of WPG consecutive tiles; every lane of wave 0 executes
+    // the atomic (addend 1 on lane 0) so the grab is never split off the loop
+    __syncthreads();
+    if (wid == 0) {
+      const uint32_t g = atomicAdd(P.counter, lane == 0 ? 1u : 0u);
+      if (lane == 0) grp_slot = g;
     }
+    __syncthreads();
+    const uint64_t g0 = (uint64_t)grp_slot * WPG;
+    if (g0 >= ntiles) break;
+    const uint64_t t = g0 + wid;
+    if (t >= ntiles) continue;
 
     // ---- which stream / tile ---------------------------------------------------------
     uint64_t lo = 0, hi = P.nstreams;
@@ -166,7 +195,6 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
     const uint64_t e0 = so + (P.entry ? P.entry[s] : 0ull);
 
     TMARK(ST_T_GRAB);
-    __syncthreads();  // previous tile's LDS reads are done
     // ---- stage: own B bytes (+ the halo) into LDS --------------------------------------
     const uint64_t lb = A + (uint64_t)lane * B;
     uint4 v[NV];
@@ -178,7 +206,7 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
       *reinterpret_cast<uint4 *>(buf + TILE + lane * 16) = load16(P.bytes, A + TILE + lane * 16, se);
     if (lane < 2) *reinterpret_cast<uint4 *>(buf + TILE + HALO + lane * 16) = make_uint4(0, 0, 0, 0);
     entry[lane] = -1;
-    __syncthreads();
+    wsync();
 
     // ---- 1. live mask over the lane's B bytes ----------------------------------------------
     const uint32_t plo = (uint32_t)(vs > lb ? umin64(vs - lb, B) : 0);
@@ -239,7 +267,7 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
     // is a dead end and must not take one of the lane's NC exit classes
 #pragma unroll
     for (int w = 0; w < NW; w++) LM(lane, NC + 1, w) = lvm[w];
-    __syncthreads();
+    wsync();
 
     // ---- 2. lane DP: classify every live position, descending --------------------------
     uint64_t cm[NC][NW], dm[NW];
@@ -333,7 +361,7 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
       for (int c = 0; c < NC; c++) LM(lane, c, w) = cm[c][w];
       LM(lane, NC, w) = dm[w];
     }
-    __syncthreads();
+    wsync();
 
     // node of an in-tile position q (vs <= q < ve): class node, N_DEAD or N_UNK
     auto resolve = [&](uint64_t q) -> uint32_t {
@@ -363,14 +391,14 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
       jmp[0][n] = (uint8_t)j;
     }
     for (int r = 1; r < LEV; r++) {
-      __syncthreads();
+      wsync();
 #pragma unroll
       for (int c = 0; c < 4; c++) {
         J[c] = jmp[r - 1][J[c]];
         jmp[r][lane * 4 + c] = (uint8_t)J[c];
       }
     }
-    __syncthreads();
+    wsync();
     // J[c] = final node of my class c
 
     TMARK(ST_T_DP);
@@ -405,17 +433,12 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
       if (lane == 0) st_agent(&P.ywd[t], yw);
     }
 
-    // ---- 4b. agg_t = f_t on Y_{t-1} (exact); published for successors' look-back --------
-    if (!first && !P.strict) {
-      uint64_t yk = 0;
-      for (uint32_t spin = 0;; spin++) {
-        yk = ld_agent(&P.ywd[t - 1]);
-        if (yk & READY) break;
-        if (spin > SPIN_MAX) { yk = READY; if (lane == 0) atomicOr(P.overflow, 2u); break; }
-        STAT(ST_Y_SPINS, 1);
-        __builtin_amdgcn_s_sleep(1);
-      }
-      yk = uniform64(yk);
+    // ---- 4b/4c. look-back for the entry x of this tile ---------------------------------
+    // agg_t = f_t on Y_{t-1} is only needed by successors while this tile has no inclusive
+    // exit, so it is published lazily: after a first failed attempt and once Y_{t-1} exists.
+    // A tile that composes forward from a predecessor's inclusive exit also publishes the
+    // exits it derives for the tiles in between ("helping"), so the frontier jumps ahead.
+    auto publish_agg = [&](uint64_t yk) {
       uint64_t aw = READY;
 #pragma unroll
       for (int k = 0; k < 3; k++) {
@@ -438,53 +461,194 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
         aw |= (uint64_t)code << (16 * k);
       }
       if (lane == 0) st_agent(&P.aggv[t], aw);
-    }
-
+    };
     TMARK(ST_T_Y);
-    // ---- 4c. look-back: the entry x of this tile ----------------------------------------
-    // Poll only the inclusive exits of the 64 predecessors; the agg / Y words are read only
-    // for the tiles between the nearest inclusive and this one, when composing.
+    // Tile-level evaluation of the exact exit v through tiles j0 .. j0+n-1 of this stream
+    // (lanes hold aggv / ywd of tile j0+lane). Returns how many tiles were passed; the exit
+    // after tile j0+k is left in lane k's `mine` (value + 1).
+    auto eval_tiles = [&](uint64_t &v, int64_t j0, uint32_t n, uint64_t av, uint64_t yk,
+                          uint64_t &mine) -> uint32_t {
+      uint32_t k = 0;
+      for (; k < n; k++) {
+        const uint64_t Aj = A - (uint64_t)((int64_t)t - (j0 + (int64_t)k)) * TILE;
+        if (v < Aj + TILE) {
+          const uint64_t ai = readlane64(av, k), yi = readlane64(yk, k);
+          if (!(ai & READY) || !(yi & READY)) break;
+          const uint64_t rel = v - Aj + 1;
+          uint32_t code = V_UNK;
+#pragma unroll
+          for (int q = 0; q < 3; q++)
+            if (((yi >> (16 * q)) & 0xFFFFu) == rel) code = (uint32_t)(ai >> (16 * q)) & 0xFFFFu;
+          if (code == V_UNK) break;
+          v = uniform64(Aj + TILE + code);
+        }
+        if (lane == k) mine = v + 1;
+      }
+      return k;
+    };
+    // Super-group bookkeeping: the last tile of a group of 64 to publish its map composes
+    // the group's 64 maps into sagg[g] (keys = Y of the tile before the group).
+    const int64_t sg = (int64_t)(t / SG), sg0 = sg * SG;
+    const uint64_t sgsize = umin64(SG, ntiles - (uint64_t)sg0);
+    auto sg_agg_done = [&]() {
+      uint32_t old = 0;
+      // relaxed: the words read below are self-validating (READY-tagged), so the last
+      // finisher just waits until every one of them is visible
+      if (lane == 0) old = __hip_atomic_fetch_add(&P.sgc_agg[sg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = readlane32(old, 0);
+      if (old != sgsize - 1) return;
+      uint64_t cw = READY | 0xFFFFFFFFFFFFull;  // all V_UNK
+      if (sgsize == SG && sg0 > (int64_t)tf && sg0 + SG - 1 < (int64_t)tl && !P.strict) {
+        const int64_t j = sg0 + lane;
+        uint64_t av = 0, yk = 0;
+        for (uint32_t w = 0; w < 1u << 16; w++) {  // a tile that never published its map
+          av = ld_agent(&P.aggv[j]);                // (resolved early) leaves its codes V_UNK
+          yk = ld_agent(&P.ywd[j - 1]);
+          if (__ballot(!(av & READY) || !(yk & READY)) == 0) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        const uint64_t keys = readlane64(yk, 0);
+        const uint64_t Ag = A - (uint64_t)((int64_t)t - sg0) * TILE;
+        cw = READY;
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+          const uint32_t rel = (uint32_t)(keys >> (16 * q)) & 0xFFFFu;
+          uint32_t code = V_UNK;
+          if (rel && (keys & READY)) {
+            uint64_t vq = Ag + rel - 1, dummy = 0;
+            if (eval_tiles(vq, sg0, SG, av, yk, dummy) == SG && vq - (Ag + (uint64_t)SG * TILE) < 0xFFF0ull)
+              code = (uint32_t)(vq - (Ag + (uint64_t)SG * TILE));
+          }
+          cw |= (uint64_t)code << (16 * q);
+        }
+      }
+      if (lane == 0) st_agent(&P.sagg[sg], cw);
+    };
+
     uint64_t x = e0;
+    bool agg_done = first || P.strict;
+    if (!agg_done) {
+      // publish agg_t before looking back: Y_{t-1} comes from a tile processed concurrently,
+      // and a map published late would stall every successor composing through this tile
+      for (uint32_t spin = 0; spin <= 4096; spin++) {
+        const uint64_t yk = uniform64(ld_agent(&P.ywd[t - 1]));
+        if (yk & READY) { publish_agg(yk); agg_done = true; break; }
+        STAT(ST_Y_SPINS, 1);
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    bool sg_counted = false;
+    if (agg_done) { sg_agg_done(); sg_counted = true; }
     if (!first) {
       uint32_t nap = 1;
+      int64_t cur = -1;  // tile whose exact exit v is known (-1: none found yet)
+      uint64_t v = 0;
+      bool force_tile = false;
       for (uint32_t spin = 0;; spin++) {
-        const int64_t j = (int64_t)t - 1 - (int64_t)lane;
-        const bool inr = j >= (int64_t)tf;
-        const uint64_t vi = inr ? ld_agent(&P.inclx[j]) : 0ull;
-        const uint64_t im = __ballot(vi != 0);
-        bool ok = false;
         STAT(ST_LB_ITERS, 1);
-        if (!im) STAT(ST_LB_NOINCL, 1);
-        if (im) {
-          const uint32_t ist = (uint32_t)__builtin_ctzll(im);
+        if (cur < 0) {  // A: nearest published exact exit
+          const int64_t lo0 = (int64_t)umax64(tf, (uint64_t)sg0);
+          {
+            const int64_t j = (int64_t)t - 1 - (int64_t)lane;
+            const uint64_t vi = j >= lo0 ? ld_agent(&P.inclx[j]) : 0ull;
+            const uint64_t im = __ballot(vi != 0);
+            if (im) {
+              const uint32_t ist = (uint32_t)__builtin_ctzll(im);
+              cur = (int64_t)t - 1 - ist;
+              v = readlane64(vi, ist) - 1;
+            }
+          }
+          if (cur < 0 && sg0 - 1 >= (int64_t)tf) {  // last tiles of the 64 previous groups
+            const int64_t b = SG * (sg - (int64_t)lane) - 1;
+            const uint64_t vi = b >= (int64_t)tf ? ld_agent(&P.inclx[b]) : 0ull;
+            const uint64_t im = __ballot(vi != 0);
+            if (im) {
+              const uint32_t ist = (uint32_t)__builtin_ctzll(im);
+              cur = SG * (sg - (int64_t)ist) - 1;
+              v = readlane64(vi, ist) - 1;
+            } else if (SG * (sg - 63) - 1 <= (int64_t)tf) {
+              const uint64_t vf = uniform64(ld_agent(&P.inclx[tf]));
+              if (vf) { cur = (int64_t)tf; v = vf - 1; }
+            }
+          }
+          if (cur < 0) STAT(ST_LB_NOINCL, 1);
+        }
+        if (P.strict && cur != (int64_t)t - 1) cur = -1;
+        // B: evaluate forward from tile cur+1, publishing every exit derived (helping)
+        while (cur >= 0 && cur < (int64_t)t - 1) {
+          if (!force_tile && (cur + 1) % SG == 0 && cur + SG <= (int64_t)t - 1) {
+            // whole super-groups k0 .. k0+m-1
+            const int64_t k0 = (cur + 1) / SG;
+            const uint32_t m = (uint32_t)min((int64_t)64, ((int64_t)t - 1 - cur) / SG);
+            const int64_t gk = k0 + lane;
+            const bool inr = lane < m;
+            const uint64_t vi = inr ? ld_agent(&P.inclx[SG * gk + SG - 1]) : 0ull;
+            const uint64_t im = __ballot(vi != 0);
+            if (im) {
+              const uint32_t hi = 63u - (uint32_t)__builtin_clzll(im);
+              cur = SG * (k0 + hi) + SG - 1;
+              v = readlane64(vi, hi) - 1;
+              continue;
+            }
+            const uint64_t sa = inr ? ld_agent(&P.sagg[gk]) : 0ull;
+            const uint64_t sk = inr ? ld_agent(&P.ywd[SG * gk - 1]) : 0ull;
+            uint32_t i = 0;
+            uint64_t mine = 0;
+            for (; i < m; i++) {
+              const uint64_t Ag = A - (uint64_t)((int64_t)t - SG * (k0 + (int64_t)i)) * TILE;
+              const uint64_t Aend = Ag + (uint64_t)SG * TILE;
+              if (v < Aend) {
+                if (v >= Ag + TILE) break;  // lands inside the group: tile level
+                const uint64_t ai = readlane64(sa, i), yi = readlane64(sk, i);
+                if (!(ai & READY) || !(yi & READY)) break;
+                const uint64_t rel = v - Ag + 1;
+                uint32_t code = V_UNK;
+#pragma unroll
+                for (int q = 0; q < 3; q++)
+                  if (((yi >> (16 * q)) & 0xFFFFu) == rel) code = (uint32_t)(ai >> (16 * q)) & 0xFFFFu;
+                if (code == V_UNK) break;
+                v = uniform64(Aend + code);
+              }
+              if (lane == i) mine = v + 1;
+            }
+            if (lane < i) st_agent(&P.inclx[SG * gk + SG - 1], mine);
+            if (i > 0) cur = SG * (k0 + (int64_t)i) - 1;
+            if (i < m) force_tile = true;  // next group goes tile by tile
+            continue;
+          }
+          // tile level, up to the end of the super-group holding tile cur+1
+          const int64_t j0 = cur + 1;
+          const uint32_t n = (uint32_t)min((int64_t)(SG - j0 % SG), (int64_t)t - 1 - cur);
+          const int64_t j = j0 + lane;
+          const bool inr = lane < n;
+          const uint64_t vi = inr ? ld_agent(&P.inclx[j]) : 0ull;
+          const uint64_t im = __ballot(vi != 0);
+          if (im) {  // someone already got further: jump to the newest published exit
+            const uint32_t hi = 63u - (uint32_t)__builtin_clzll(im);
+            cur = j0 + hi;
+            v = readlane64(vi, hi) - 1;
+            if ((cur + 1) % SG == 0) force_tile = false;
+            continue;
+          }
           uint64_t av = 0, yk = 0;
-          if (lane < ist && j > (int64_t)tf && !P.strict) {
+          if (inr && !P.strict) {
             av = ld_agent(&P.aggv[j]);
             if (av & READY) yk = ld_agent(&P.ywd[j - 1]);
           }
-          uint64_t xv = readlane64(vi, ist) - 1;
-          ok = true;
-          for (int32_t i = (int32_t)ist - 1; i >= 0 && ok; i--) {
-            const uint64_t Aj = A - (uint64_t)(i + 1) * TILE;
-            if (xv >= Aj + TILE) continue;  // passes over tile j (also: chain already ended)
-            const uint64_t ai = readlane64(av, (uint32_t)i), yi = readlane64(yk, (uint32_t)i);
-            if (!(ai & READY) || !(yi & READY)) { ok = false; STAT(ST_LB_NOAGG, 1); break; }
-            const uint64_t rel = xv - Aj + 1;
-            uint32_t code = V_UNK;
-            bool hit = false;
-#pragma unroll
-            for (int k = 0; k < 3; k++)
-              if (((yi >> (16 * k)) & 0xFFFFu) == rel) { code = (uint32_t)(ai >> (16 * k)) & 0xFFFFu; hit = true; }
-            if (code == V_UNK) {
-              STAT(hit ? ST_LB_VUNK : ST_LB_KEYMISS, 1);
-              ok = false;
-              break;
-            }
-            xv = Aj + TILE + code;
-          }
-          if (ok) { x = xv; STAT(ist ? ST_LB_OKN : ST_LB_OK0, 1); }
+          uint64_t mine = 0;
+          const uint32_t k = eval_tiles(v, j0, n, av, yk, mine);
+          if (lane < k) st_agent(&P.inclx[j], mine);
+          if (k == 0) { STAT(ST_LB_NOAGG, 1); break; }
+          cur = j0 + k - 1;
+          if ((cur + 1) % SG == 0) force_tile = false;
+          if (k < n) break;  // stuck on a missing map: retry after a nap
         }
-        if (ok) break;
+        if (cur == (int64_t)t - 1) { x = v; STAT(ST_LB_OKN, 1); break; }
+        if (!agg_done) {
+          const uint64_t yk = uniform64(ld_agent(&P.ywd[t - 1]));
+          if (yk & READY) { publish_agg(yk); agg_done = true; }
+          if (agg_done && !sg_counted) { sg_agg_done(); sg_counted = true; }
+        }
         if (spin > SPIN_MAX) {
           if (lane == 0) atomicOr(P.overflow, 2u);
           x = MARK_TERM | vs;
@@ -494,6 +658,7 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
         nap = nap < 8 ? nap * 2 : 8;
       }
     }
+    if (!sg_counted) sg_agg_done();
     x = uniform64(x);
     STAT(ST_TILES, 1);
     if (x >= ve) STAT(ST_PASS, 1);
@@ -529,10 +694,10 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
           // mark the path: after level r the marked set is {J^k(n0) : k < 2^(r+1)}
 #pragma unroll
           for (int c = 0; c < 4; c++) mark[lane * 4 + c] = 0;
-          __syncthreads();
+          wsync();
           if (lane == 0) mark[n0] = 1;
           for (int r = 0; r < LEV - 1; r++) {
-            __syncthreads();
+            wsync();
             uint32_t tg[4];
             bool mk[4];
 #pragma unroll
@@ -540,12 +705,12 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
               mk[c] = mark[lane * 4 + c] != 0;
               tg[c] = jmp[r][lane * 4 + c];
             }
-            __syncthreads();
+            wsync();
 #pragma unroll
             for (int c = 0; c < 4; c++)
               if (mk[c]) mark[tg[c]] = 1;
           }
-          __syncthreads();
+          wsync();
 #pragma unroll
           for (int c = 0; c < NC; c++) {
             const uint32_t n = lane * 4 + c;
@@ -572,7 +737,7 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
           cur = uniform64(h.succ);
         }
       }
-      __syncthreads();
+      wsync();
     }
 
     // ---- 5b. lane walks: delivered frames of the path inside my bytes --------------------
@@ -616,38 +781,115 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
       if (!early) st_agent(&P.inclx[t], exit_t + 1);
       st_agent(&P.aggc[t], (uint64_t)count_t + 1);
     }
+    {  // the last tile of the super-group to publish its count publishes the group sum
+      uint32_t old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(&P.sgc_cnt[sg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = readlane32(old, 0);
+      if (old == sgsize - 1) {
+        uint64_t c = 0;
+        for (;;) {  // counts are value + 1: wait until all 64 are visible
+          c = lane < sgsize ? ld_agent(&P.aggc[sg0 + lane]) : 1ull;
+          if (__ballot(c == 0) == 0) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        const uint64_t sum = wave_sum64(c - 1);
+        if (lane == 0) st_agent(&P.scnt[sg], sum + 1);
+      }
+    }
 
     TMARK(ST_T_PATH);
     // ---- 5c. count look-back -> first output slot ------------------------------------------
-    // Decoupled look-back over sums: windows of 64 predecessors, moving back while a whole
-    // window has counts but no inclusive prefix.
+    // Same shape as the exit look-back: the nearest inclusive prefix among this group's tiles
+    // or the last tiles of the 64 previous groups, then sums forward by whole groups (scnt)
+    // and tiles (aggc), publishing the inclusive prefix of every boundary passed (helping).
     uint64_t base = 0;
     if (t > 0) {
-      uint64_t csum = 0;
-      int64_t top = (int64_t)t - 1;
       uint32_t nap = 1;
+      int64_t cur = -2;  // tile whose inclusive prefix v is known (-1: virtual tile before 0)
+      uint64_t v = 0;
+      bool force_tile = false;
       for (uint32_t spin = 0;;) {
-        const int64_t pi = top - (int64_t)lane;
-        uint64_t vi = 0, va = 0;
-        if (pi >= 0) {
-          vi = ld_agent(&P.inclc[pi]);
-          if (!vi) va = ld_agent(&P.aggc[pi]);
-        } else if (pi == -1) {
-          vi = 1;  // virtual inclusive prefix 0 before tile 0
-        }
-        const uint64_t im = __ballot(vi != 0);
-        const uint32_t ist = im ? (uint32_t)__builtin_ctzll(im) : 64u;
-        const uint64_t am = __ballot(va != 0);
-        const uint64_t need = ist >= 64 ? ~0ull : ((1ull << ist) - 1);
-        if ((am & need) == need) {
-          csum += wave_sum64(lane < ist ? va - 1 : 0ull);
-          if (ist < 64) {
-            base = csum + readlane64(vi, ist) - 1;
-            break;
+        if (cur < -1) {
+          {
+            const int64_t j = (int64_t)t - 1 - (int64_t)lane;
+            const uint64_t vi = j >= sg0 ? ld_agent(&P.inclc[j]) : 0ull;
+            const uint64_t im = __ballot(vi != 0);
+            if (im) {
+              const uint32_t ist = (uint32_t)__builtin_ctzll(im);
+              cur = (int64_t)t - 1 - ist;
+              v = readlane64(vi, ist) - 1;
+            }
           }
-          top -= 64;
-          continue;
+          if (cur < -1) {
+            const int64_t b = SG * (sg - (int64_t)lane) - 1;
+            const uint64_t vi = b >= 0 ? ld_agent(&P.inclc[b]) : (b == -1 ? 1ull : 0ull);
+            const uint64_t im = __ballot(vi != 0);
+            if (im) {
+              const uint32_t ist = (uint32_t)__builtin_ctzll(im);
+              cur = SG * (sg - (int64_t)ist) - 1;
+              v = readlane64(vi, ist) - 1;
+            }
+          }
         }
+        while (cur >= -1 && cur < (int64_t)t - 1) {
+          if (!force_tile && (cur + 1) % SG == 0 && cur + SG <= (int64_t)t - 1) {
+            const int64_t k0 = (cur + 1) / SG;
+            const uint32_t m = (uint32_t)min((int64_t)64, ((int64_t)t - 1 - cur) / SG);
+            const int64_t gk = k0 + lane;
+            const bool inr = lane < m;
+            const uint64_t vi = inr ? ld_agent(&P.inclc[SG * gk + SG - 1]) : 0ull;
+            const uint64_t im = __ballot(vi != 0);
+            if (im) {
+              const uint32_t hi = 63u - (uint32_t)__builtin_clzll(im);
+              cur = SG * (k0 + hi) + SG - 1;
+              v = readlane64(vi, hi) - 1;
+              continue;
+            }
+            const uint64_t sc = inr ? ld_agent(&P.scnt[gk]) : 0ull;
+            const uint64_t am = __ballot(sc != 0);
+            const uint32_t k = (~am) ? (uint32_t)__builtin_ctzll(~am) : 64u;
+            const uint32_t kk = k < m ? k : m;
+            if (kk == 0) { force_tile = true; continue; }
+            const uint64_t c = lane < kk ? sc - 1 : 0ull;
+            uint64_t pre = c;  // inclusive prefix over lanes
+#pragma unroll
+            for (uint32_t d = 1; d < WAVE; d <<= 1) {
+              const uint64_t o = shfl_up64(pre, d);
+              if (lane >= d) pre += o;
+            }
+            if (lane < kk) st_agent(&P.inclc[SG * gk + SG - 1], v + pre + 1);
+            v += readlane64(pre, kk - 1);
+            cur = SG * (k0 + (int64_t)kk) - 1;
+            if (kk < m) force_tile = true;
+            continue;
+          }
+          const int64_t j0 = cur + 1;
+          const uint32_t n = (uint32_t)min((int64_t)(SG - j0 % SG), (int64_t)t - 1 - cur);
+          const int64_t j = j0 + lane;
+          const bool inr = lane < n;
+          const uint64_t vi = inr ? ld_agent(&P.inclc[j]) : 0ull;
+          const uint64_t im = __ballot(vi != 0);
+          if (im) {
+            const uint32_t hi = 63u - (uint32_t)__builtin_clzll(im);
+            cur = j0 + hi;
+            v = readlane64(vi, hi) - 1;
+            if ((cur + 1) % SG == 0) force_tile = false;
+            continue;
+          }
+          const uint64_t va = inr ? ld_agent(&P.aggc[j]) : 0ull;
+          const uint64_t am = __ballot(va != 0);
+          const uint32_t k = (~am) ? (uint32_t)__builtin_ctzll(~am) : 64u;
+          const uint32_t kk = k < n ? k : n;
+          if (kk == 0) break;
+          const uint32_t c = lane < kk ? (uint32_t)(va - 1) : 0u;
+          const uint32_t pre = wave_incl_scan32(c);
+          if (lane < kk) st_agent(&P.inclc[j], v + pre + 1);
+          v += readlane32(pre, kk - 1);
+          cur = j0 + kk - 1;
+          if ((cur + 1) % SG == 0) force_tile = false;
+          if (kk < n) break;
+        }
+        if (cur == (int64_t)t - 1) { base = v; break; }
         if (++spin > SPIN_MAX) {
           if (lane == 0) atomicOr(P.overflow, 2u);
           break;
@@ -724,6 +966,12 @@ __global__ __launch_bounds__(64) void decode_tiles(DecodeParams P) {
       P.tile_count[t] = count_t;
     }
     TMARK(ST_T_EMIT);
+  }
+  if (PROF) {
+    acc[ST_OVF_LANES] = wave_sum32(novf);
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < (int)ST_NSTATS; i++) atomicAdd(P.stats + i, (unsigned long long)acc[i]);
   }
 }
 
@@ -861,10 +1109,18 @@ extern "C" hipError_t drp_launch_tile_prefix(uint32_t B, const uint64_t *stream_
   return hipGetLastError();
 }
 
+extern "C" uint32_t drp_decode_waves_per_group(void) { return WPG; }
+
 extern "C" hipError_t drp_launch_decode(uint32_t B, const DecodeParams *P, uint32_t grid, hipStream_t st) {
   switch (B) {
-    case 64: hipLaunchKernelGGL(decode_tiles<64>, dim3(grid), dim3(64), 0, st, *P); break;
-    case 128: hipLaunchKernelGGL(decode_tiles<128>, dim3(grid), dim3(64), 0, st, *P); break;
+    case 64:
+      if (P->stats) hipLaunchKernelGGL((decode_tiles<64, true>), dim3(grid), dim3(64 * WPG), 0, st, *P);
+      else hipLaunchKernelGGL((decode_tiles<64, false>), dim3(grid), dim3(64 * WPG), 0, st, *P);
+      break;
+    case 128:
+      if (P->stats) hipLaunchKernelGGL((decode_tiles<128, true>), dim3(grid), dim3(64 * WPG), 0, st, *P);
+      else hipLaunchKernelGGL((decode_tiles<128, false>), dim3(grid), dim3(64 * WPG), 0, st, *P);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

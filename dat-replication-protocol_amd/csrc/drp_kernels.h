@@ -29,6 +29,9 @@ struct DecodeParams {
   uint64_t *aggc;   // delivered frames of tile t + 1
   uint64_t *inclc;  // frames of tiles <= t + 1
   uint64_t *tile_exit, *tile_base, *tile_count;  // per-tile records for finalize
+  // per super-group (64 tiles): completion counters, composed map, count sum (value + 1)
+  uint32_t *sgc_agg, *sgc_cnt;
+  uint64_t *sagg, *scnt;
   // per-stream scratch
   uint64_t *payload_err;  // min absolute index of a malformed Change
   uint64_t *scount;       // [2*s] changes, [2*s+1] blobs
@@ -56,6 +59,7 @@ extern "C" {
 hipError_t drp_launch_tile_prefix(uint32_t B, const uint64_t *stream_off, uint64_t nstreams,
                                   uint64_t *tile_prefix, hipStream_t st);
 hipError_t drp_launch_decode(uint32_t B, const drp::DecodeParams *P, uint32_t grid, hipStream_t st);
+uint32_t drp_decode_waves_per_group(void);  // tiles (waves) per workgroup; grid counts groups
 hipError_t drp_launch_finalize(const uint8_t *bytes, const uint64_t *stream_off, uint64_t nstreams,
                                const uint64_t *tile_prefix, const uint64_t *tile_exit,
                                const uint64_t *tile_base, const uint64_t *tile_count,
