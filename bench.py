@@ -221,11 +221,11 @@ def main():
             "config": {"workload": "C2: 100M Change frames x 86 B (64 B values), one 8.6 GB stream per GPU",
                        "frames_per_gpu": nframes, "wire_bytes_per_gpu": nframes * FRAME,
                        "parallelism": f"independent streams, {world} GPU(s); RCCL all-gather of stream stats",
-                       "tile_bytes": args.tile or 4096},
+                       "tile_bytes": args.tile or 8192},
             "wire_GBps": wire_total / elapsed / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                         "kernel": f"decode_tiles<{(args.tile or 4096) // 64}>", "kernel_ms": dec_avg_s * 1e3,
+                         "kernel": f"decode_tiles<{(args.tile or 8192) // 64}>", "kernel_ms": dec_avg_s * 1e3,
                          "bytes_per_launch": b_dec,
                          "bytes_model": "W + 13*frames + 49*changes (86+13+49 = 148 B/frame)"},
             "step_ms_hip_events": ev_ms / args.steps,

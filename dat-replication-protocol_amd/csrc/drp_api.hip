@@ -75,7 +75,7 @@ struct drp_ctx {
   int device = 0;
   hipStream_t st = nullptr;
   hipEvent_t ev[4] = {};
-  uint32_t B = 64;
+  uint32_t B = 128;
   int strict = 0;
   int cus = 256;
   uint32_t waves_per_cu = 16;
@@ -154,7 +154,7 @@ int drp_last_timing(drp_ctx *c, drp_timing *out) {
 
 int drp_set_tile(drp_ctx *c, uint32_t tile_bytes) {
   if (!c) return DRP_E_INVAL;
-  if (tile_bytes == 0) tile_bytes = 4096;
+  if (tile_bytes == 0) tile_bytes = 8192;
   if (tile_bytes != 4096 && tile_bytes != 8192) return DRP_E_INVAL;
   c->B = tile_bytes / 64;
   return DRP_OK;
@@ -178,9 +178,9 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.ntiles_max = nbytes / tile + 2 * ns + 2;
   size_t o = 0;
   L.tile_prefix = o; o += al((ns + 1) * 8);
-  L.rec = o; o += al(5 * L.ntiles_max * 8);    // ywd, aggv, inclx, aggc, inclc (zeroed per call)
+  L.rec = o; o += al(6 * L.ntiles_max * 8);    // ywd, aggv, aggn, inclx, aggc, inclc (zeroed per call)
   L.nsg = L.ntiles_max / 64 + 2;
-  L.sgrp = o; o += al(L.nsg * 24);             // sgc_agg+sgc_cnt (u32 x2), sagg, scnt (zeroed)
+  L.sgrp = o; o += al(L.nsg * 32);             // sgc_agg+sgc_cnt (u32 x2), sagg, saggn, scnt (zeroed)
   L.tiles = o; o += al(3 * L.ntiles_max * 8);  // exit, base, count
   L.perr = o; o += al(ns * 8);
   L.scount = o; o += al(2 * ns * 8);
@@ -214,9 +214,9 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
 
   hipStream_t st = c->st;
   CHK(hipEventRecord(c->ev[0], st));
-  CHK(hipMemsetAsync(rec, 0, 5 * NT * 8, st));
+  CHK(hipMemsetAsync(rec, 0, 6 * NT * 8, st));
   uint8_t *sgrp = c->scratch.at<uint8_t>(L.sgrp);
-  CHK(hipMemsetAsync(sgrp, 0, L.nsg * 24, st));
+  CHK(hipMemsetAsync(sgrp, 0, L.nsg * 32, st));
   CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
   CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
   CHK(hipMemsetAsync(ctrl, 0, 16, st));
@@ -249,10 +249,12 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
   P.inclx = rec + 2 * NT;
   P.aggc = rec + 3 * NT;
   P.inclc = rec + 4 * NT;
+  P.aggn = rec + 5 * NT;
   P.sgc_agg = reinterpret_cast<uint32_t *>(sgrp);
   P.sgc_cnt = P.sgc_agg + L.nsg;
   P.sagg = reinterpret_cast<uint64_t *>(sgrp + L.nsg * 8);
-  P.scnt = P.sagg + L.nsg;
+  P.saggn = P.sagg + L.nsg;
+  P.scnt = P.saggn + L.nsg;
   P.tile_exit = tiles;
   P.tile_base = tiles + NT;
   P.tile_count = tiles + 2 * NT;
@@ -300,9 +302,10 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
     CHK(hipMemcpy(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost));
     static const char *nm[] = {"lb_iters", "lb_noincl", "lb_noagg", "lb_keymiss", "lb_vunk", "lb_ok0", "lb_okn",
                                "y_spins", "serial", "cnt_spins", "y_count", "agg_unk", "tiles", "pass", "ovf_pos",
-                               "t_grab", "t_stage", "t_dp", "t_y", "t_lb", "t_path", "t_cnt", "t_emit"};
+                               "t_grab", "t_stage", "t_dp", "t_y", "t_lb", "t_path", "t_cnt", "t_emit",
+                               "ev_tiles", "ev_sg", "skips", "phaseA"};
     fprintf(stderr, "[drp-stats]");
-    for (int i = 0; i < 23; i++) fprintf(stderr, " %s=%llu", nm[i], hs[i]);
+    for (int i = 0; i < 27; i++) fprintf(stderr, " %s=%llu", nm[i], hs[i]);
     fprintf(stderr, " decode_ms=%.3f\n", c->timing.decode_ms);
     hipFree(dstats);
   }

@@ -48,7 +48,7 @@ enum : uint32_t {
   ST_LB_ITERS = 0, ST_LB_NOINCL, ST_LB_NOAGG, ST_LB_KEYMISS, ST_LB_VUNK, ST_LB_OK0, ST_LB_OKN,
   ST_Y_SPINS, ST_SERIAL, ST_CNT_SPINS, ST_Y_COUNT, ST_AGG_UNK, ST_TILES, ST_PASS, ST_OVF_LANES,
   ST_T_GRAB, ST_T_STAGE, ST_T_DP, ST_T_Y, ST_T_LB, ST_T_PATH, ST_T_CNT, ST_T_EMIT,
-  ST_NSTATS
+  ST_EV_TILES, ST_EV_SG, ST_SKIPS, ST_PHASEA, ST_NSTATS
 };
 #define STAT(k, v)                         \
   do {                                     \
@@ -121,6 +121,7 @@ struct WaveLds {
   uint8_t jmp[LEV][256];      // doubling levels of the lane graph
   uint8_t mark[256];
   int32_t entry[64];          // per lane: entry of the tile's path (tile-relative), -1 none
+  uint16_t nsum[2][256];      // doubling sums of delivered frames along the lane graph
 };
 
 // Orders this wave's LDS accesses (a wave's DS instructions execute in order; this keeps
@@ -154,6 +155,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
   uint8_t(*const jmp)[256] = wl[wid].jmp;
   uint8_t *const mark = wl[wid].mark;
   int32_t *const entry = wl[wid].entry;
+  uint16_t(*const nsum)[256] = wl[wid].nsum;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
 
   // lm accessors: lane m, mask k (0..NC-1 class, NC dead, NC+1 live), word w
@@ -377,28 +379,59 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     };
 
     // ---- 3. lane graph + pointer doubling ------------------------------------------------
-    uint32_t J[4];
+    // Delivered frames of a path inside one lane, walking from position q of lane m up to
+    // the lane's end (or the path's end). Used per graph edge and for keys / the entry.
+    auto lane_count = [&](uint64_t q) -> uint32_t {
+      const uint32_t m = (uint32_t)(q - A) / B;
+      const uint64_t mh = umin64(A + (uint64_t)(m + 1) * B, ve);
+      uint32_t nd = 0;
+      for (uint64_t cur = q; cur < mh;) {
+        const Hdr h = parse_hdr_lds(buf, A, cur, se);
+        nd += hdr_delivered(h) ? 1u : 0u;
+        if (h.kind != H_VALID) break;
+        cur = h.succ;
+      }
+      return nd;
+    };
+    // Node (lane, class): edge to the node holding the class exit; edge weight = frames
+    // delivered in the lane the exit lands in (from the exit to that lane's end).
+    uint32_t J[4], Sm[4];
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       const uint32_t n = lane * 4 + c;
       uint32_t j = n;  // self loop: EXIT node, unused slot, or the special nodes 3 / 7
+      uint32_t w = 0;
       if ((uint32_t)c < ncls) {
         const uint64_t e = cex[c];
         exv[n] = e;
-        if (e < ve) j = resolve(e);
+        if (e < ve) {
+          j = resolve(e);
+          if (j != N_UNK) w = lane_count(e);
+        }
       }
       J[c] = j;
+      Sm[c] = w;
       jmp[0][n] = (uint8_t)j;
+      nsum[0][n] = (uint16_t)w;
     }
     for (int r = 1; r < LEV; r++) {
       wsync();
 #pragma unroll
       for (int c = 0; c < 4; c++) {
+        Sm[c] += nsum[(r - 1) & 1][J[c]];
         J[c] = jmp[r - 1][J[c]];
         jmp[r][lane * 4 + c] = (uint8_t)J[c];
+        nsum[r & 1][lane * 4 + c] = (uint16_t)Sm[c];
       }
     }
     wsync();
+    // frames delivered by the path entering at in-tile position q (valid only when the
+    // final node is not N_UNK); q's node n0 = resolve(q)
+    auto path_count = [&](uint64_t q, uint32_t n0) -> uint32_t {
+      uint32_t c = lane_count(q);
+      if (n0 != N_DEAD && n0 != N_UNK) c += nsum[(LEV - 1) & 1][n0];
+      return c;
+    };
     // J[c] = final node of my class c
 
     TMARK(ST_T_DP);
@@ -439,11 +472,11 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     // A tile that composes forward from a predecessor's inclusive exit also publishes the
     // exits it derives for the tiles in between ("helping"), so the frontier jumps ahead.
     auto publish_agg = [&](uint64_t yk) {
-      uint64_t aw = READY;
+      uint64_t aw = READY, nw = READY;
 #pragma unroll
       for (int k = 0; k < 3; k++) {
         const uint32_t rel = (uint32_t)(yk >> (16 * k)) & 0xFFFFu;
-        uint32_t code = V_UNK;
+        uint32_t code = V_UNK, cnt = 0;
         if (rel) {
           const uint64_t q = A + rel - 1;
           if (q >= vs && q < ve) {
@@ -452,37 +485,49 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
               const uint32_t f = jmp[LEV - 1][n];
               if (f != N_DEAD && f != N_UNK) {
                 const uint64_t e = exv[f];
-                if (e - (A + TILE) < 0xFFF0ull) code = (uint32_t)(e - (A + TILE));
+                if (e - (A + TILE) < 0xFFF0ull) {
+                  code = (uint32_t)(e - (A + TILE));
+                  cnt = path_count(q, n);
+                }
               }
             }
           }
         }
         if (rel && code == V_UNK) STAT(ST_AGG_UNK, 1);
         aw |= (uint64_t)code << (16 * k);
+        nw |= (uint64_t)cnt << (16 * k);
       }
-      if (lane == 0) st_agent(&P.aggv[t], aw);
+      if (lane == 0) {
+        st_agent(&P.aggn[t], nw);
+        st_agent(&P.aggv[t], aw);
+      }
     };
     TMARK(ST_T_Y);
     // Tile-level evaluation of the exact exit v through tiles j0 .. j0+n-1 of this stream
     // (lanes hold aggv / ywd of tile j0+lane). Returns how many tiles were passed; the exit
     // after tile j0+k is left in lane k's `mine` (value + 1).
-    auto eval_tiles = [&](uint64_t &v, int64_t j0, uint32_t n, uint64_t av, uint64_t yk,
-                          uint64_t &mine) -> uint32_t {
+    auto eval_tiles = [&](uint64_t &v, uint64_t &cn, int64_t j0, uint32_t n, uint64_t av, uint64_t an,
+                          uint64_t yk, uint64_t &mine, uint64_t &minec) -> uint32_t {
       uint32_t k = 0;
       for (; k < n; k++) {
         const uint64_t Aj = A - (uint64_t)((int64_t)t - (j0 + (int64_t)k)) * TILE;
+        uint32_t add = 0;
         if (v < Aj + TILE) {
-          const uint64_t ai = readlane64(av, k), yi = readlane64(yk, k);
-          if (!(ai & READY) || !(yi & READY)) break;
+          const uint64_t ai = readlane64(av, k), yi = readlane64(yk, k), ni = readlane64(an, k);
+          if (!(ai & READY) || !(yi & READY) || !(ni & READY)) break;
           const uint64_t rel = v - Aj + 1;
           uint32_t code = V_UNK;
 #pragma unroll
           for (int q = 0; q < 3; q++)
-            if (((yi >> (16 * q)) & 0xFFFFu) == rel) code = (uint32_t)(ai >> (16 * q)) & 0xFFFFu;
+            if (((yi >> (16 * q)) & 0xFFFFu) == rel) {
+              code = (uint32_t)(ai >> (16 * q)) & 0xFFFFu;
+              add = (uint32_t)(ni >> (16 * q)) & 0xFFFFu;
+            }
           if (code == V_UNK) break;
           v = uniform64(Aj + TILE + code);
         }
-        if (lane == k) mine = v + 1;
+        cn += add;
+        if (lane == k) { mine = v + 1; minec = (uint64_t)add + 1; }
       }
       return k;
     };
@@ -500,27 +545,33 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       uint64_t cw = READY | 0xFFFFFFFFFFFFull;  // all V_UNK
       if (sgsize == SG && sg0 > (int64_t)tf && sg0 + SG - 1 < (int64_t)tl && !P.strict) {
         const int64_t j = sg0 + lane;
-        uint64_t av = 0, yk = 0;
+        uint64_t av = 0, an = 0, yk = 0;
         for (uint32_t w = 0; w < 1u << 16; w++) {  // a tile that never published its map
           av = ld_agent(&P.aggv[j]);                // (resolved early) leaves its codes V_UNK
+          an = ld_agent(&P.aggn[j]);
           yk = ld_agent(&P.ywd[j - 1]);
-          if (__ballot(!(av & READY) || !(yk & READY)) == 0) break;
+          if (__ballot(!(av & READY) || !(yk & READY) || !(an & READY)) == 0) break;
           __builtin_amdgcn_s_sleep(2);
         }
         const uint64_t keys = readlane64(yk, 0);
         const uint64_t Ag = A - (uint64_t)((int64_t)t - sg0) * TILE;
         cw = READY;
+        uint64_t nw = READY;
 #pragma unroll
         for (int q = 0; q < 3; q++) {
           const uint32_t rel = (uint32_t)(keys >> (16 * q)) & 0xFFFFu;
           uint32_t code = V_UNK;
+          uint64_t cq = 0;
           if (rel && (keys & READY)) {
-            uint64_t vq = Ag + rel - 1, dummy = 0;
-            if (eval_tiles(vq, sg0, SG, av, yk, dummy) == SG && vq - (Ag + (uint64_t)SG * TILE) < 0xFFF0ull)
+            uint64_t vq = Ag + rel - 1, d0 = 0, d1 = 0;
+            if (eval_tiles(vq, cq, sg0, SG, av, an, yk, d0, d1) == SG &&
+                vq - (Ag + (uint64_t)SG * TILE) < 0xFFF0ull)
               code = (uint32_t)(vq - (Ag + (uint64_t)SG * TILE));
           }
           cw |= (uint64_t)code << (16 * q);
+          nw |= (code == V_UNK ? 0ull : cq) << (20 * q);
         }
+        if (lane == 0) st_agent(&P.saggn[sg], nw);
       }
       if (lane == 0) st_agent(&P.sagg[sg], cw);
     };
@@ -547,20 +598,22 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       for (uint32_t spin = 0;; spin++) {
         STAT(ST_LB_ITERS, 1);
         if (cur < 0) {  // A: nearest published exact exit
+          STAT(ST_PHASEA, 1);
           const int64_t lo0 = (int64_t)umax64(tf, (uint64_t)sg0);
+          const int64_t j = (int64_t)t - 1 - (int64_t)lane;
+          const int64_t b = SG * (sg - (int64_t)lane) - 1;  // last tiles of the 64 previous groups
+          const uint64_t vj = j >= lo0 ? ld_agent(&P.inclx[j]) : 0ull;
+          const uint64_t vb = b >= (int64_t)tf ? ld_agent(&P.inclx[b]) : 0ull;
           {
-            const int64_t j = (int64_t)t - 1 - (int64_t)lane;
-            const uint64_t vi = j >= lo0 ? ld_agent(&P.inclx[j]) : 0ull;
-            const uint64_t im = __ballot(vi != 0);
+            const uint64_t im = __ballot(vj != 0);
             if (im) {
               const uint32_t ist = (uint32_t)__builtin_ctzll(im);
               cur = (int64_t)t - 1 - ist;
-              v = readlane64(vi, ist) - 1;
+              v = readlane64(vj, ist) - 1;
             }
           }
-          if (cur < 0 && sg0 - 1 >= (int64_t)tf) {  // last tiles of the 64 previous groups
-            const int64_t b = SG * (sg - (int64_t)lane) - 1;
-            const uint64_t vi = b >= (int64_t)tf ? ld_agent(&P.inclx[b]) : 0ull;
+          if (cur < 0 && sg0 - 1 >= (int64_t)tf) {
+            const uint64_t vi = vb;
             const uint64_t im = __ballot(vi != 0);
             if (im) {
               const uint32_t ist = (uint32_t)__builtin_ctzll(im);
@@ -582,36 +635,50 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
             const uint32_t m = (uint32_t)min((int64_t)64, ((int64_t)t - 1 - cur) / SG);
             const int64_t gk = k0 + lane;
             const bool inr = lane < m;
-            const uint64_t vi = inr ? ld_agent(&P.inclx[SG * gk + SG - 1]) : 0ull;
+            // one round trip: every word this step may need is loaded together
+            uint64_t vi = 0, sa = 0, sn = 0, sk = 0;
+            if (inr) {
+              vi = ld_agent(&P.inclx[SG * gk + SG - 1]);
+              sa = ld_agent(&P.sagg[gk]);
+              sn = ld_agent(&P.saggn[gk]);
+              sk = ld_agent(&P.ywd[SG * gk - 1]);
+            }
             const uint64_t im = __ballot(vi != 0);
             if (im) {
               const uint32_t hi = 63u - (uint32_t)__builtin_clzll(im);
               cur = SG * (k0 + hi) + SG - 1;
               v = readlane64(vi, hi) - 1;
+              STAT(ST_SKIPS, 1);
               continue;
             }
-            const uint64_t sa = inr ? ld_agent(&P.sagg[gk]) : 0ull;
-            const uint64_t sk = inr ? ld_agent(&P.ywd[SG * gk - 1]) : 0ull;
             uint32_t i = 0;
-            uint64_t mine = 0;
+            uint64_t mine = 0, minec = 0;
             for (; i < m; i++) {
               const uint64_t Ag = A - (uint64_t)((int64_t)t - SG * (k0 + (int64_t)i)) * TILE;
               const uint64_t Aend = Ag + (uint64_t)SG * TILE;
+              uint64_t add = 0;
               if (v < Aend) {
                 if (v >= Ag + TILE) break;  // lands inside the group: tile level
-                const uint64_t ai = readlane64(sa, i), yi = readlane64(sk, i);
-                if (!(ai & READY) || !(yi & READY)) break;
+                const uint64_t ai = readlane64(sa, i), yi = readlane64(sk, i), ni = readlane64(sn, i);
+                if (!(ai & READY) || !(yi & READY) || !(ni & READY)) break;
                 const uint64_t rel = v - Ag + 1;
                 uint32_t code = V_UNK;
 #pragma unroll
                 for (int q = 0; q < 3; q++)
-                  if (((yi >> (16 * q)) & 0xFFFFu) == rel) code = (uint32_t)(ai >> (16 * q)) & 0xFFFFu;
+                  if (((yi >> (16 * q)) & 0xFFFFu) == rel) {
+                    code = (uint32_t)(ai >> (16 * q)) & 0xFFFFu;
+                    add = (ni >> (20 * q)) & 0xFFFFFull;
+                  }
                 if (code == V_UNK) break;
                 v = uniform64(Aend + code);
               }
-              if (lane == i) mine = v + 1;
+              if (lane == i) { mine = v + 1; minec = add + 1; }
             }
-            if (lane < i) st_agent(&P.inclx[SG * gk + SG - 1], mine);
+            STAT(ST_EV_SG, i);
+            if (lane < i) {  // helping: exit of each group's last tile, and the group's count
+              st_agent(&P.inclx[SG * gk + SG - 1], mine);
+              st_agent(&P.scnt[gk], minec);
+            }
             if (i > 0) cur = SG * (k0 + (int64_t)i) - 1;
             if (i < m) force_tile = true;  // next group goes tile by tile
             continue;
@@ -621,23 +688,31 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           const uint32_t n = (uint32_t)min((int64_t)(SG - j0 % SG), (int64_t)t - 1 - cur);
           const int64_t j = j0 + lane;
           const bool inr = lane < n;
-          const uint64_t vi = inr ? ld_agent(&P.inclx[j]) : 0ull;
+          uint64_t vi = 0, av = 0, an = 0, yk = 0;
+          if (inr) {  // one round trip for the whole chunk
+            vi = ld_agent(&P.inclx[j]);
+            if (!P.strict) {
+              av = ld_agent(&P.aggv[j]);
+              an = ld_agent(&P.aggn[j]);
+              yk = ld_agent(&P.ywd[j - 1]);
+            }
+          }
           const uint64_t im = __ballot(vi != 0);
           if (im) {  // someone already got further: jump to the newest published exit
             const uint32_t hi = 63u - (uint32_t)__builtin_clzll(im);
             cur = j0 + hi;
             v = readlane64(vi, hi) - 1;
             if ((cur + 1) % SG == 0) force_tile = false;
+            STAT(ST_SKIPS, 1);
             continue;
           }
-          uint64_t av = 0, yk = 0;
-          if (inr && !P.strict) {
-            av = ld_agent(&P.aggv[j]);
-            if (av & READY) yk = ld_agent(&P.ywd[j - 1]);
+          uint64_t mine = 0, minec = 0, cdummy = 0;
+          const uint32_t k = eval_tiles(v, cdummy, j0, n, av, an, yk, mine, minec);
+          STAT(ST_EV_TILES, k);
+          if (lane < k) {  // helping: exact exit and frame count of tiles j0 .. j0+k-1
+            st_agent(&P.inclx[j], mine);
+            st_agent(&P.aggc[j], minec);
           }
-          uint64_t mine = 0;
-          const uint32_t k = eval_tiles(v, j0, n, av, yk, mine);
-          if (lane < k) st_agent(&P.inclx[j], mine);
           if (k == 0) { STAT(ST_LB_NOAGG, 1); break; }
           cur = j0 + k - 1;
           if ((cur + 1) % SG == 0) force_tile = false;
@@ -666,19 +741,43 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     TMARK(ST_T_LB);
     // the exact exit is known right away unless the path ends inside the tile / is serial:
     // publish it before the lane walks so successors' look-backs advance sooner
-    bool early = false;
-    uint32_t n0 = N_DEAD;
+    bool early = false, early_cnt = false;
+    uint32_t n0 = N_DEAD, gcount = 0;
     if (x >= ve) {
-      early = true;
+      early = early_cnt = true;
     } else {
       n0 = uniform32(resolve(x));
+      uint32_t f = n0;
       if (n0 != N_DEAD && n0 != N_UNK) {
-        const uint32_t f = jmp[LEV - 1][n0];
+        f = jmp[LEV - 1][n0];
         early = (f != N_DEAD && f != N_UNK);
         if (early && lane == 0) st_agent(&P.inclx[t], exv[f] + 1);
       }
+      if (n0 != N_UNK && f != N_UNK) {  // frame count of the path from x, from the graph
+        early_cnt = true;
+        gcount = uniform32(path_count(x, n0));
+      }
     }
     if (x >= ve && lane == 0) st_agent(&P.inclx[t], x + 1);
+    auto count_published = [&]() {  // the last tile of the group to get here sums its counts
+      uint32_t old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(&P.sgc_cnt[sg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = readlane32(old, 0);
+      if (old == sgsize - 1) {
+        uint64_t c = 0;
+        for (;;) {  // counts are value + 1: wait until all 64 are visible
+          c = lane < sgsize ? ld_agent(&P.aggc[sg0 + lane]) : 1ull;
+          if (__ballot(c == 0) == 0) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        const uint64_t sum = wave_sum64(c - 1);
+        if (lane == 0) st_agent(&P.scnt[sg], sum + 1);
+      }
+    };
+    if (early_cnt) {
+      if (lane == 0) st_agent(&P.aggc[t], (uint64_t)gcount + 1);
+      count_published();
+    }
 
     // ---- 5a. this tile's path: entries per lane -------------------------------------------
     bool graph_exit = false;
@@ -777,24 +876,12 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     }
     exit_t = uniform64(exit_t);
     count_t = uniform32(count_t);
-    if (lane == 0) {
-      if (!early) st_agent(&P.inclx[t], exit_t + 1);
-      st_agent(&P.aggc[t], (uint64_t)count_t + 1);
-    }
-    {  // the last tile of the super-group to publish its count publishes the group sum
-      uint32_t old = 0;
-      if (lane == 0) old = __hip_atomic_fetch_add(&P.sgc_cnt[sg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      old = readlane32(old, 0);
-      if (old == sgsize - 1) {
-        uint64_t c = 0;
-        for (;;) {  // counts are value + 1: wait until all 64 are visible
-          c = lane < sgsize ? ld_agent(&P.aggc[sg0 + lane]) : 1ull;
-          if (__ballot(c == 0) == 0) break;
-          __builtin_amdgcn_s_sleep(2);
-        }
-        const uint64_t sum = wave_sum64(c - 1);
-        if (lane == 0) st_agent(&P.scnt[sg], sum + 1);
-      }
+    if (lane == 0 && !early) st_agent(&P.inclx[t], exit_t + 1);
+    if (early_cnt) {
+      if (count_t != gcount && lane == 0) atomicOr(P.overflow, 4u);
+    } else {
+      if (lane == 0) st_agent(&P.aggc[t], (uint64_t)count_t + 1);
+      count_published();
     }
 
     TMARK(ST_T_PATH);

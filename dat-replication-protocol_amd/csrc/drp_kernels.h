@@ -25,13 +25,14 @@ struct DecodeParams {
   // per-tile look-back words (value + 1, or READY-tagged; 0 = not yet published)
   uint64_t *ywd;    // Y_t: <= 3 distinct exits landing in tile t+1 (16-bit rel + 1) | READY
   uint64_t *aggv;   // agg_t: f_t on the slots of Y_{t-1} (16-bit codes) | READY
+  uint64_t *aggn;   // frames delivered by tile t on each of those paths (16-bit) | READY
   uint64_t *inclx;  // exact exit of tile t + 1
   uint64_t *aggc;   // delivered frames of tile t + 1
   uint64_t *inclc;  // frames of tiles <= t + 1
   uint64_t *tile_exit, *tile_base, *tile_count;  // per-tile records for finalize
   // per super-group (64 tiles): completion counters, composed map, count sum (value + 1)
   uint32_t *sgc_agg, *sgc_cnt;
-  uint64_t *sagg, *scnt;
+  uint64_t *sagg, *saggn, *scnt;  // saggn: 20-bit frame counts per key
   // per-stream scratch
   uint64_t *payload_err;  // min absolute index of a malformed Change
   uint64_t *scount;       // [2*s] changes, [2*s+1] blobs

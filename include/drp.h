@@ -151,7 +151,7 @@ void drp_close(drp_ctx *ctx);
 void *drp_stream(drp_ctx *ctx);
 int drp_synchronize(drp_ctx *ctx);
 int drp_last_timing(drp_ctx *ctx, drp_timing *out);
-/* Tunables (0 = default 4096). tile_bytes is 4096 or 8192 (64 lanes x 64 or 128 bytes). */
+/* Tunables (0 = default 8192). tile_bytes is 4096 or 8192 (64 lanes x 64 or 128 bytes). */
 int drp_set_tile(drp_ctx *ctx, uint32_t tile_bytes);
 /* Look-back composes exact inclusive exits only, never the per-tile maps agg_t. Test hook. */
 int drp_set_strict(drp_ctx *ctx, int strict);
