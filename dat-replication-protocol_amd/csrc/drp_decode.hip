@@ -48,7 +48,7 @@ enum : uint32_t {
   ST_LB_ITERS = 0, ST_LB_NOINCL, ST_LB_NOAGG, ST_LB_KEYMISS, ST_LB_VUNK, ST_LB_OK0, ST_LB_OKN,
   ST_Y_SPINS, ST_SERIAL, ST_CNT_SPINS, ST_Y_COUNT, ST_AGG_UNK, ST_TILES, ST_PASS, ST_OVF_LANES,
   ST_T_GRAB, ST_T_STAGE, ST_T_DP, ST_T_Y, ST_T_LB, ST_T_PATH, ST_T_CNT, ST_T_EMIT,
-  ST_EV_TILES, ST_EV_SG, ST_SKIPS, ST_PHASEA, ST_NSTATS
+  ST_EV_TILES, ST_EV_SG, ST_SKIPS, ST_PHASEA, ST_RT_CYC, ST_DRAIN_CYC, ST_NSTATS
 };
 #define STAT(k, v)                         \
   do {                                     \
@@ -132,7 +132,10 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-constexpr int WPG = 4;  // waves (= consecutive tiles) per workgroup: one grab per group
+#ifndef DRP_WPG
+#define DRP_WPG 4
+#endif
+constexpr int WPG = DRP_WPG;  // waves (= consecutive tiles) per workgroup: one grab per group
 constexpr int64_t SG = 64;  // tiles per super-group (second look-back level)
 #ifndef DRP_MIN_WAVES
 #define DRP_MIN_WAVES 3  // waves per SIMD the register allocation must allow
@@ -602,8 +605,19 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           const int64_t lo0 = (int64_t)umax64(tf, (uint64_t)sg0);
           const int64_t j = (int64_t)t - 1 - (int64_t)lane;
           const int64_t b = SG * (sg - (int64_t)lane) - 1;  // last tiles of the 64 previous groups
+          uint64_t rt0 = 0;
+          if (PROF) {  // drain this wave's outstanding stores first, then time the loads alone
+            const uint64_t d0 = clock64();
+            __builtin_amdgcn_s_waitcnt(0);
+            rt0 = clock64();
+            acc[ST_DRAIN_CYC] += rt0 - d0;
+          }
           const uint64_t vj = j >= lo0 ? ld_agent(&P.inclx[j]) : 0ull;
           const uint64_t vb = b >= (int64_t)tf ? ld_agent(&P.inclx[b]) : 0ull;
+          if (PROF) {
+            __builtin_amdgcn_s_waitcnt(0);
+            acc[ST_RT_CYC] += clock64() - rt0 + (uint64_t)(__ballot(vj == 12345) & 0);
+          }
           {
             const uint64_t im = __ballot(vj != 0);
             if (im) {
