@@ -28,6 +28,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "dat-replication-protocol_amd", "python"))
 import drp_amd  # noqa: E402
+import drp_dist  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FRAME = 86
@@ -126,14 +127,51 @@ def h2d_rate(dev, nbytes=1 << 30):
     return {"GBps": nbytes / dt / 1e9, "bytes": nbytes, "note": "pinned host -> HBM, 1 GiB batch"}
 
 
+def c4_on_device(nstreams_total, rank, world, dev, seed=4):
+    """C4: 8192 independent streams, stream s has U[8192,16384] C2-shaped frames
+    (seeded, identical on every rank); this rank decodes the contiguous block drp_dist gives it."""
+    rng = np.random.default_rng(seed)
+    counts = rng.integers(8192, 16385, size=nstreams_total, dtype=np.int64)
+    lo, hi = drp_dist.shard_range(nstreams_total, world, rank)
+    mine = counts[lo:hi]
+    nframes = int(mine.sum())
+    wire = c2_on_device(nframes, seed=seed * 1000 + rank, dev=dev)
+    stream_off = torch.from_numpy(np.concatenate([[0], np.cumsum(mine)]) * FRAME).to(dev)
+    return wire, stream_off, mine, (lo, hi)
+
+
+def verify_c4(o, res, counts, base, lo, dev):
+    """Size-independent properties: per-stream frame counts, clean ends, dense in-order
+    frame table and the all-gathered global index."""
+    rs = C.sizeof(drp_amd.StreamResult)
+    raw = res.cpu().numpy().tobytes()
+    begin = 0
+    for s, n in enumerate(counts):
+        r = drp_amd.StreamResult.from_buffer_copy(raw[s * rs:(s + 1) * rs])
+        assert (r.frame_begin, r.frames, r.changes, r.err_code, r.tail_kind, r.consumed) == \
+            (begin, n, n, 0, 0, n * FRAME), (s, r.frame_begin, r.frames, r.err_code)
+        begin += int(n)
+    nf = int(counts.sum())
+    i = torch.arange(nf, device=dev, dtype=torch.int64)
+    assert torch.equal(o["payload_off"][:nf], i * FRAME + 2), "payload offsets"
+    assert bool((o["value_len"][:nf] == 64).all()) and bool((o["flags"][:nf] == 2).all())
+    if base is not None:
+        exp = torch.cumsum(torch.as_tensor(counts, device=dev), 0) - torch.as_tensor(counts, device=dev)
+        assert torch.equal(base[lo:lo + len(counts)] - base[lo], exp), "global index"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--frames", type=int, default=100_000_000)
+    ap.add_argument("--frames", type=int, default=100_000_000, help="C2 frames per GPU")
+    ap.add_argument("--workload", choices=["c2", "c4"], default="c2")
+    ap.add_argument("--streams", type=int, default=8192, help="C4 streams across all GPUs")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse "
+                    "several ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -142,37 +180,45 @@ def main():
     dist = world > 1
     if dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        if args.backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(args.backend)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
 
-    nframes = args.frames
-    wire = c2_on_device(nframes, seed=1234 + rank, dev=dev)
-    stream_off = torch.tensor([0, wire.numel()], dtype=torch.int64, device=dev)
-    outs = alloc_outputs(nframes + 64, dev)
-    res = torch.zeros(C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
-    stats = torch.zeros(4, dtype=torch.int64, device=dev)
-    gathered = torch.zeros(world * 4, dtype=torch.int64, device=dev)
-    gbase = torch.zeros(world, dtype=torch.int64, device=dev)
+    if args.workload == "c2":
+        nframes = args.frames
+        wire = c2_on_device(nframes, seed=1234 + rank, dev=dev)
+        stream_off = torch.tensor([0, wire.numel()], dtype=torch.int64, device=dev)
+        counts, (lo, _) = np.array([nframes]), (rank, rank + 1)
+        nstreams_total = world
+    else:
+        wire, stream_off, counts, (lo, _) = c4_on_device(args.streams, rank, world, dev)
+        nframes = int(counts.sum())
+        nstreams_total = args.streams
+    nlocal = stream_off.numel() - 1
+    cap = nframes + 64
+    outs = alloc_outputs(cap, dev)
+    res = torch.zeros(nlocal * C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize(dev)
 
-    ctx = drp_amd.Ctx(local, tile=args.tile)
-    L = ctx.L
-    sp = lambda t: C.c_void_p(t.data_ptr())
+    ctx = drp_amd.Ctx(dev.index, tile=args.tile)
+    state = {"base": None}
 
     def step():
-        ctx.decode_device(wire, stream_off, None, outs, nframes + 64, res)
-        if dist:
-            drp_amd._chk("stats", L.drp_stream_stats_from_results(ctx.h, sp(res), sp(stream_off), 1, sp(stats)))
-            drp_amd._chk("sync", L.drp_synchronize(ctx.h))
-            torch.distributed.all_gather_into_tensor(gathered, stats)  # RCCL over xGMI
-            torch.cuda.synchronize(dev)
-            drp_amd._chk("index", L.drp_index_scan(ctx.h, sp(gathered), world, sp(gbase)))
-            drp_amd._chk("sync", L.drp_synchronize(ctx.h))
+        ctx.decode_device(wire, stream_off, None, outs, cap, res)
+        if dist:  # the only collective: all-gather of 32-byte per-stream stats (RCCL over xGMI)
+            stats = drp_dist.local_stats_device(ctx, res, stream_off)
+            table = drp_dist.gather_stats(stats, nstreams_total)
+            state["base"] = drp_dist.global_index_device(ctx, table)
 
-    for _ in range(args.warmup):
+    for _ in range(max(1, args.warmup)):
         step()
-    verify_c2(outs, res, nframes, dev)
+    if args.workload == "c2":
+        verify_c2(outs, res, nframes, dev)
+    else:
+        verify_c4(outs, res, counts, state["base"], lo, dev)
 
     ext = torch.cuda.ExternalStream(ctx.stream, device=dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -192,17 +238,33 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
+    frames_all = torch.tensor([float(nframes)], dtype=torch.float64, device=dev)
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        cdev = dev if args.backend == "nccl" else torch.device("cpu")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(tt.item())
+        frames_all = frames_all.to(cdev)
+        torch.distributed.all_reduce(frames_all)
+    frames_node = int(frames_all.item())
 
-    frames_total = nframes * world * args.steps
-    wire_total = nframes * FRAME * world * args.steps
+    frames_total = frames_node * args.steps
+    wire_total = frames_node * FRAME * args.steps
     ms_per_step = elapsed / args.steps * 1e3
     dec_avg_s = float(np.mean(dec_ms)) / 1e3
-    b_dec = nframes * FRAME + 13 * nframes + 49 * nframes  # W + 13F + 49C
+    b_dec = nframes * FRAME + 13 * nframes + 49 * nframes  # W + 13F + 49C, this GPU
     achieved = b_dec / dec_avg_s / 1e9
+    tile = args.tile or 8192
+    if args.workload == "c2":
+        workload = {"workload": "C2: 100M Change frames x 86 B (64 B values), one 8.6 GB stream per GPU",
+                    "frames_per_gpu": nframes, "wire_bytes_per_gpu": nframes * FRAME,
+                    "parallelism": f"replicas: one stream per GPU, {world} GPU(s); RCCL all-gather of stream stats"}
+    else:
+        workload = {"workload": f"C4: {nstreams_total} independent streams of U[8192,16384] C2 frames, "
+                                f"contiguous shards over {world} GPU(s)",
+                    "frames_node": frames_node, "streams": nstreams_total,
+                    "parallelism": f"stream shards, {world} GPU(s); RCCL all-gather of 32 B stream stats + index scan"}
+    workload["tile_bytes"] = tile
 
     if rank == 0:
         out = {
@@ -217,15 +279,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: C2 generator on device (seeded), resident in HBM before timing",
-            "config": {"workload": "C2: 100M Change frames x 86 B (64 B values), one 8.6 GB stream per GPU",
-                       "frames_per_gpu": nframes, "wire_bytes_per_gpu": nframes * FRAME,
-                       "parallelism": f"independent streams, {world} GPU(s); RCCL all-gather of stream stats",
-                       "tile_bytes": args.tile or 8192},
+            "data": "synthetic: C2-shaped generator on device (seeded), resident in HBM before timing",
+            "config": workload,
             "wire_GBps": wire_total / elapsed / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                         "kernel": f"decode_tiles<{(args.tile or 8192) // 64}>", "kernel_ms": dec_avg_s * 1e3,
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profile(tile, nframes),
+                         "kernel": f"decode_tiles<{tile // 64}>", "kernel_ms": dec_avg_s * 1e3,
                          "bytes_per_launch": b_dec,
                          "bytes_model": "W + 13*frames + 49*changes (86+13+49 = 148 B/frame)"},
             "step_ms_hip_events": ev_ms / args.steps,
@@ -237,6 +296,21 @@ def main():
     ctx.close()
     if dist:
         torch.distributed.destroy_process_group()
+
+
+def traffic_from_profile(tile, nframes):
+    """HBM bytes per decode launch from the committed rocprofv3 PMC summary of this kernel
+    build (FETCH_SIZE x2 + WRITE_SIZE per frame, guide §HBM, measured on a C2 launch by
+    scripts/gpu_pmc.sh), times this launch's frames; None if absent or for another tile."""
+    p = os.path.join(ROOT, "profiles", "pmc_decode.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("tile_bytes") != tile:
+        return None
+    return d["hbm_bytes_per_frame"] * nframes if d.get("hbm_bytes_per_frame") else None
 
 
 if __name__ == "__main__":
