@@ -124,6 +124,25 @@ struct WaveLds {
   uint16_t nsum[2][256];      // doubling sums of delivered frames along the lane graph
 };
 
+__device__ __forceinline__ uint64_t lds_ld(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// spin until a sibling's LDS word is non-zero (bounded)
+__device__ __forceinline__ uint64_t lds_wait(const uint64_t *p, uint32_t *overflow, uint32_t lane) {
+  for (uint32_t spin = 0;; spin++) {
+    const uint64_t v = lds_ld(p);
+    if (v) return v;
+    if (spin > (1u << 24)) {
+      if (lane == 0) atomicOr(overflow, 2u);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // Orders this wave's LDS accesses (a wave's DS instructions execute in order; this keeps
 // the compiler from moving them and drains outstanding LDS traffic).
 __device__ __forceinline__ void wsync() {
@@ -149,6 +168,10 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
   constexpr int NM = NC + 2;           // per lane: class masks, dead mask, live mask
   __shared__ WaveLds<B> wl[WPG];
   __shared__ uint32_t grp_slot;
+  // sibling hand-off: the WPG tiles of a group are consecutive, so tile t gets Y_{t-1}, its
+  // entry and its output base from the wave before it through LDS (~100 cycles) instead of
+  // global round trips (~4 us under load); only the group's first wave looks back globally
+  __shared__ uint64_t gyl[WPG], gxl[WPG], gcl[WPG];
 
   const uint32_t lane = lane_id();
   const uint32_t wid = threadIdx.x >> 6;
@@ -178,6 +201,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       const uint32_t g = atomicAdd(P.counter, lane == 0 ? 1u : 0u);
       if (lane == 0) grp_slot = g;
     }
+    if (lane == 0) { gyl[wid] = 0; gxl[wid] = 0; gcl[wid] = 0; }
     __syncthreads();
     const uint64_t g0 = (uint64_t)grp_slot * WPG;
     if (g0 >= ntiles) break;
@@ -466,7 +490,12 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
         yw |= (y - (A + TILE) + 1) << (16 * k);
         STAT(ST_Y_COUNT, 1);
       }
-      if (lane == 0) st_agent(&P.ywd[t], yw);
+      if (lane == 0) {
+        st_agent(&P.ywd[t], yw);
+        lds_st(&gyl[wid], yw);
+      }
+    } else if (lane == 0) {
+      lds_st(&gyl[wid], READY);
     }
 
     // ---- 4b/4c. look-back for the entry x of this tile ---------------------------------
@@ -581,6 +610,10 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
 
     uint64_t x = e0;
     bool agg_done = first || P.strict;
+    if (!agg_done && wid > 0) {  // Y_{t-1} from the sibling wave
+      publish_agg(uniform64(lds_wait(&gyl[wid - 1], P.overflow, lane)) | READY);
+      agg_done = true;
+    }
     if (!agg_done) {
       // publish agg_t before looking back: Y_{t-1} comes from a tile processed concurrently,
       // and a map published late would stall every successor composing through this tile
@@ -593,7 +626,10 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     }
     bool sg_counted = false;
     if (agg_done) { sg_agg_done(); sg_counted = true; }
-    if (!first) {
+    if (!first && wid > 0) {  // entry = the sibling's exact exit
+      x = uniform64(lds_wait(&gxl[wid - 1], P.overflow, lane)) - 1;
+      STAT(ST_LB_OK0, 1);
+    } else if (!first) {
       uint32_t nap = 1;
       int64_t cur = -1;  // tile whose exact exit v is known (-1: none found yet)
       uint64_t v = 0;
@@ -765,14 +801,20 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       if (n0 != N_DEAD && n0 != N_UNK) {
         f = jmp[LEV - 1][n0];
         early = (f != N_DEAD && f != N_UNK);
-        if (early && lane == 0) st_agent(&P.inclx[t], exv[f] + 1);
+        if (early && lane == 0) {
+          st_agent(&P.inclx[t], exv[f] + 1);
+          lds_st(&gxl[wid], exv[f] + 1);
+        }
       }
       if (n0 != N_UNK && f != N_UNK) {  // frame count of the path from x, from the graph
         early_cnt = true;
         gcount = uniform32(path_count(x, n0));
       }
     }
-    if (x >= ve && lane == 0) st_agent(&P.inclx[t], x + 1);
+    if (x >= ve && lane == 0) {
+      st_agent(&P.inclx[t], x + 1);
+      lds_st(&gxl[wid], x + 1);
+    }
     auto count_published = [&]() {  // the last tile of the group to get here sums its counts
       uint32_t old = 0;
       if (lane == 0) old = __hip_atomic_fetch_add(&P.sgc_cnt[sg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -890,7 +932,10 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     }
     exit_t = uniform64(exit_t);
     count_t = uniform32(count_t);
-    if (lane == 0 && !early) st_agent(&P.inclx[t], exit_t + 1);
+    if (lane == 0 && !early) {
+      st_agent(&P.inclx[t], exit_t + 1);
+      lds_st(&gxl[wid], exit_t + 1);
+    }
     if (early_cnt) {
       if (count_t != gcount && lane == 0) atomicOr(P.overflow, 4u);
     } else {
@@ -904,7 +949,9 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     // or the last tiles of the 64 previous groups, then sums forward by whole groups (scnt)
     // and tiles (aggc), publishing the inclusive prefix of every boundary passed (helping).
     uint64_t base = 0;
-    if (t > 0) {
+    if (t > 0 && wid > 0) {  // the sibling's inclusive prefix
+      base = uniform64(lds_wait(&gcl[wid - 1], P.overflow, lane)) - 1;
+    } else if (t > 0) {
       uint32_t nap = 1;
       int64_t cur = -2;  // tile whose inclusive prefix v is known (-1: virtual tile before 0)
       uint64_t v = 0;
@@ -1001,7 +1048,10 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       }
     }
     base = uniform64(base);
-    if (lane == 0) st_agent(&P.inclc[t], base + count_t + 1);
+    if (lane == 0) {
+      st_agent(&P.inclc[t], base + count_t + 1);
+      lds_st(&gcl[wid], base + count_t + 1);
+    }
     if (base + count_t > P.cap && lane == 0) atomicOr(P.overflow, 1u);
 
     TMARK(ST_T_CNT);
