@@ -156,6 +156,12 @@ __device__ __forceinline__ void wsync() {
 #endif
 constexpr int WPG = DRP_WPG;  // waves (= consecutive tiles) per workgroup: one grab per group
 constexpr int64_t SG = 64;  // tiles per super-group (second look-back level)
+#ifndef DRP_NAP
+#define DRP_NAP 2  // s_sleep units (64 cycles) between polls of a global look-back word
+#endif
+#ifndef DRP_EAGER_Y
+#define DRP_EAGER_Y 1  // group-first waves wait for Y_{t-1} before looking back (else lazy)
+#endif
 #ifndef DRP_MIN_WAVES
 #define DRP_MIN_WAVES 3  // waves per SIMD the register allocation must allow
 #endif
@@ -583,7 +589,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           an = ld_agent(&P.aggn[j]);
           yk = ld_agent(&P.ywd[j - 1]);
           if (__ballot(!(av & READY) || !(yk & READY) || !(an & READY)) == 0) break;
-          __builtin_amdgcn_s_sleep(2);
+          __builtin_amdgcn_s_sleep(DRP_NAP);
         }
         const uint64_t keys = readlane64(yk, 0);
         const uint64_t Ag = A - (uint64_t)((int64_t)t - sg0) * TILE;
@@ -614,14 +620,14 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       publish_agg(uniform64(lds_wait(&gyl[wid - 1], P.overflow, lane)) | READY);
       agg_done = true;
     }
-    if (!agg_done) {
+    if (!agg_done && DRP_EAGER_Y) {
       // publish agg_t before looking back: Y_{t-1} comes from a tile processed concurrently,
       // and a map published late would stall every successor composing through this tile
       for (uint32_t spin = 0; spin <= 4096; spin++) {
         const uint64_t yk = uniform64(ld_agent(&P.ywd[t - 1]));
         if (yk & READY) { publish_agg(yk); agg_done = true; break; }
         STAT(ST_Y_SPINS, 1);
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(DRP_NAP);
       }
     }
     bool sg_counted = false;
@@ -779,7 +785,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           x = MARK_TERM | vs;
           break;
         }
-        for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(2);
+        for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(DRP_NAP);
         nap = nap < 8 ? nap * 2 : 8;
       }
     }
@@ -824,7 +830,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
         for (;;) {  // counts are value + 1: wait until all 64 are visible
           c = lane < sgsize ? ld_agent(&P.aggc[sg0 + lane]) : 1ull;
           if (__ballot(c == 0) == 0) break;
-          __builtin_amdgcn_s_sleep(2);
+          __builtin_amdgcn_s_sleep(DRP_NAP);
         }
         const uint64_t sum = wave_sum64(c - 1);
         if (lane == 0) st_agent(&P.scnt[sg], sum + 1);
@@ -1043,7 +1049,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           break;
         }
         STAT(ST_CNT_SPINS, 1);
-        for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(2);
+        for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(DRP_NAP);
         nap = nap < 8 ? nap * 2 : 8;
       }
     }
