@@ -269,6 +269,12 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
     CHK(hipMemsetAsync(dstats, 0, 64 * 8, st));
     P.stats = dstats;
   }
+  unsigned long long *dtrace = nullptr;
+  if (dstats && getenv("DRP_TRACE_FILE")) {
+    CHK(hipMalloc((void **)&dtrace, NT * 64));
+    CHK(hipMemsetAsync(dtrace, 0, NT * 64, st));
+    P.trace = dtrace;
+  }
 
   // persistent grid: single-wave blocks, several per CU; tiles are handed out in stream
   // order by an atomic counter, so a tile only ever waits on tiles already taken.
@@ -308,6 +314,15 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
     for (int i = 0; i < 29; i++) fprintf(stderr, " %s=%llu", nm[i], hs[i]);
     fprintf(stderr, " decode_ms=%.3f\n", c->timing.decode_ms);
     hipFree(dstats);
+  }
+  if (dtrace) {
+    std::vector<unsigned long long> ht(NT * 8);
+    CHK(hipMemcpy(ht.data(), dtrace, NT * 64, hipMemcpyDeviceToHost));
+    if (FILE *f = fopen(getenv("DRP_TRACE_FILE"), "wb")) {
+      fwrite(ht.data(), 8, ht.size(), f);
+      fclose(f);
+    }
+    hipFree(dtrace);
   }
   if (h[1] & 6u) return DRP_E_HIP;  // bounded wait expired / inconsistent walk inside the kernel
   if (h[1]) return DRP_E_CAPACITY;

@@ -54,6 +54,10 @@ enum : uint32_t {
   do {                                     \
     if (PROF) acc[k] += (uint64_t)(v);     \
   } while (0)
+#define TSTAMP(k)                                                               \
+  do {                                                                          \
+    if (PROF && P.trace && lane == 0) P.trace[t * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #define TMARK(k)                             \
   do {                                       \
     if (PROF) {                              \
@@ -65,6 +69,29 @@ enum : uint32_t {
 
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+// ---- tile maps in index form ----------------------------------------------------------
+// A tile's map sends the index (0..2) of its entry among the keys Y_{t-1} to the index of its
+// exit among Y_t, 2 bits per key; 3 = not expressible (dead path, exit outside Y_t). Maps
+// compose in O(1), so a wave scans 64 consecutive tiles' maps in 6 shuffle steps.
+constexpr uint32_t MAP_ID = 0x24u;   // identity: 0->0, 1->1, 2->2
+constexpr uint32_t MAP_NONE = 0x3Fu;
+__device__ __forceinline__ uint32_t map_apply(uint32_t m, uint32_t q) {
+  return q >= 3u ? 3u : (m >> (2u * q)) & 3u;
+}
+// f first, then g
+__device__ __forceinline__ uint32_t map_then(uint32_t f, uint32_t g) {
+  return map_apply(g, f & 3u) | (map_apply(g, (f >> 2) & 3u) << 2) | (map_apply(g, (f >> 4) & 3u) << 4);
+}
+// inclusive scan of maps over lanes (lane 0's map applied first)
+__device__ __forceinline__ uint32_t map_scan(uint32_t m, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < WAVE; d <<= 1) {
+    const uint32_t o = shfl_up32(m, d);
+    if (lane >= d) m = map_then(o, m);
+  }
+  return m;
+}
 
 // ---- bit arrays of NW 64-bit words (lane-private, fully unrolled) ---------------------
 template <int NW>
@@ -159,6 +186,9 @@ constexpr int64_t SG = 64;  // tiles per super-group (second look-back level)
 #ifndef DRP_NAP
 #define DRP_NAP 2  // s_sleep units (64 cycles) between polls of a global look-back word
 #endif
+#ifndef DRP_MEASURE_NO_EMIT
+#define DRP_MEASURE_NO_EMIT 0  // 1: skip the column writes (timing attribution only)
+#endif
 #ifndef DRP_EAGER_Y
 #define DRP_EAGER_Y 1  // group-first waves wait for Y_{t-1} before looking back (else lazy)
 #endif
@@ -230,6 +260,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     const uint64_t e0 = so + (P.entry ? P.entry[s] : 0ull);
 
     TMARK(ST_T_GRAB);
+    TSTAMP(0);
     // ---- stage: own B bytes (+ the halo) into LDS --------------------------------------
     const uint64_t lb = A + (uint64_t)lane * B;
     uint4 v[NV];
@@ -468,8 +499,10 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     // J[c] = final node of my class c
 
     TMARK(ST_T_DP);
+    TSTAMP(1);
     // ---- 4a. Y_t: distinct exits of my classes that land in the next tile ----------------
     const bool has_next = (t + 1 < tl);
+    uint64_t ywt = READY;  // Y_t (keys of tile t+1), for the index form of agg_t
     if (has_next) {
       uint64_t cand[NC];
 #pragma unroll
@@ -496,6 +529,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
         yw |= (y - (A + TILE) + 1) << (16 * k);
         STAT(ST_Y_COUNT, 1);
       }
+      ywt = yw;
       if (lane == 0) {
         st_agent(&P.ywd[t], yw);
         lds_st(&gyl[wid], yw);
@@ -532,6 +566,11 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           }
         }
         if (rel && code == V_UNK) STAT(ST_AGG_UNK, 1);
+        uint32_t ix = 3;
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+          if (code != V_UNK && ((ywt >> (16 * r)) & 0xFFFFu) == code + 1u) ix = (uint32_t)r;
+        aw |= (uint64_t)ix << (48 + 2 * k);
         aw |= (uint64_t)code << (16 * k);
         nw |= (uint64_t)cnt << (16 * k);
       }
@@ -539,6 +578,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
         st_agent(&P.aggn[t], nw);
         st_agent(&P.aggv[t], aw);
       }
+      TSTAMP(2);
     };
     TMARK(ST_T_Y);
     // Tile-level evaluation of the exact exit v through tiles j0 .. j0+n-1 of this stream
@@ -583,16 +623,24 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       uint64_t cw = READY | 0xFFFFFFFFFFFFull;  // all V_UNK
       if (sgsize == SG && sg0 > (int64_t)tf && sg0 + SG - 1 < (int64_t)tl && !P.strict) {
         const int64_t j = sg0 + lane;
-        uint64_t av = 0, an = 0, yk = 0;
+        uint64_t av = 0, an = 0, yk = 0, yo = 0;
         for (uint32_t w = 0; w < 1u << 16; w++) {  // a tile that never published its map
           av = ld_agent(&P.aggv[j]);                // (resolved early) leaves its codes V_UNK
           an = ld_agent(&P.aggn[j]);
           yk = ld_agent(&P.ywd[j - 1]);
-          if (__ballot(!(av & READY) || !(yk & READY) || !(an & READY)) == 0) break;
+          yo = (lane == SG - 1 && sg0 + SG < (int64_t)tl) ? ld_agent(&P.ywd[j]) : READY;
+          if (__ballot(!(av & READY) || !(yk & READY) || !(an & READY) || !(yo & READY)) == 0) break;
           __builtin_amdgcn_s_sleep(DRP_NAP);
         }
         const uint64_t keys = readlane64(yk, 0);
         const uint64_t Ag = A - (uint64_t)((int64_t)t - sg0) * TILE;
+        // the group's map in index form: one scan over the 64 tile maps
+        const bool rdy = (av & READY) && (an & READY) && (yk & READY) && (yo & READY);
+        const uint32_t I = map_scan(rdy ? (uint32_t)(av >> 48) & 63u : MAP_NONE, lane);
+        uint32_t E = shfl_up32(I, 1);
+        if (lane == 0) E = MAP_ID;
+        const uint32_t Ig = readlane32(I, SG - 1);
+        const uint64_t ylast = readlane64(yo, SG - 1);
         cw = READY;
         uint64_t nw = READY;
 #pragma unroll
@@ -600,7 +648,13 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           const uint32_t rel = (uint32_t)(keys >> (16 * q)) & 0xFFFFu;
           uint32_t code = V_UNK;
           uint64_t cq = 0;
-          if (rel && (keys & READY)) {
+          const uint32_t og = map_apply(Ig, (uint32_t)q);
+          if (rel && (keys & READY) && og != 3 && ((ylast >> (16 * og)) & 0xFFFFu)) {
+            code = (uint32_t)((ylast >> (16 * og)) & 0xFFFFu) - 1u;
+            const uint32_t ik = map_apply(E, (uint32_t)q);
+            cq = wave_sum32((uint32_t)(an >> (16 * ik)) & 0xFFFFu);
+            cw |= (uint64_t)og << (48 + 2 * q);
+          } else if (rel && (keys & READY)) {
             uint64_t vq = Ag + rel - 1, d0 = 0, d1 = 0;
             if (eval_tiles(vq, cq, sg0, SG, av, an, yk, d0, d1) == SG &&
                 vq - (Ag + (uint64_t)SG * TILE) < 0xFFF0ull)
@@ -744,13 +798,14 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           const uint32_t n = (uint32_t)min((int64_t)(SG - j0 % SG), (int64_t)t - 1 - cur);
           const int64_t j = j0 + lane;
           const bool inr = lane < n;
-          uint64_t vi = 0, av = 0, an = 0, yk = 0;
+          uint64_t vi = 0, av = 0, an = 0, yk = 0, yo = 0;
           if (inr) {  // one round trip for the whole chunk
             vi = ld_agent(&P.inclx[j]);
             if (!P.strict) {
               av = ld_agent(&P.aggv[j]);
               an = ld_agent(&P.aggn[j]);
               yk = ld_agent(&P.ywd[j - 1]);
+              yo = ld_agent(&P.ywd[j]);
             }
           }
           const uint64_t im = __ballot(vi != 0);
@@ -761,6 +816,40 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
             if ((cur + 1) % SG == 0) force_tile = false;
             STAT(ST_SKIPS, 1);
             continue;
+          }
+          if (!P.strict) {
+            // all lanes at once: scan the chunk's maps in index form from v's key index;
+            // the exact evaluation below takes over where the index chain breaks
+            const uint64_t Aj0 = A - (uint64_t)((int64_t)t - j0) * TILE;
+            const uint64_t y0 = readlane64(yk, 0);
+            uint32_t i0 = 3;
+            if (v >= Aj0 && v < Aj0 + TILE && (y0 & READY)) {
+#pragma unroll
+              for (int r = 0; r < 3; r++)
+                if (((y0 >> (16 * r)) & 0xFFFFu) == v - Aj0 + 1) i0 = (uint32_t)r;
+            }
+            if (i0 != 3) {
+              const bool rdy = inr && (av & READY) && (an & READY) && (yk & READY) && (yo & READY);
+              const uint32_t m = rdy ? (uint32_t)(av >> 48) & 63u : MAP_NONE;
+              const uint32_t I = map_scan(m, lane);
+              uint32_t E = shfl_up32(I, 1);
+              if (lane == 0) E = MAP_ID;
+              const uint32_t ik = map_apply(E, i0), ok = map_apply(m, ik);
+              const uint64_t gm = __ballot(inr && ok != 3);
+              const uint32_t k = (~gm) ? (uint32_t)__builtin_ctzll(~gm) : 64u;
+              if (k > 0) {
+                const uint64_t ex = Aj0 + (uint64_t)(lane + 1) * TILE + ((yo >> (16 * ok)) & 0xFFFFu) - 1;
+                if (lane < k) {  // helping: exact exit and frame count of tiles j0 .. j0+k-1
+                  st_agent(&P.inclx[j], ex + 1);
+                  st_agent(&P.aggc[j], ((an >> (16 * ik)) & 0xFFFFu) + 1);
+                }
+                STAT(ST_EV_TILES, k);
+                v = readlane64(ex, k - 1);
+                cur = j0 + (int64_t)k - 1;
+                if ((cur + 1) % SG == 0) force_tile = false;
+                continue;
+              }
+            }
           }
           uint64_t mine = 0, minec = 0, cdummy = 0;
           const uint32_t k = eval_tiles(v, cdummy, j0, n, av, an, yk, mine, minec);
@@ -791,6 +880,8 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     }
     if (!sg_counted) sg_agg_done();
     x = uniform64(x);
+    TSTAMP(3);
+    if (PROF && P.trace && lane == 0) P.trace[t * 8 + 6] = (uint64_t)__builtin_amdgcn_s_getreg(4 << 0 | 0 << 6 | 31 << 11) | ((uint64_t)wid << 32);
     STAT(ST_TILES, 1);
     if (x >= ve) STAT(ST_PASS, 1);
 
@@ -1061,13 +1152,14 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     if (base + count_t > P.cap && lane == 0) atomicOr(P.overflow, 1u);
 
     TMARK(ST_T_CNT);
+    TSTAMP(4);
     // ---- 5d. emit ------------------------------------------------------------------------
     const uint32_t myoff = wave_incl_scan32(cnt) - cnt;
     uint32_t nch = 0, nbl = 0, k = 0;
     uint64_t badf = ~0ull;
 #pragma unroll
     for (int w = 0; w < NW; w++) {
-      uint64_t bits = dmask[w];
+      uint64_t bits = DRP_MEASURE_NO_EMIT ? 0ull : dmask[w];  // measurement builds only
       while (bits) {
         const uint32_t o = 64u * w + (uint32_t)__builtin_ctzll(bits);
         bits &= bits - 1;
@@ -1123,6 +1215,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       P.tile_count[t] = count_t;
     }
     TMARK(ST_T_EMIT);
+    TSTAMP(5);
   }
   if (PROF) {
     acc[ST_OVF_LANES] = wave_sum32(novf);

@@ -41,6 +41,7 @@ struct DecodeParams {
   uint32_t *overflow;  // bit 0 capacity, bit 1 bounded wait expired, bit 2 inconsistent walk
   uint32_t strict;     // look-back uses exact inclusive exits only (test hook)
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
+  unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
 };
 
 struct EncodeParams {
