@@ -136,6 +136,17 @@ __device__ __forceinline__ uint4 load16(const uint8_t *g, uint64_t p, uint64_t s
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// Per-key results of phase 1 that phase 2 needs once the entry is known (the key the entry
+// turns out to be selects one row).
+enum : uint32_t { KF_KEY = 1, KF_EXIT = 2, KF_COUNT = 4, KF_SERIAL = 8 };
+struct KeyRec {
+  uint64_t keys;        // Y_{t-1} word (16-bit fields: tile-relative position + 1)
+  uint64_t kexit[3];    // exact tile exit of the key's path (KF_EXIT)
+  uint32_t kcnt[3];     // frames it delivers in the tile (KF_COUNT)
+  uint32_t kfl[3];
+  uint8_t ent[3][64];   // per lane: lane-relative entry of the key's path, 0xFF none
+};
+
 // LDS of one wave (one tile).
 template <int B>
 struct WaveLds {
@@ -149,6 +160,7 @@ struct WaveLds {
   uint8_t mark[256];
   int32_t entry[64];          // per lane: entry of the tile's path (tile-relative), -1 none
   uint16_t nsum[2][256];      // doubling sums of delivered frames along the lane graph
+  KeyRec rec[2];              // phase 1 -> phase 2 (two tiles in flight per wave)
 };
 
 __device__ __forceinline__ uint64_t lds_ld(const uint64_t *p) {
@@ -223,13 +235,25 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
   // lm accessors: lane m, mask k (0..NC-1 class, NC dead, NC+1 live), word w
   auto LM = [&](uint32_t m, uint32_t k, uint32_t w) -> uint64_t & { return lm[(m * NM + k) * NW + w]; };
 
-  uint64_t acc[PROF ? ST_NSTATS : 1];
-#pragma unroll
-  for (int i = 0; i < (PROF ? (int)ST_NSTATS : 1); i++) acc[i] = 0;
+  // profiling counters live in LDS so the profiling build keeps the production occupancy
+  // (all updates are wave-uniform: every lane writes the same value)
+  __shared__ uint64_t sacc[PROF ? WPG : 1][PROF ? ST_NSTATS : 1];
+  uint64_t *const acc = sacc[PROF ? wid : 0];
+  if (PROF && lane < ST_NSTATS) acc[lane] = 0;
   uint64_t tclk = PROF ? clock64() : 0;
   uint32_t novf = 0;
 
+  // Software pipeline per wave: phase 1 of the tile just taken (everything that does not
+  // depend on its entry: staging, live mask, DP, lane graph, Y_t, agg_t and the lane entries
+  // of every key's path), then phase 2 of the tile taken one round earlier (look-back for
+  // its entry, lane walks, output slot, emission). By the time a tile reaches phase 2 its
+  // predecessors have had a whole phase 1 to publish their maps, so the look-back rarely
+  // waits. Phase 1 only ever waits on Y_{t-1} of a tile taken earlier, whose phase 1 starts
+  // right after its grab, so the pipeline cannot deadlock.
+  uint64_t tp = ~0ull;  // tile whose phase 2 is pending
+  uint32_t slot = 0;    // key record of the tile in phase 1 (phase 2 uses slot ^ 1)
   for (;;) {
+    const uint64_t tgrab = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
     // one atomic grab per group of WPG consecutive tiles; every lane of wave 0 executes
     // the atomic (addend 1 on lane 0) so the grab is never split off the loop
     __syncthreads();
@@ -240,10 +264,13 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     if (lane == 0) { gyl[wid] = 0; gxl[wid] = 0; gcl[wid] = 0; }
     __syncthreads();
     const uint64_t g0 = (uint64_t)grp_slot * WPG;
-    if (g0 >= ntiles) break;
-    const uint64_t t = g0 + wid;
-    if (t >= ntiles) continue;
+    const uint64_t tn = g0 + wid;
+    const bool have = g0 < ntiles && tn < ntiles;
 
+    // ======== phase 1 of tile tn ===========================================================
+    if (have) {
+    const uint64_t t = tn;
+    KeyRec &R = wl[wid].rec[slot];
     // ---- which stream / tile ---------------------------------------------------------
     uint64_t lo = 0, hi = P.nstreams;
     while (hi - lo > 1) {
@@ -258,9 +285,11 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     const uint64_t vs = umax64(so, A), ve = umin64(se, A + TILE);
     const bool first = (t == tf);
     const uint64_t e0 = so + (P.entry ? P.entry[s] : 0ull);
-
+    (void)tl;
+    (void)vs;
     TMARK(ST_T_GRAB);
     TSTAMP(0);
+    if (PROF && P.trace && lane == 0) P.trace[t * 8 + 7] = tgrab;
     // ---- stage: own B bytes (+ the halo) into LDS --------------------------------------
     const uint64_t lb = A + (uint64_t)lane * B;
     uint4 v[NV];
@@ -538,49 +567,71 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       lds_st(&gyl[wid], READY);
     }
 
-    // ---- 4b/4c. look-back for the entry x of this tile ---------------------------------
-    // agg_t = f_t on Y_{t-1} is only needed by successors while this tile has no inclusive
-    // exit, so it is published lazily: after a first failed attempt and once Y_{t-1} exists.
-    // A tile that composes forward from a predecessor's inclusive exit also publishes the
-    // exits it derives for the tiles in between ("helping"), so the frontier jumps ahead.
-    auto publish_agg = [&](uint64_t yk) {
-      uint64_t aw = READY, nw = READY;
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const uint32_t rel = (uint32_t)(yk >> (16 * k)) & 0xFFFFu;
-        uint32_t code = V_UNK, cnt = 0;
-        if (rel) {
-          const uint64_t q = A + rel - 1;
-          if (q >= vs && q < ve) {
-            const uint32_t n = resolve(q);
-            if (n != N_DEAD && n != N_UNK) {
-              const uint32_t f = jmp[LEV - 1][n];
-              if (f != N_DEAD && f != N_UNK) {
-                const uint64_t e = exv[f];
-                if (e - (A + TILE) < 0xFFF0ull) {
-                  code = (uint32_t)(e - (A + TILE));
-                  cnt = path_count(q, n);
-                }
-              }
-            }
-          }
+
+    // ---- 4b. keys of this tile: Y_{t-1}, or the stream entry for a stream's first tile ----
+    uint64_t keys = READY;
+    if (first) {
+      if (e0 < ve) keys = READY | (e0 - A + 1);
+    } else if (wid > 0) {  // Y_{t-1} from the sibling wave
+      keys = uniform64(lds_wait(&gyl[wid - 1], P.overflow, lane)) | READY;
+    } else {
+      for (uint32_t spin = 0;; spin++) {
+        const uint64_t yk = uniform64(ld_agent(&P.ywd[t - 1]));
+        if (yk & READY) { keys = yk; break; }
+        STAT(ST_Y_SPINS, 1);
+        if (spin > SPIN_MAX) {
+          if (lane == 0) atomicOr(P.overflow, 2u);
+          break;
         }
-        if (rel && code == V_UNK) STAT(ST_AGG_UNK, 1);
-        uint32_t ix = 3;
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-          if (code != V_UNK && ((ywt >> (16 * r)) & 0xFFFFu) == code + 1u) ix = (uint32_t)r;
-        aw |= (uint64_t)ix << (48 + 2 * k);
-        aw |= (uint64_t)code << (16 * k);
-        nw |= (uint64_t)cnt << (16 * k);
+        __builtin_amdgcn_s_sleep(DRP_NAP);
       }
-      if (lane == 0) {
+    }
+
+    // ---- 4c. per key (lane k < 3): final exit, frames delivered, agg_t = f_t on Y_{t-1} ----
+    uint32_t kn = N_DEAD, kf = N_DEAD, kc = 0, kfl = 0, code = V_UNK;
+    uint64_t kq = 0, kex = 0;
+    {
+      const uint32_t rel = lane < 3 ? (uint32_t)(keys >> (16 * lane)) & 0xFFFFu : 0u;
+      if (rel) {
+        kq = A + rel - 1;
+        if (kq >= vs && kq < ve) {
+          kfl = KF_KEY;
+          kn = resolve(kq);
+          kf = (kn != N_DEAD && kn != N_UNK) ? (uint32_t)jmp[LEV - 1][kn] : kn;
+          if (kf != N_DEAD && kf != N_UNK) {
+            kex = exv[kf];
+            kfl |= KF_EXIT;
+          }
+          if (kn == N_UNK || kf == N_UNK) {
+            kfl |= KF_SERIAL;
+          } else {
+            kc = path_count(kq, kn);
+            kfl |= KF_COUNT;
+          }
+          if ((kfl & KF_EXIT) && kex - (A + TILE) < 0xFFF0ull) code = (uint32_t)(kex - (A + TILE));
+        }
+      }
+      if (PROF) STAT(ST_AGG_UNK, __builtin_popcountll(__ballot(rel != 0 && code == V_UNK)));
+      uint32_t ix = 3;
+#pragma unroll
+      for (int r = 0; r < 3; r++)
+        if (code != V_UNK && ((ywt >> (16 * r)) & 0xFFFFu) == code + 1u) ix = (uint32_t)r;
+      const uint64_t aw_l = lane < 3 ? ((uint64_t)code << (16 * lane)) | ((uint64_t)ix << (48 + 2 * lane)) : 0ull;
+      const uint64_t nw_l = lane < 3 && code != V_UNK ? (uint64_t)kc << (16 * lane) : 0ull;
+      const uint64_t aw = READY | readlane64(aw_l, 0) | readlane64(aw_l, 1) | readlane64(aw_l, 2);
+      const uint64_t nw = READY | readlane64(nw_l, 0) | readlane64(nw_l, 1) | readlane64(nw_l, 2);
+      if (!first && !P.strict && lane == 0) {
         st_agent(&P.aggn[t], nw);
         st_agent(&P.aggv[t], aw);
       }
-      TSTAMP(2);
-    };
-    TMARK(ST_T_Y);
+      if (lane < 3) {
+        R.kexit[lane] = kex;
+        R.kcnt[lane] = kc;
+        R.kfl[lane] = kfl;
+      }
+      if (lane == 0) R.keys = keys;
+    }
+    TSTAMP(2);
     // Tile-level evaluation of the exact exit v through tiles j0 .. j0+n-1 of this stream
     // (lanes hold aggv / ywd of tile j0+lane). Returns how many tiles were passed; the exit
     // after tile j0+k is left in lane k's `mine` (value + 1).
@@ -668,24 +719,132 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       if (lane == 0) st_agent(&P.sagg[sg], cw);
     };
 
-    uint64_t x = e0;
-    bool agg_done = first || P.strict;
-    if (!agg_done && wid > 0) {  // Y_{t-1} from the sibling wave
-      publish_agg(uniform64(lds_wait(&gyl[wid - 1], P.overflow, lane)) | READY);
-      agg_done = true;
-    }
-    if (!agg_done && DRP_EAGER_Y) {
-      // publish agg_t before looking back: Y_{t-1} comes from a tile processed concurrently,
-      // and a map published late would stall every successor composing through this tile
-      for (uint32_t spin = 0; spin <= 4096; spin++) {
-        const uint64_t yk = uniform64(ld_agent(&P.ywd[t - 1]));
-        if (yk & READY) { publish_agg(yk); agg_done = true; break; }
-        STAT(ST_Y_SPINS, 1);
-        __builtin_amdgcn_s_sleep(DRP_NAP);
+    sg_agg_done();
+    TMARK(ST_T_Y);
+
+    // ---- 4d. lane entries of every key's path: marking over the doubling levels ----------
+    // mark byte of node n = set of keys whose path passes n; after level r it holds the
+    // first 2^(r+1) nodes of each path
+    {
+      uint32_t *const mark32 = reinterpret_cast<uint32_t *>(mark);
+      mark32[lane] = 0;
+#pragma unroll
+      for (int q = 0; q < 3; q++) R.ent[q][lane] = 0xFF;
+      wsync();
+      if (lane < 3 && (kfl & KF_KEY)) {
+        const uint32_t r = (uint32_t)(kq - A);
+        R.ent[lane][r / B] = (uint8_t)(r % B);
+        if (kn != N_DEAD && kn != N_UNK && !(kfl & KF_SERIAL))
+          __hip_atomic_fetch_or(&mark32[kn >> 2], (1u << lane) << (8 * (kn & 3)), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      if (__ballot(lane < 3 && kn != N_DEAD && kn != N_UNK && !(kfl & KF_SERIAL) && (kfl & KF_KEY))) {
+        for (int r = 0; r < LEV - 1; r++) {
+          wsync();
+          const uint32_t mw = mark32[lane];
+          uint32_t tg[4];
+#pragma unroll
+          for (int c = 0; c < 4; c++) tg[c] = jmp[r][lane * 4 + c];
+          wsync();
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            const uint32_t bb = (mw >> (8 * c)) & 0xFFu;
+            if (bb)
+              __hip_atomic_fetch_or(&mark32[tg[c] >> 2], bb << (8 * (tg[c] & 3)), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+        wsync();
+        const uint32_t mw = mark32[lane];
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+          const uint32_t n = lane * 4 + c;
+          const uint32_t bb = (mw >> (8 * c)) & 7u;
+          if ((uint32_t)c < ncls && bb) {
+            const uint32_t nx = jmp[0][n];
+            const uint64_t e = cex[c];
+            if (e < ve && nx != n) {  // the path continues in a later lane (class or death)
+              const uint32_t r = (uint32_t)(e - A);
+#pragma unroll
+              for (int q = 0; q < 3; q++)
+                if ((bb >> q) & 1u) R.ent[q][r / B] = (uint8_t)(r % B);
+            }
+          }
+        }
+      }
+      wsync();
     }
-    bool sg_counted = false;
-    if (agg_done) { sg_agg_done(); sg_counted = true; }
+    }  // phase 1
+
+    // ======== phase 2 of tile tp ===========================================================
+    if (tp != ~0ull) {
+    const uint64_t t = tp;
+    const KeyRec &R = wl[wid].rec[slot ^ 1];
+    // ---- which stream / tile ---------------------------------------------------------
+    uint64_t lo = 0, hi = P.nstreams;
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (P.tile_prefix[mid] <= t) lo = mid; else hi = mid;
+    }
+    const uint64_t s = uniform64(lo);
+    const uint64_t tf = P.tile_prefix[s], tl = P.tile_prefix[s + 1];
+    const uint64_t so = P.stream_off[s], se = P.stream_off[s + 1];
+    const uint64_t A0 = so & ~(uint64_t)(TILE - 1);
+    const uint64_t A = A0 + (t - tf) * TILE;
+    const uint64_t vs = umax64(so, A), ve = umin64(se, A + TILE);
+    const bool first = (t == tf);
+    const uint64_t e0 = so + (P.entry ? P.entry[s] : 0ull);
+    (void)tl;
+    (void)vs;
+
+    TMARK(ST_T_GRAB);
+    // ---- restage: own B bytes (+ the halo) into LDS ---------------------------------------
+    const uint64_t lb = A + (uint64_t)lane * B;
+    uint4 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) v[k] = load16(P.bytes, lb + 16 * k, se);
+#pragma unroll
+    for (int k = 0; k < NV; k++) *reinterpret_cast<uint4 *>(buf + lane * B + 16 * k) = v[k];
+    if (lane < HALO / 16)
+      *reinterpret_cast<uint4 *>(buf + TILE + lane * 16) = load16(P.bytes, A + TILE + lane * 16, se);
+    if (lane < 2) *reinterpret_cast<uint4 *>(buf + TILE + HALO + lane * 16) = make_uint4(0, 0, 0, 0);
+    entry[lane] = -1;
+    wsync();
+    const uint32_t phi = (uint32_t)(ve > lb ? umin64(ve - lb, B) : 0);
+    const uint64_t lhi = lb + phi;  // lane's valid end (absolute)
+
+    TMARK(ST_T_STAGE);
+    const int64_t sg = (int64_t)(t / SG), sg0 = sg * SG;
+    const uint64_t sgsize = umin64(SG, ntiles - (uint64_t)sg0);
+    // Tile-level evaluation of the exact exit v through tiles j0 .. j0+n-1 of this stream
+    // (lanes hold aggv / ywd of tile j0+lane). Returns how many tiles were passed; the exit
+    // after tile j0+k is left in lane k's `mine` (value + 1).
+    auto eval_tiles = [&](uint64_t &v, uint64_t &cn, int64_t j0, uint32_t n, uint64_t av, uint64_t an,
+                          uint64_t yk, uint64_t &mine, uint64_t &minec) -> uint32_t {
+      uint32_t k = 0;
+      for (; k < n; k++) {
+        const uint64_t Aj = A - (uint64_t)((int64_t)t - (j0 + (int64_t)k)) * TILE;
+        uint32_t add = 0;
+        if (v < Aj + TILE) {
+          const uint64_t ai = readlane64(av, k), yi = readlane64(yk, k), ni = readlane64(an, k);
+          if (!(ai & READY) || !(yi & READY) || !(ni & READY)) break;
+          const uint64_t rel = v - Aj + 1;
+          uint32_t code = V_UNK;
+#pragma unroll
+          for (int q = 0; q < 3; q++)
+            if (((yi >> (16 * q)) & 0xFFFFu) == rel) {
+              code = (uint32_t)(ai >> (16 * q)) & 0xFFFFu;
+              add = (uint32_t)(ni >> (16 * q)) & 0xFFFFu;
+            }
+          if (code == V_UNK) break;
+          v = uniform64(Aj + TILE + code);
+        }
+        cn += add;
+        if (lane == k) { mine = v + 1; minec = (uint64_t)add + 1; }
+      }
+      return k;
+    };
+    uint64_t x = e0;
     if (!first && wid > 0) {  // entry = the sibling's exact exit
       x = uniform64(lds_wait(&gxl[wid - 1], P.overflow, lane)) - 1;
       STAT(ST_LB_OK0, 1);
@@ -864,11 +1023,6 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           if (k < n) break;  // stuck on a missing map: retry after a nap
         }
         if (cur == (int64_t)t - 1) { x = v; STAT(ST_LB_OKN, 1); break; }
-        if (!agg_done) {
-          const uint64_t yk = uniform64(ld_agent(&P.ywd[t - 1]));
-          if (yk & READY) { publish_agg(yk); agg_done = true; }
-          if (agg_done && !sg_counted) { sg_agg_done(); sg_counted = true; }
-        }
         if (spin > SPIN_MAX) {
           if (lane == 0) atomicOr(P.overflow, 2u);
           x = MARK_TERM | vs;
@@ -878,39 +1032,47 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
         nap = nap < 8 ? nap * 2 : 8;
       }
     }
-    if (!sg_counted) sg_agg_done();
     x = uniform64(x);
     TSTAMP(3);
-    if (PROF && P.trace && lane == 0) P.trace[t * 8 + 6] = (uint64_t)__builtin_amdgcn_s_getreg(4 << 0 | 0 << 6 | 31 << 11) | ((uint64_t)wid << 32);
+    if (PROF && P.trace && lane == 0)
+      P.trace[t * 8 + 6] = (uint64_t)__builtin_amdgcn_s_getreg(4 << 0 | 0 << 6 | 31 << 11) | ((uint64_t)wid << 32) |
+                           ((uint64_t)(__builtin_amdgcn_s_getreg(20 << 0 | 0 << 6 | 15 << 11) & 15u) << 40);
     STAT(ST_TILES, 1);
     if (x >= ve) STAT(ST_PASS, 1);
 
     TMARK(ST_T_LB);
+    // ---- 5a. the key x is, and its path's lane entries from phase 1 -----------------------
+    int32_t kx = -1;
+    if (x < ve) {
+#pragma unroll
+      for (int q = 0; q < 3; q++)
+        if (((R.keys >> (16 * q)) & 0xFFFFu) == x - A + 1 && (R.kfl[q] & KF_KEY)) kx = q;
+    }
+    const uint32_t xfl = kx >= 0 ? R.kfl[kx] : 0u;
     // the exact exit is known right away unless the path ends inside the tile / is serial:
     // publish it before the lane walks so successors' look-backs advance sooner
-    bool early = false, early_cnt = false;
-    uint32_t n0 = N_DEAD, gcount = 0;
+    bool early = false, early_cnt = false, graph_exit = false;
+    uint32_t gcount = 0;
+    uint64_t gexit = 0;
     if (x >= ve) {
       early = early_cnt = true;
+      if (lane == 0) {
+        st_agent(&P.inclx[t], x + 1);
+        lds_st(&gxl[wid], x + 1);
+      }
     } else {
-      n0 = uniform32(resolve(x));
-      uint32_t f = n0;
-      if (n0 != N_DEAD && n0 != N_UNK) {
-        f = jmp[LEV - 1][n0];
-        early = (f != N_DEAD && f != N_UNK);
-        if (early && lane == 0) {
-          st_agent(&P.inclx[t], exv[f] + 1);
-          lds_st(&gxl[wid], exv[f] + 1);
+      if (xfl & KF_EXIT) {
+        early = graph_exit = true;
+        gexit = R.kexit[kx];
+        if (lane == 0) {
+          st_agent(&P.inclx[t], gexit + 1);
+          lds_st(&gxl[wid], gexit + 1);
         }
       }
-      if (n0 != N_UNK && f != N_UNK) {  // frame count of the path from x, from the graph
+      if (xfl & KF_COUNT) {  // frame count of the path from x, from the graph
         early_cnt = true;
-        gcount = uniform32(path_count(x, n0));
+        gcount = R.kcnt[kx];
       }
-    }
-    if (x >= ve && lane == 0) {
-      st_agent(&P.inclx[t], x + 1);
-      lds_st(&gxl[wid], x + 1);
     }
     auto count_published = [&]() {  // the last tile of the group to get here sums its counts
       uint32_t old = 0;
@@ -932,53 +1094,14 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       count_published();
     }
 
-    // ---- 5a. this tile's path: entries per lane -------------------------------------------
-    bool graph_exit = false;
-    uint64_t gexit = 0;
     if (x < ve) {
-      if (lane == 0) entry[(uint32_t)(x - A) / B] = (int32_t)(x - A);
-      bool serial = (n0 == N_UNK);
-      if (n0 != N_DEAD && n0 != N_UNK) {
-        const uint32_t f = jmp[LEV - 1][n0];
-        if (f == N_UNK) serial = true;
-        if (f != N_DEAD && f != N_UNK) { graph_exit = true; gexit = exv[f]; }
-        if (!serial) {
-          // mark the path: after level r the marked set is {J^k(n0) : k < 2^(r+1)}
-#pragma unroll
-          for (int c = 0; c < 4; c++) mark[lane * 4 + c] = 0;
-          wsync();
-          if (lane == 0) mark[n0] = 1;
-          for (int r = 0; r < LEV - 1; r++) {
-            wsync();
-            uint32_t tg[4];
-            bool mk[4];
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-              mk[c] = mark[lane * 4 + c] != 0;
-              tg[c] = jmp[r][lane * 4 + c];
-            }
-            wsync();
-#pragma unroll
-            for (int c = 0; c < 4; c++)
-              if (mk[c]) mark[tg[c]] = 1;
-          }
-          wsync();
-#pragma unroll
-          for (int c = 0; c < NC; c++) {
-            const uint32_t n = lane * 4 + c;
-            if ((uint32_t)c < ncls && mark[n]) {
-              const uint32_t nx = jmp[0][n];
-              const uint64_t e = cex[c];
-              if (e < ve && nx != n) {  // the path continues in a later lane (class or death)
-                const uint32_t r = (uint32_t)(e - A);
-                entry[r / B] = (int32_t)r;
-              }
-            }
-          }
-        }
-      }
-      if (serial) STAT(ST_SERIAL, 1);
-      if (serial) {  // class overflow on the path: walk it frame by frame (rare)
+      const bool serial = kx < 0 || (xfl & KF_SERIAL);
+      if (!serial) {
+        const uint32_t o = R.ent[kx][lane];
+        entry[lane] = o == 0xFFu ? -1 : (int32_t)(lane * B + o);
+      } else {  // class overflow on the path, or an entry that is no key: walk it (rare)
+        STAT(ST_SERIAL, 1);
+        if (lane == 0) entry[(uint32_t)(x - A) / B] = (int32_t)(x - A);
         uint64_t cur = x;
         for (;;) {
           if (cur >= ve) break;
@@ -991,7 +1114,6 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       }
       wsync();
     }
-
     // ---- 5b. lane walks: delivered frames of the path inside my bytes --------------------
     // The path leaves the last entered lane at wend; if that is still inside the tile (a
     // path that dies at a dead-end exit), the lane holding it walks next.
@@ -1216,9 +1338,16 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     }
     TMARK(ST_T_EMIT);
     TSTAMP(5);
+    }  // phase 2
+    if (g0 >= ntiles) break;
+    tp = have ? tn : ~0ull;
+    slot ^= 1;
   }
   if (PROF) {
-    acc[ST_OVF_LANES] = wave_sum32(novf);
+    const uint64_t ovl = wave_sum32(novf);
+    wsync();
+    acc[ST_OVF_LANES] = ovl;
+    wsync();
     if (lane == 0)
 #pragma unroll
       for (int i = 0; i < (int)ST_NSTATS; i++) atomicAdd(P.stats + i, (unsigned long long)acc[i]);
