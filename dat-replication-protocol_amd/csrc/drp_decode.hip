@@ -252,13 +252,15 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
   // right after its grab, so the pipeline cannot deadlock.
   uint64_t tp = ~0ull;  // tile whose phase 2 is pending
   uint32_t slot = 0;    // key record of the tile in phase 1 (phase 2 uses slot ^ 1)
+  uint64_t c_s = 0, c_tf = 1, c_tl = 0, c_so = 0, c_se = 0, c_e0 = 0;  // cached stream geometry
+  uint32_t gpre = ~0u;  // wave 0: next group, grabbed ahead (before the previous phase 2)
   for (;;) {
     const uint64_t tgrab = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
     // one atomic grab per group of WPG consecutive tiles; every lane of wave 0 executes
     // the atomic (addend 1 on lane 0) so the grab is never split off the loop
     __syncthreads();
     if (wid == 0) {
-      const uint32_t g = atomicAdd(P.counter, lane == 0 ? 1u : 0u);
+      const uint32_t g = gpre != ~0u ? gpre : atomicAdd(P.counter, lane == 0 ? 1u : 0u);
       if (lane == 0) grp_slot = g;
     }
     if (lane == 0) { gyl[wid] = 0; gxl[wid] = 0; gcl[wid] = 0; }
@@ -271,21 +273,28 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     if (have) {
     const uint64_t t = tn;
     KeyRec &R = wl[wid].rec[slot];
-    // ---- which stream / tile ---------------------------------------------------------
-    uint64_t lo = 0, hi = P.nstreams;
-    while (hi - lo > 1) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (P.tile_prefix[mid] <= t) lo = mid; else hi = mid;
+    // ---- which stream / tile (the last stream's geometry is cached) ------------------------
+    if (t < c_tf || t >= c_tl) {
+      uint64_t lo = 0, hi = P.nstreams;
+      while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (P.tile_prefix[mid] <= t) lo = mid; else hi = mid;
+      }
+      c_s = uniform64(lo);
+      c_tf = uniform64(P.tile_prefix[c_s]);
+      c_tl = uniform64(P.tile_prefix[c_s + 1]);
+      c_so = uniform64(P.stream_off[c_s]);
+      c_se = uniform64(P.stream_off[c_s + 1]);
+      c_e0 = uniform64(c_so + (P.entry ? P.entry[c_s] : 0ull));
     }
-    const uint64_t s = uniform64(lo);
-    const uint64_t tf = P.tile_prefix[s], tl = P.tile_prefix[s + 1];
-    const uint64_t so = P.stream_off[s], se = P.stream_off[s + 1];
+    const uint64_t s = c_s, tf = c_tf, tl = c_tl, so = c_so, se = c_se;
     const uint64_t A0 = so & ~(uint64_t)(TILE - 1);
     const uint64_t A = A0 + (t - tf) * TILE;
     const uint64_t vs = umax64(so, A), ve = umin64(se, A + TILE);
     const bool first = (t == tf);
-    const uint64_t e0 = so + (P.entry ? P.entry[s] : 0ull);
+    const uint64_t e0 = c_e0;
     (void)tl;
+    (void)s;
     (void)vs;
     TMARK(ST_T_GRAB);
     TSTAMP(0);
@@ -776,25 +785,36 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     }
     }  // phase 1
 
+    // grab the next group now: the atomic's latency hides behind phase 2. Taking a group
+    // one phase early is safe: its phase 1 still only waits on groups taken before it.
+    if (wid == 0 && g0 < ntiles) gpre = atomicAdd(P.counter, lane == 0 ? 1u : 0u);
+
     // ======== phase 2 of tile tp ===========================================================
     if (tp != ~0ull) {
     const uint64_t t = tp;
     const KeyRec &R = wl[wid].rec[slot ^ 1];
-    // ---- which stream / tile ---------------------------------------------------------
-    uint64_t lo = 0, hi = P.nstreams;
-    while (hi - lo > 1) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (P.tile_prefix[mid] <= t) lo = mid; else hi = mid;
+    // ---- which stream / tile (the last stream's geometry is cached) ------------------------
+    if (t < c_tf || t >= c_tl) {
+      uint64_t lo = 0, hi = P.nstreams;
+      while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (P.tile_prefix[mid] <= t) lo = mid; else hi = mid;
+      }
+      c_s = uniform64(lo);
+      c_tf = uniform64(P.tile_prefix[c_s]);
+      c_tl = uniform64(P.tile_prefix[c_s + 1]);
+      c_so = uniform64(P.stream_off[c_s]);
+      c_se = uniform64(P.stream_off[c_s + 1]);
+      c_e0 = uniform64(c_so + (P.entry ? P.entry[c_s] : 0ull));
     }
-    const uint64_t s = uniform64(lo);
-    const uint64_t tf = P.tile_prefix[s], tl = P.tile_prefix[s + 1];
-    const uint64_t so = P.stream_off[s], se = P.stream_off[s + 1];
+    const uint64_t s = c_s, tf = c_tf, tl = c_tl, so = c_so, se = c_se;
     const uint64_t A0 = so & ~(uint64_t)(TILE - 1);
     const uint64_t A = A0 + (t - tf) * TILE;
     const uint64_t vs = umax64(so, A), ve = umin64(se, A + TILE);
     const bool first = (t == tf);
-    const uint64_t e0 = so + (P.entry ? P.entry[s] : 0ull);
+    const uint64_t e0 = c_e0;
     (void)tl;
+    (void)s;
     (void)vs;
 
     TMARK(ST_T_GRAB);
