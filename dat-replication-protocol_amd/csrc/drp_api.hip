@@ -304,14 +304,15 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
   c->timing.strict_reruns = 0;
   TRACE("decode done: tiles=%u flags=%u", h[0], h[1]);
   if (dstats) {
-    unsigned long long hs[32];
+    unsigned long long hs[40];
     CHK(hipMemcpy(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost));
     static const char *nm[] = {"lb_iters", "lb_noincl", "lb_noagg", "lb_keymiss", "lb_vunk", "lb_ok0", "lb_okn",
                                "y_spins", "serial", "cnt_spins", "y_count", "agg_unk", "tiles", "pass", "ovf_pos",
                                "t_grab", "t_stage", "t_dp", "t_y", "t_lb", "t_path", "t_cnt", "t_emit",
-                               "ev_tiles", "ev_sg", "skips", "phaseA", "rt_cyc", "drain_cyc"};
+                               "ev_tiles", "ev_sg", "skips", "phaseA", "rt_cyc", "drain_cyc", "dp_live", "dp_trips",
+                               "t_dploop", "emit_frames", "emit_trips", "t_dpparse"};
     fprintf(stderr, "[drp-stats]");
-    for (int i = 0; i < 29; i++) fprintf(stderr, " %s=%llu", nm[i], hs[i]);
+    for (int i = 0; i < 35; i++) fprintf(stderr, " %s=%llu", nm[i], hs[i]);
     fprintf(stderr, " decode_ms=%.3f\n", c->timing.decode_ms);
     hipFree(dstats);
   }

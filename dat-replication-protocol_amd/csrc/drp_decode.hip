@@ -48,7 +48,8 @@ enum : uint32_t {
   ST_LB_ITERS = 0, ST_LB_NOINCL, ST_LB_NOAGG, ST_LB_KEYMISS, ST_LB_VUNK, ST_LB_OK0, ST_LB_OKN,
   ST_Y_SPINS, ST_SERIAL, ST_CNT_SPINS, ST_Y_COUNT, ST_AGG_UNK, ST_TILES, ST_PASS, ST_OVF_LANES,
   ST_T_GRAB, ST_T_STAGE, ST_T_DP, ST_T_Y, ST_T_LB, ST_T_PATH, ST_T_CNT, ST_T_EMIT,
-  ST_EV_TILES, ST_EV_SG, ST_SKIPS, ST_PHASEA, ST_RT_CYC, ST_DRAIN_CYC, ST_NSTATS
+  ST_EV_TILES, ST_EV_SG, ST_SKIPS, ST_PHASEA, ST_RT_CYC, ST_DRAIN_CYC, ST_DP_LIVE, ST_DP_TRIPS,
+  ST_T_DPLOOP, ST_EMIT_FRAMES, ST_EMIT_TRIPS, ST_T_DPPARSE, ST_NSTATS
 };
 #define STAT(k, v)                         \
   do {                                     \
@@ -147,6 +148,10 @@ struct KeyRec {
   uint8_t ent[3][64];   // per lane: lane-relative entry of the key's path, 0xFF none
 };
 
+// Live positions per tile parsed load-balanced across the wave (more: per-lane parsing).
+constexpr uint32_t PCAP = 832;
+enum : uint32_t { PR_DEAD = 0, PR_IN = 1u << 30, PR_EXIT = 2u << 30, PR_FAR = 3u << 30, PR_OFF = (1u << 30) - 1 };
+
 // LDS of one wave (one tile).
 template <int B>
 struct WaveLds {
@@ -155,11 +160,19 @@ struct WaveLds {
   static constexpr int NM = NC + 2;
   uint8_t buf[TILE + HALO + 32] __attribute__((aligned(16)));
   uint64_t lm[64 * NM * NW];  // per lane: class masks, dead mask, live mask
-  uint64_t exv[256];          // node -> its class exit
-  uint8_t jmp[LEV][256];      // doubling levels of the lane graph
-  uint8_t mark[256];
+  union {
+    struct {                  // lane graph (built after the DP)
+      uint64_t exv[256];      // node -> its class exit
+      uint8_t jmp[LEV][256];  // doubling levels of the lane graph
+      uint8_t mark[256];
+      uint16_t nsum[2][256];  // doubling sums of delivered frames along the lane graph
+    };
+    struct {                  // during the DP: the tile's live positions, parsed load-balanced
+      uint16_t ppos[PCAP];    // tile-relative position, lanes in order, ascending in a lane
+      uint32_t prec[PCAP];    // its parse: PR_* tag | tile-relative successor / exit
+    };
+  };
   int32_t entry[64];          // per lane: entry of the tile's path (tile-relative), -1 none
-  uint16_t nsum[2][256];      // doubling sums of delivered frames along the lane graph
   KeyRec rec[2];              // phase 1 -> phase 2 (two tiles in flight per wave)
 };
 
@@ -374,6 +387,20 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     wsync();
 
     // ---- 2. lane DP: classify every live position, descending --------------------------
+    if (PROF) {
+      uint32_t nl = 0, trips = 0;
+#pragma unroll
+      for (int w = 0; w < NW; w++) {
+        const uint32_t c = (uint32_t)__builtin_popcountll(lvm[w]);
+        nl += c;
+        uint32_t mx = c;
+        for (uint32_t m = 1; m < WAVE; m <<= 1) mx = max(mx, shfl_xor32(mx, m));
+        trips += mx;
+      }
+      STAT(ST_DP_LIVE, wave_sum32(nl));
+      STAT(ST_DP_TRIPS, trips);
+      TMARK(ST_T_STAGE);
+    }
     uint64_t cm[NC][NW], dm[NW];
     uint64_t cex[NC];
     uint32_t ncls = 0;
@@ -385,27 +412,94 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     }
 #pragma unroll
     for (int w = 0; w < NW; w++) dm[w] = 0;
+    // 2a. Every live position of the tile is parsed once, spread evenly over the lanes
+    // (a lane owns 4 live positions on average but the busiest owns ~4x that): the lanes'
+    // positions go to a list, each lane parses list entries lane, lane+64, ..., and the
+    // classification below only reads the results back.
+    uint32_t nlive = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) nlive += (uint32_t)__builtin_popcountll(lvm[w]);
+    const uint32_t pend = wave_incl_scan32(nlive);
+    const uint32_t ptotal = readlane32(pend, WAVE - 1);
+    const bool balanced = ptotal <= PCAP;
+    uint16_t *const ppos = wl[wid].ppos;
+    uint32_t *const prec = wl[wid].prec;
+    if (balanced) {
+      uint32_t i = pend - nlive;
+#pragma unroll
+      for (int w = 0; w < NW; w++) {
+        uint64_t bits = lvm[w];
+        while (bits) {
+          ppos[i++] = (uint16_t)(lane * B + 64u * w + (uint32_t)__builtin_ctzll(bits));
+          bits &= bits - 1;
+        }
+      }
+      wsync();
+      for (uint32_t i2 = lane; i2 < ptotal; i2 += WAVE) {
+        const uint32_t r = ppos[i2];
+        const uint64_t p = A + r;
+        const uint64_t mhi = umin64(A + (uint64_t)(r / B + 1) * B, ve);
+        const Hdr h = parse_hdr_lds(buf, A, p, se);
+        uint32_t code = PR_DEAD;
+        if (h.kind == H_VALID) {
+          const uint64_t nx = h.succ;
+          if (nx < mhi) {
+            code = PR_IN | (uint32_t)(nx - A);
+          } else {
+            bool exit_dead = false;
+            if (nx < ve) {
+              const uint32_t r2 = (uint32_t)(nx - A);
+              exit_dead = !((LM(r2 / B, NC + 1, (r2 % B) >> 6) >> (r2 & 63)) & 1ull);
+            } else if (nx < se && nx + 16 <= A + TILE + HALO) {
+              const Hdr h2 = parse_hdr_lds(buf, A, nx, se);  // exit into the halo: error header there?
+              exit_dead = h2.kind >= H_ERR_VARINT;
+            }
+            if (!exit_dead) code = nx - A <= PR_OFF ? PR_EXIT | (uint32_t)(nx - A) : PR_FAR;
+          }
+        }
+        prec[i2] = code;
+      }
+      wsync();
+    }
+    TMARK(ST_T_DPPARSE);
+
+    // 2b. classification, descending over the lane's live positions
+    uint32_t pidx = pend;  // one past the list index of the current position
 #pragma unroll
     for (int w = NW - 1; w >= 0; w--) {
       uint64_t bits = lvm[w];
       while (bits) {
         const uint32_t o = 64u * w + (63u - (uint32_t)__builtin_clzll(bits));
         bits &= ~(1ull << (o & 63));
-        const Hdr h = parse_hdr_lds(buf, A, lb + o, se);
-        int cls = -1;  // -1 dead, -2 unresolved (class overflow)
-        if (h.kind == H_VALID) {
-          const uint64_t nx = h.succ;
-          bool exit_dead = false;
-          if (nx >= lhi && nx < ve) {
-            const uint32_t r2 = (uint32_t)(nx - A);
-            exit_dead = !((LM(r2 / B, NC + 1, (r2 % B) >> 6) >> (r2 & 63)) & 1ull);
-          } else if (nx >= ve && nx < se && nx + 16 <= A + TILE + HALO) {
-            const Hdr h2 = parse_hdr_lds(buf, A, nx, se);  // exit into the halo: error header there?
-            exit_dead = h2.kind >= H_ERR_VARINT;
+        // successor of position o: dead, inside the lane, or an exit nx >= lhi
+        bool dead = true, inl = false;
+        uint64_t nx = 0;
+        if (balanced) {
+          const uint32_t code = prec[--pidx];
+          const uint32_t tag = code & PR_FAR;
+          dead = tag == PR_DEAD;
+          inl = tag == PR_IN;
+          nx = A + (code & PR_OFF);
+          if (tag == PR_FAR) nx = parse_hdr_lds(buf, A, lb + o, se).succ;
+        } else {
+          const Hdr h = parse_hdr_lds(buf, A, lb + o, se);
+          if (h.kind == H_VALID) {
+            nx = h.succ;
+            inl = nx < lhi;
+            bool exit_dead = false;
+            if (nx >= lhi && nx < ve) {
+              const uint32_t r2 = (uint32_t)(nx - A);
+              exit_dead = !((LM(r2 / B, NC + 1, (r2 % B) >> 6) >> (r2 & 63)) & 1ull);
+            } else if (nx >= ve && nx < se && nx + 16 <= A + TILE + HALO) {
+              const Hdr h2 = parse_hdr_lds(buf, A, nx, se);  // exit into the halo: error header there?
+              exit_dead = h2.kind >= H_ERR_VARINT;
+            }
+            dead = exit_dead;
           }
-          if (exit_dead) {
-            cls = -1;
-          } else if (nx >= lhi) {
+        }
+        int cls = -1;  // -1 dead, -2 unresolved (class overflow)
+        if (!dead) {
+          if (!inl) {
             cls = -2;
 #pragma unroll
             for (int c = 0; c < NC; c++)
@@ -435,7 +529,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
                   if (c == far) {
                     cex[c] = nx;
 #pragma unroll
-                    for (int w = 0; w < NW; w++) cm[c][w] = 0;
+                    for (int w2 = 0; w2 < NW; w2++) cm[c][w2] = 0;
                   }
                 cls = far;
               }
@@ -459,6 +553,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           if (cls == c) sbit<NW>(cm[c], o);
       }
     }
+    TMARK(ST_T_DPLOOP);
 #pragma unroll
     for (int w = 0; w < NW; w++) {
 #pragma unroll
@@ -1297,6 +1392,12 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     TSTAMP(4);
     // ---- 5d. emit ------------------------------------------------------------------------
     const uint32_t myoff = wave_incl_scan32(cnt) - cnt;
+    if (PROF) {
+      uint32_t mx = cnt;
+      for (uint32_t m = 1; m < WAVE; m <<= 1) mx = max(mx, shfl_xor32(mx, m));
+      STAT(ST_EMIT_FRAMES, wave_sum32(cnt));
+      STAT(ST_EMIT_TRIPS, mx);
+    }
     uint32_t nch = 0, nbl = 0, k = 0;
     uint64_t badf = ~0ull;
 #pragma unroll
