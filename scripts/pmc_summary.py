@@ -1,0 +1,47 @@
+"""Summarises the rocprofv3 --pmc passes of scripts/gpu_pmc.sh (gpurun_out/pmc/<pass>/...csv)
+into profiles/pmc_decode.json: per-launch averages of the decode kernel's counters and the
+HBM bytes per frame that bench.py reports as roofline.traffic (FETCH_SIZE doubled on gfx950,
+MI355X_MICROARCH.md §HBM, plus WRITE_SIZE). Usage: python scripts/pmc_summary.py frames tile"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+frames, tile = int(sys.argv[1]), int(sys.argv[2])
+kern = f"decode_tiles<{tile // 64}"
+tot = collections.defaultdict(float)
+disp = collections.defaultdict(set)
+os.makedirs(os.path.join(ROOT, "profiles", "pmc_r1"), exist_ok=True)
+for name in ["sq1", "sq2", "fetch", "write"]:
+    fs = glob.glob(os.path.join(ROOT, "gpurun_out", "pmc", name, "**", "*counter_collection.csv"), recursive=True)
+    if not fs:
+        continue
+    shutil.copy(fs[0], os.path.join(ROOT, "profiles", "pmc_r1", name + ".csv"))
+    for r in csv.DictReader(open(fs[0])):
+        if kern in r["Kernel_Name"]:
+            tot[r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[r["Counter_Name"]].add(r["Dispatch_Id"])
+avg = {k: v / len(disp[k]) for k, v in tot.items()}
+fetch = avg.get("FETCH_SIZE", 0.0) * 1024 * 2
+write = avg.get("WRITE_SIZE", 0.0) * 1024
+out = {
+    "kernel": f"decode_tiles<{tile // 64}, false>",
+    "tile_bytes": tile,
+    "workload": f"C2, {frames:,} frames (bench.py --frames {frames}), per dispatch",
+    "frames": frames,
+    "wire_bytes": frames * 86,
+    "FETCH_SIZE_kB": avg.get("FETCH_SIZE"),
+    "WRITE_SIZE_kB": avg.get("WRITE_SIZE"),
+    "fetch_bytes_corrected": fetch,
+    "write_bytes": write,
+    "note": "rocprofv3 --pmc, one pass per counter group (scripts/gpu_pmc.sh); FETCH_SIZE doubled per "
+            "MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B); averages over the dispatches",
+    "SQ": {k[3:]: v for k, v in sorted(avg.items()) if k.startswith("SQ_")},
+    "hbm_bytes_per_frame": (fetch + write) / frames if fetch else None,
+}
+json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_decode.json"), "w"), indent=1)
+print(json.dumps({k: out[k] for k in ["fetch_bytes_corrected", "write_bytes", "hbm_bytes_per_frame"]}))
