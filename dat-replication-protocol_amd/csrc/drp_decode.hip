@@ -913,18 +913,13 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     (void)vs;
 
     TMARK(ST_T_GRAB);
-    // ---- restage: own B bytes (+ the halo) into LDS ---------------------------------------
+    // ---- restage: own B bytes (+ the halo); the loads are issued here and land in LDS after
+    // the look-back, so the two latencies overlap
     const uint64_t lb = A + (uint64_t)lane * B;
-    uint4 v[NV];
+    uint4 rv[NV], rh = make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int k = 0; k < NV; k++) v[k] = load16(P.bytes, lb + 16 * k, se);
-#pragma unroll
-    for (int k = 0; k < NV; k++) *reinterpret_cast<uint4 *>(buf + lane * B + 16 * k) = v[k];
-    if (lane < HALO / 16)
-      *reinterpret_cast<uint4 *>(buf + TILE + lane * 16) = load16(P.bytes, A + TILE + lane * 16, se);
-    if (lane < 2) *reinterpret_cast<uint4 *>(buf + TILE + HALO + lane * 16) = make_uint4(0, 0, 0, 0);
-    entry[lane] = -1;
-    wsync();
+    for (int k = 0; k < NV; k++) rv[k] = load16(P.bytes, lb + 16 * k, se);
+    if (lane < HALO / 16) rh = load16(P.bytes, A + TILE + lane * 16, se);
     const uint32_t phi = (uint32_t)(ve > lb ? umin64(ve - lb, B) : 0);
     const uint64_t lhi = lb + phi;  // lane's valid end (absolute)
 
@@ -1148,6 +1143,12 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       }
     }
     x = uniform64(x);
+#pragma unroll
+    for (int k = 0; k < NV; k++) *reinterpret_cast<uint4 *>(buf + lane * B + 16 * k) = rv[k];
+    if (lane < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + lane * 16) = rh;
+    if (lane < 2) *reinterpret_cast<uint4 *>(buf + TILE + HALO + lane * 16) = make_uint4(0, 0, 0, 0);
+    entry[lane] = -1;
+    wsync();
     TSTAMP(3);
     if (PROF && P.trace && lane == 0)
       P.trace[t * 8 + 6] = (uint64_t)__builtin_amdgcn_s_getreg(4 << 0 | 0 << 6 | 31 << 11) | ((uint64_t)wid << 32) |
