@@ -135,6 +135,7 @@ __device__ __forceinline__ Hdr parse_hdr_lds(const uint8_t *lds, uint64_t base, 
 
 // Byte readers for the Change decoder.
 struct LdsReader {
+  static constexpr bool kFast = true;  // two-byte peeks are cheap: decode_change fast path
   const uint8_t *lds;
   uint64_t base;  // absolute position of lds[0]
   uint64_t lim;   // absolute end of valid LDS bytes (exclusive)
@@ -142,9 +143,15 @@ struct LdsReader {
   __device__ __forceinline__ void win(uint64_t p, uint64_t &w0, uint64_t &w1) const {
     lds_win16(lds, (uint32_t)(p - base), w0, w1);
   }
+  __device__ __forceinline__ void peek2(uint64_t p, uint32_t &b0, uint32_t &b1) const {
+    const uint32_t o = (uint32_t)(p - base);
+    b0 = lds[o];
+    b1 = lds[o + 1];
+  }
 };
 
 struct GlobalReader {
+  static constexpr bool kFast = false;
   const uint8_t *g;
   uint64_t lim;  // absolute end of readable bytes
   __device__ __forceinline__ bool ok(uint64_t p, uint64_t n) const { return p + n <= lim; }
@@ -189,6 +196,46 @@ __device__ __forceinline__ ChangeCols decode_change(const R &rd, uint64_t pstart
   uint64_t off = 0;
   while (off < len) {
     uint64_t avail = len - off;
+    if constexpr (R::kFast) if (avail >= 2 && rd.ok(pstart + off, 2)) {
+      // fast path: one-byte field prefix of a known tag and a one-byte varint after it (the
+      // shape the reference's encoder writes for short fields); same results as below
+      uint32_t b0, b1;
+      rd.peek2(pstart + off, b0, b1);
+      const uint32_t tag = b0 >> 3;
+      if (b0 < 0x80u && b1 < 0x80u && tag >= 1u && tag <= 6u) {
+        if (tag == 3u || tag == 4u || tag == 5u) {
+          if (tag == 3u) {
+            c.change = b1;
+            found |= 2;
+          } else if (tag == 4u) {
+            c.from = b1;
+            found |= 4;
+          } else {
+            c.to = b1;
+            found |= 8;
+          }
+          off += 2;
+        } else {
+          const uint64_t o2 = off + 2;
+          if ((uint64_t)b1 > len - o2) goto bad;
+          if (tag == 1u) {
+            c.subset_off = (uint32_t)o2;
+            c.subset_len = b1;
+            c.flags |= DRP_F_SUBSET;
+          } else if (tag == 2u) {
+            c.key_off = (uint32_t)o2;
+            c.key_len = b1;
+            found |= 1;
+          } else {
+            c.value_off = (uint32_t)o2;
+            c.value_len = b1;
+            c.flags |= DRP_F_VALUE;
+          }
+          off = o2 + b1;
+        }
+        continue;
+      }
+    }
     uint64_t need = avail < 16 ? avail : 16;
     if (!rd.ok(pstart + off, need)) {
       c.err = ERR_UNREACHABLE;
