@@ -325,7 +325,7 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
     }
     hipFree(dtrace);
   }
-  if (h[1] & 6u) return DRP_E_HIP;  // bounded wait expired / inconsistent walk inside the kernel
+  if (h[1] & ~1u) return DRP_E_HIP;  // bounded wait expired / inconsistent walk inside the kernel
   if (h[1]) return DRP_E_CAPACITY;
   return DRP_OK;
 }

@@ -183,12 +183,12 @@ __device__ __forceinline__ void lds_st(uint64_t *p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // spin until a sibling's LDS word is non-zero (bounded)
-__device__ __forceinline__ uint64_t lds_wait(const uint64_t *p, uint32_t *overflow, uint32_t lane) {
+__device__ __forceinline__ uint64_t lds_wait(const uint64_t *p, uint32_t *overflow, uint32_t lane, uint32_t bit = 2u) {
   for (uint32_t spin = 0;; spin++) {
     const uint64_t v = lds_ld(p);
     if (v) return v;
     if (spin > (1u << 24)) {
-      if (lane == 0) atomicOr(overflow, 2u);
+      if (lane == 0) atomicOr(overflow, bit);
       return 0;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
   constexpr int NV = B / 16;           // 16-byte loads per lane
   constexpr int NM = NC + 2;           // per lane: class masks, dead mask, live mask
   __shared__ WaveLds<B> wl[WPG];
-  __shared__ uint32_t grp_slot, grp_next;
+  __shared__ uint32_t grp_slot;
   // sibling hand-off: the WPG tiles of a group are consecutive, so tile t gets Y_{t-1}, its
   // entry and its output base from the wave before it through LDS (~100 cycles) instead of
   // global round trips (~4 us under load); only the group's first wave looks back globally
@@ -237,10 +237,6 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
   const uint32_t lane = lane_id();
   const uint32_t wid = threadIdx.x >> 6;
   uint8_t *const buf = wl[wid].buf;
-  // phase 2's byte image lives over lm + the graph union, which phase 1 is done with; buf is
-  // then free for the LDS-DMA of the next round's tile
-  uint8_t *const buf2 = reinterpret_cast<uint8_t *>(wl[wid].lm);
-  static_assert(offsetof(WaveLds<B>, entry) - offsetof(WaveLds<B>, lm) >= TILE + HALO + 32, "buf2 fits");
   uint64_t *const lm = wl[wid].lm;
   uint64_t *const exv = wl[wid].exv;
   uint8_t(*const jmp)[256] = wl[wid].jmp;
@@ -270,27 +266,18 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
   uint64_t tp = ~0ull;  // tile whose phase 2 is pending
   uint32_t slot = 0;    // key record of the tile in phase 1 (phase 2 uses slot ^ 1)
   uint64_t c_s = 0, c_tf = 1, c_tl = 0, c_so = 0, c_se = 0, c_e0 = 0;  // cached stream geometry
-  // Groups are grabbed two rounds ahead (wave 0 keeps them): the next round's group must be
-  // known during this round's phase 2, whose time hides the LDS-DMA of its tiles' bytes.
-  uint32_t gA = ~0u, gB = ~0u;  // wave 0: this round's group, next round's group
-  uint64_t pf = ~0ull;          // tile whose bytes the DMA has put in buf (phase 1 skips staging)
   for (;;) {
     const uint64_t tgrab = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
     // one atomic grab per group of WPG consecutive tiles; every lane of wave 0 executes
-    // the atomic (addend 1 on lane 0) so the grab is never split off the loop. The barrier
-    // also retires this wave's LDS-DMA (the fence before it waits for vmcnt(0)).
+    // the atomic (addend 1 on lane 0) so the grab is never split off the loop
     __syncthreads();
     if (wid == 0) {
-      if (gA == ~0u) gA = atomicAdd(P.counter, lane == 0 ? 1u : 0u);
-      if (gB == ~0u) gB = atomicAdd(P.counter, lane == 0 ? 1u : 0u);
-      if (lane == 0) {
-        grp_slot = gA;
-        grp_next = gB;
-      }
+      const uint32_t g = atomicAdd(P.counter, lane == 0 ? 1u : 0u);
+      if (lane == 0) grp_slot = g;
     }
     if (lane == 0) { gyl[wid] = 0; gxl[wid] = 0; gcl[wid] = 0; }
     __syncthreads();
-    const uint64_t g0 = (uint64_t)grp_slot * WPG, gn0 = (uint64_t)grp_next * WPG;
+    const uint64_t g0 = (uint64_t)grp_slot * WPG;
     const uint64_t tn = g0 + wid;
     const bool have = g0 < ntiles && tn < ntiles;
 
@@ -327,28 +314,12 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     // ---- stage: own B bytes (+ the halo) into LDS --------------------------------------
     const uint64_t lb = A + (uint64_t)lane * B;
     uint4 v[NV];
-    if (pf == t) {
-      // bytes already landed by last round's LDS-DMA; bytes past the stream end (or chunks
-      // the DMA could not take) are redone here, zero-filled like load16
-      if (se < A + TILE + HALO + 16) {
 #pragma unroll
-        for (int k = 0; k <= NV; k++) {
-          const uint64_t p = A + 1024u * k + 16u * lane;
-          if ((k < NV || lane < HALO / 16) && p + 16 > se)
-            *reinterpret_cast<uint4 *>(buf + 1024u * k + 16u * lane) = load16(P.bytes, p, se);
-        }
-        wsync();
-      }
+    for (int k = 0; k < NV; k++) v[k] = load16(P.bytes, lb + 16 * k, se);
 #pragma unroll
-      for (int k = 0; k < NV; k++) v[k] = *reinterpret_cast<const uint4 *>(buf + lane * B + 16 * k);
-    } else {
-#pragma unroll
-      for (int k = 0; k < NV; k++) v[k] = load16(P.bytes, lb + 16 * k, se);
-#pragma unroll
-      for (int k = 0; k < NV; k++) *reinterpret_cast<uint4 *>(buf + lane * B + 16 * k) = v[k];
-      if (lane < HALO / 16)
-        *reinterpret_cast<uint4 *>(buf + TILE + lane * 16) = load16(P.bytes, A + TILE + lane * 16, se);
-    }
+    for (int k = 0; k < NV; k++) *reinterpret_cast<uint4 *>(buf + lane * B + 16 * k) = v[k];
+    if (lane < HALO / 16)
+      *reinterpret_cast<uint4 *>(buf + TILE + lane * 16) = load16(P.bytes, A + TILE + lane * 16, se);
     if (lane < 2) *reinterpret_cast<uint4 *>(buf + TILE + HALO + lane * 16) = make_uint4(0, 0, 0, 0);
     entry[lane] = -1;
     wsync();
@@ -705,14 +676,14 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     if (first) {
       if (e0 < ve) keys = READY | (e0 - A + 1);
     } else if (wid > 0) {  // Y_{t-1} from the sibling wave
-      keys = uniform64(lds_wait(&gyl[wid - 1], P.overflow, lane)) | READY;
+      keys = uniform64(lds_wait(&gyl[wid - 1], P.overflow, lane, 16u)) | READY;
     } else {
       for (uint32_t spin = 0;; spin++) {
         const uint64_t yk = uniform64(ld_agent(&P.ywd[t - 1]));
         if (yk & READY) { keys = yk; break; }
         STAT(ST_Y_SPINS, 1);
         if (spin > SPIN_MAX) {
-          if (lane == 0) atomicOr(P.overflow, 2u);
+          if (lane == 0) atomicOr(P.overflow, 8u);
           break;
         }
         __builtin_amdgcn_s_sleep(DRP_NAP);
@@ -908,48 +879,10 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     }
     }  // phase 1
 
-    // grab the group after next now (its atomic's latency hides behind phase 2). Taking
-    // groups early is safe: a phase 1 only ever waits on groups taken before its own, and
-    // every taken group reaches its phase 1 within two rounds.
-    if (wid == 0 && g0 < ntiles) {
-      gA = gB;
-      gB = atomicAdd(P.counter, lane == 0 ? 1u : 0u);
-    }
-    // LDS-DMA of the next round's tile into buf (phase 2 works in buf2): 8 x 1 KiB for the
-    // tile + 512 B of halo, lane-linear. Chunks that would read past the byte buffer are
-    // left to phase 1's fix-up (with the ones past the stream end).
-    pf = ~0ull;
-    if (g0 < ntiles && gn0 + wid < ntiles) {
-      const uint64_t t = gn0 + wid;
-      // ---- which stream / tile (the last stream's geometry is cached) ------------------------
-      if (t < c_tf || t >= c_tl) {
-        uint64_t lo = 0, hi = P.nstreams;
-        while (hi - lo > 1) {
-          const uint64_t mid = (lo + hi) >> 1;
-          if (P.tile_prefix[mid] <= t) lo = mid; else hi = mid;
-        }
-        c_s = uniform64(lo);
-        c_tf = uniform64(P.tile_prefix[c_s]);
-        c_tl = uniform64(P.tile_prefix[c_s + 1]);
-        c_so = uniform64(P.stream_off[c_s]);
-        c_se = uniform64(P.stream_off[c_s + 1]);
-        c_e0 = uniform64(c_so + (P.entry ? P.entry[c_s] : 0ull));
-      }
-      const uint64_t s = c_s, tf = c_tf, tl = c_tl, so = c_so, se = c_se;
-      const uint64_t A0 = so & ~(uint64_t)(TILE - 1);
-      const uint64_t A = A0 + (t - tf) * TILE;
-      (void)tl;
-      (void)s;
-      (void)se;
-#pragma unroll
-      for (int k = 0; k <= NV; k++) {
-        const uint64_t p = A + 1024u * k + 16u * lane;
-        if ((k < NV || lane < HALO / 16) && p + 16 <= P.nbytes)
-          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(P.bytes + p),
-                                           reinterpret_cast<__shared__ void *>(buf + 1024u * k), 16, 0, 0);
-      }
-      pf = t;
-    }
+    // (No grab ahead of phase 2: a group taken before a phase 2 that waits on a
+    // predecessor's phase 2 can close a wait cycle — the predecessor's holder may itself be
+    // in phase 1 waiting on Y of the group taken early. A group is only ever held while its
+    // phase 1 is running or done.)
 
     // ======== phase 2 of tile tp ===========================================================
     if (tp != ~0ull) {
@@ -1023,7 +956,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     };
     uint64_t x = e0;
     if (!first && wid > 0) {  // entry = the sibling's exact exit
-      x = uniform64(lds_wait(&gxl[wid - 1], P.overflow, lane)) - 1;
+      x = uniform64(lds_wait(&gxl[wid - 1], P.overflow, lane, 32u)) - 1;
       STAT(ST_LB_OK0, 1);
     } else if (!first) {
       uint32_t nap = 1;
@@ -1201,7 +1134,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
         }
         if (cur == (int64_t)t - 1) { x = v; STAT(ST_LB_OKN, 1); break; }
         if (spin > SPIN_MAX) {
-          if (lane == 0) atomicOr(P.overflow, 2u);
+          if (lane == 0) atomicOr(P.overflow, 128u);
           x = MARK_TERM | vs;
           break;
         }
@@ -1211,9 +1144,9 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     }
     x = uniform64(x);
 #pragma unroll
-    for (int k = 0; k < NV; k++) *reinterpret_cast<uint4 *>(buf2 + lane * B + 16 * k) = rv[k];
-    if (lane < HALO / 16) *reinterpret_cast<uint4 *>(buf2 + TILE + lane * 16) = rh;
-    if (lane < 2) *reinterpret_cast<uint4 *>(buf2 + TILE + HALO + lane * 16) = make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < NV; k++) *reinterpret_cast<uint4 *>(buf + lane * B + 16 * k) = rv[k];
+    if (lane < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + lane * 16) = rh;
+    if (lane < 2) *reinterpret_cast<uint4 *>(buf + TILE + HALO + lane * 16) = make_uint4(0, 0, 0, 0);
     entry[lane] = -1;
     wsync();
     TSTAMP(3);
@@ -1290,7 +1223,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           if (cur >= ve) break;
           const uint32_t r = (uint32_t)(cur - A);
           if (lane == 0 && entry[r / B] < 0) entry[r / B] = (int32_t)r;
-          const Hdr h = parse_hdr_lds(buf2, A, cur, se);
+          const Hdr h = parse_hdr_lds(buf, A, cur, se);
           if (h.kind != H_VALID) break;
           cur = uniform64(h.succ);
         }
@@ -1315,7 +1248,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           uint64_t cur = A + (uint32_t)myent;
           for (;;) {
             if (cur >= lhi) { wend = cur; break; }
-            const Hdr h = parse_hdr_lds(buf2, A, cur, se);
+            const Hdr h = parse_hdr_lds(buf, A, cur, se);
             if (hdr_delivered(h)) { sbit<NW>(dmask, (uint32_t)(cur - lb)); cnt++; }
             if (h.kind != H_VALID) { wend = MARK_TERM | cur; break; }
             cur = h.succ;
@@ -1352,7 +1285,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     // and tiles (aggc), publishing the inclusive prefix of every boundary passed (helping).
     uint64_t base = 0;
     if (t > 0 && wid > 0) {  // the sibling's inclusive prefix
-      base = uniform64(lds_wait(&gcl[wid - 1], P.overflow, lane)) - 1;
+      base = uniform64(lds_wait(&gcl[wid - 1], P.overflow, lane, 64u)) - 1;
     } else if (t > 0) {
       uint32_t nap = 1;
       int64_t cur = -2;  // tile whose inclusive prefix v is known (-1: virtual tile before 0)
@@ -1441,7 +1374,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
         }
         if (cur == (int64_t)t - 1) { base = v; break; }
         if (++spin > SPIN_MAX) {
-          if (lane == 0) atomicOr(P.overflow, 2u);
+          if (lane == 0) atomicOr(P.overflow, 256u);
           break;
         }
         STAT(ST_CNT_SPINS, 1);
@@ -1475,7 +1408,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
         const uint32_t o = 64u * w + (uint32_t)__builtin_ctzll(bits);
         bits &= bits - 1;
         const uint64_t pos = lb + o;
-        const Hdr h = parse_hdr_lds(buf2, A, pos, se);
+        const Hdr h = parse_hdr_lds(buf, A, pos, se);
         const uint64_t f = base + myoff + k;
         k++;
         const uint64_t po = pos + h.vlen + 1;
@@ -1487,7 +1420,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
           P.payload_len[f] = pl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pl;
           P.type[f] = (uint8_t)ty;
           if (h.id == 1) {
-            const LdsReader rd{buf2, A, umin64(A + TILE + HALO, se)};
+            const LdsReader rd{buf, A, umin64(A + TILE + HALO, se)};
             ChangeCols c = decode_change(rd, po, pl);
             if (c.err == ERR_UNREACHABLE) {
               const GlobalReader gr{P.bytes, se};
