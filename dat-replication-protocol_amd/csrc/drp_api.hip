@@ -77,6 +77,7 @@ struct drp_ctx {
   hipEvent_t ev[4] = {};
   uint32_t B = 128;
   int strict = 0;
+  int exact = 0;  // 1: always the exact kernel (decode_tiles), never the speculative one
   int cus = 256;
   uint32_t waves_per_cu = 16;
   DevBuf scratch, in_stage, out_stage, aux;
@@ -117,6 +118,7 @@ int drp_open(int device, drp_ctx **out) {
     uint32_t tb = (uint32_t)atoi(t);
     if (tb == 4096 || tb == 8192) c->B = tb / 64;
   }
+  if (const char *d = getenv("DRP_DECODE")) c->exact = strcmp(d, "exact") == 0;
   if (const char *w = getenv("DRP_WAVES_PER_CU")) {
     int v = atoi(w);
     if (v > 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
@@ -160,6 +162,12 @@ int drp_set_tile(drp_ctx *c, uint32_t tile_bytes) {
   return DRP_OK;
 }
 
+int drp_set_exact(drp_ctx *c, int exact) {
+  if (!c) return DRP_E_INVAL;
+  c->exact = exact ? 1 : 0;
+  return DRP_OK;
+}
+
 int drp_set_strict(drp_ctx *c, int strict) {
   if (!c) return DRP_E_INVAL;
   c->strict = strict ? 1 : 0;
@@ -169,7 +177,7 @@ int drp_set_strict(drp_ctx *c, int strict) {
 // scratch layout for a decode of `nbytes` over `ns` streams
 struct DecLayout {
   uint64_t ntiles_max;
-  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, total;
+  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, tstream, ent, scan_tmp, total;
   uint64_t nsg;
 };
 static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
@@ -181,10 +189,13 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.rec = o; o += al(6 * L.ntiles_max * 8);    // ywd, aggv, aggn, inclx, aggc, inclc (zeroed per call)
   L.nsg = L.ntiles_max / 64 + 2;
   L.sgrp = o; o += al(L.nsg * 32);             // sgc_agg+sgc_cnt (u32 x2), sagg, saggn, scnt (zeroed)
-  L.tiles = o; o += al(3 * L.ntiles_max * 8);  // exit, base, count
+  L.tiles = o; o += al(5 * L.ntiles_max * 8);  // exit, base, count, changes, changes prefix
   L.perr = o; o += al(ns * 8);
   L.scount = o; o += al(2 * ns * 8);
   L.ctrl = o; o += 256;
+  L.tstream = o; o += al(L.ntiles_max * 4);    // tile -> stream (speculative kernel)
+  L.ent = o; o += al(L.ntiles_max * 128);      // per-thread entries (speculative kernel)
+  L.scan_tmp = o; o += al((L.ntiles_max / 4096 + 2) * 8);  // tile scans: block sums
   L.total = o;
   return L;
 }
@@ -197,7 +208,7 @@ uint64_t drp_decode_scratch_bytes(drp_ctx *c, uint64_t n, uint64_t nstreams) {
 
 namespace {
 
-int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
+int run_decode_exact(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
                const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
                uint64_t cap, drp_stream_result *res) {
   if (ns == 0) return DRP_OK;
@@ -287,7 +298,12 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
   TRACE("decode: nbytes=%llu ns=%llu B=%u grid=%u NT=%llu", (unsigned long long)nbytes,
         (unsigned long long)ns, c->B, grid, (unsigned long long)NT);
   CHK(hipEventRecord(c->ev[1], st));
+  P.tile_nch = tiles + 3 * NT;
+  P.tile_nch_base = tiles + 4 * NT;
   CHK(drp_launch_decode(c->B, &P, grid, st));
+  CHK(drp_launch_tile_scan(P.tile_nch, tile_prefix, ns, NT, c->scratch.at<uint64_t>(L.scan_tmp), P.tile_nch_base,
+                           ~0ull, P.overflow, st));
+  CHK(drp_launch_stream_counts(tile_prefix, ns, P.tile_count, P.tile_base, P.tile_nch, P.tile_nch_base, scount, st));
   CHK(hipEventRecord(c->ev[2], st));
   CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
                           scount, fr->type, co->flags, cap, res, st));
@@ -328,6 +344,130 @@ int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t
   if (h[1] & ~1u) return DRP_E_HIP;  // bounded wait expired / inconsistent walk inside the kernel
   if (h[1]) return DRP_E_CAPACITY;
   return DRP_OK;
+}
+
+// The default decode: speculate-and-verify kernel (drp_decode_spec.hip). Returns DRP_E_RETRY
+// when a prediction failed (or a bounded wait expired): the caller then runs the exact kernel.
+int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
+                    const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
+                    uint64_t cap, drp_stream_result *res) {
+  if (((uintptr_t)bytes & 15) != 0) return DRP_E_INVAL;
+  const uint32_t B = drp_spec_tile_bytes() / 64;
+  const DecLayout L = dec_layout(B, nbytes, ns);
+  if (!c->scratch.ensure(L.total)) return DRP_E_NOMEM;
+  const uint64_t NT = L.ntiles_max;
+  uint64_t *tile_prefix = c->scratch.at<uint64_t>(L.tile_prefix);
+  uint64_t *rec = c->scratch.at<uint64_t>(L.rec);
+  uint64_t *tiles = c->scratch.at<uint64_t>(L.tiles);
+  uint64_t *perr = c->scratch.at<uint64_t>(L.perr);
+  uint64_t *scount = c->scratch.at<uint64_t>(L.scount);
+  uint32_t *ctrl = c->scratch.at<uint32_t>(L.ctrl);
+  uint32_t *tstream = c->scratch.at<uint32_t>(L.tstream);
+  uint64_t *sgscan = c->scratch.at<uint64_t>(L.scan_tmp);
+  hipStream_t st = c->st;
+  CHK(hipEventRecord(c->ev[0], st));
+  CHK(hipMemsetAsync(rec, 0, 2 * NT * 8, st));  // claim, incl_e
+  CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
+  CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
+  CHK(hipMemsetAsync(ctrl, 0, 16, st));
+  CHK(drp_launch_tile_prefix(B, stream_off, ns, tile_prefix, st));
+  DecodeParams P;
+  memset(&P, 0, sizeof(P));
+  P.bytes = bytes;
+  P.nbytes = nbytes;
+  P.stream_off = stream_off;
+  P.entry = entry;
+  P.nstreams = ns;
+  P.tile_prefix = tile_prefix;
+  P.payload_off = fr->payload_off;
+  P.payload_len = fr->payload_len;
+  P.type = fr->type;
+  P.key_off = co->key_off;
+  P.key_len = co->key_len;
+  P.subset_off = co->subset_off;
+  P.subset_len = co->subset_len;
+  P.value_off = co->value_off;
+  P.value_len = co->value_len;
+  P.change = co->change;
+  P.from = co->from;
+  P.to = co->to;
+  P.flags = co->flags;
+  P.cap = cap;
+  P.claim = rec;
+  P.incl_e = rec + NT;
+  P.agg_n = rec + 2 * NT;
+  P.incl_n = rec + 3 * NT;
+  P.tile_exit = tiles;
+  P.tile_base = tiles + NT;
+  P.tile_count = tiles + 2 * NT;
+  P.payload_err = perr;
+  P.scount = scount;
+  P.counter = ctrl;
+  P.overflow = ctrl + 1;
+  P.ent = c->scratch.at<uint8_t>(L.ent);
+  P.tile_nch = tiles + 3 * NT;
+  P.tile_nch_base = tiles + 4 * NT;
+  unsigned long long *dstats = nullptr;
+  if (getenv("DRP_STATS")) {
+    CHK(hipMalloc((void **)&dstats, 64 * 8));
+    CHK(hipMemsetAsync(dstats, 0, 64 * 8, st));
+    P.stats = dstats;
+  }
+  CHK(hipEventRecord(c->ev[1], st));
+  CHK(drp_launch_decode_spec(&P, NT, ns, tstream, sgscan, st));
+  CHK(hipEventRecord(c->ev[2], st));
+  CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
+                          scount, fr->type, co->flags, cap, res, st));
+  CHK(hipEventRecord(c->ev[3], st));
+  uint32_t h[2];
+  CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  float ms = 0;
+  hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
+  c->timing.decode_ms = ms;
+  hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
+  c->timing.total_ms = ms;
+  c->timing.finalize_ms = 0;
+  c->timing.strict_reruns = 0;
+  TRACE("decode_spec done: tiles=%u flags=%#x", h[0], h[1]);
+  if (dstats) {
+    unsigned long long hs[56];
+    CHK(hipMemcpy(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost));
+    fprintf(stderr, "[drp-spec] misses=%llu", hs[0]);
+    for (unsigned k = 0; k < 5 && k < hs[0]; k++)
+      fprintf(stderr, " | t=%llu e=%#llx claim=%#llx exit=%#llx", hs[1 + 6 * k], hs[2 + 6 * k], hs[3 + 6 * k],
+              hs[4 + 6 * k]);
+    static const char *ph[] = {"k1_stage", "k1_cand", "k1_link", "k1_dense", "", "", "", "",
+                               "k2_stage", "k2_entry", "k2_link", "k3_stage", "k3_link", "k3_emit"};
+    for (int k = 0; k < 14; k++)
+      if (ph[k][0]) fprintf(stderr, " %s=%.0f", ph[k], (double)hs[40 + k] / (double)(h[0] ? h[0] : 1));
+    fprintf(stderr, " (avg cycles per tile)\n");
+    (void)hipFree(dstats);
+  }
+  if (h[1] & drp_spec_retry_mask()) return DRP_E_RETRY;
+  if (h[1]) return DRP_E_CAPACITY;
+  return DRP_OK;
+}
+
+int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
+               const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
+               uint64_t cap, drp_stream_result *res) {
+  if (ns == 0) return DRP_OK;
+  float spec_ms = 0, spec_total = 0;
+  if (!c->exact && !c->strict) {
+    const int r = run_decode_spec(c, bytes, nbytes, stream_off, entry, ns, fr, co, cap, res);
+    if (r != DRP_E_RETRY) return r;
+    spec_ms = c->timing.decode_ms;
+    spec_total = c->timing.total_ms;
+    TRACE("decode_spec: prediction failed, exact re-run");
+  }
+  const int r = run_decode_exact(c, bytes, nbytes, stream_off, entry, ns, fr, co, cap, res);
+  if (spec_total > 0) {  // report the whole cost of the call
+    c->timing.decode_ms += spec_ms;
+    c->timing.total_ms += spec_total;
+    c->timing.strict_reruns = 1;
+  }
+  return r;
 }
 
 // carve SoA outputs for `cap` frames out of a device buffer

@@ -68,8 +68,6 @@ enum : uint32_t {
     }                                        \
   } while (0)
 
-__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
-__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 
 // ---- tile maps in index form ----------------------------------------------------------
 // A tile's map sends the index (0..2) of its entry among the keys Y_{t-1} to the index of its
@@ -116,18 +114,6 @@ __device__ __forceinline__ void shr(const uint64_t (&a)[N], uint32_t d, uint64_t
   for (int i = 0; i < N; i++) o[i] = (a[i] >> d) | (i + 1 < N ? (a[i + 1] << (64 - d)) : 0ull);
 }
 
-// bit k of the result = MSB of byte k of x
-__device__ __forceinline__ uint32_t msb4(uint32_t x) {
-  return (((x >> 7) & 0x01010101u) * 0x01020408u) >> 24;
-}
-// MSB of each byte set iff that byte <= 2
-__device__ __forceinline__ uint32_t le2(uint32_t x) {
-  return ~(((x & 0x7F7F7F7Fu) + 0x7D7D7D7Du) | x) & 0x80808080u;
-}
-__device__ __forceinline__ void gather16(const uint4 v, uint32_t &m16, uint32_t &s16) {
-  m16 = msb4(v.x) | (msb4(v.y) << 4) | (msb4(v.z) << 8) | (msb4(v.w) << 12);
-  s16 = msb4(le2(v.x)) | (msb4(le2(v.y)) << 4) | (msb4(le2(v.z)) << 8) | (msb4(le2(v.w)) << 12);
-}
 
 __device__ __forceinline__ uint4 load16(const uint8_t *g, uint64_t p, uint64_t se) {
   if (p + 16 <= se) return *reinterpret_cast<const uint4 *>(g + p);
@@ -1444,15 +1430,14 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
       }
     }
     nch = wave_sum32(nch);
-    nbl = wave_sum32(nbl);
+    (void)nbl;
 #pragma unroll
     for (uint32_t m = 1; m < WAVE; m <<= 1) {
       const uint64_t o = ((uint64_t)shfl_xor32((uint32_t)(badf >> 32), m) << 32) | shfl_xor32((uint32_t)badf, m);
       badf = o < badf ? o : badf;
     }
     if (lane == 0) {
-      if (nch) atomicAdd((unsigned long long *)&P.scount[2 * s], (unsigned long long)nch);
-      if (nbl) atomicAdd((unsigned long long *)&P.scount[2 * s + 1], (unsigned long long)nbl);
+      P.tile_nch[t] = nch;  // per-stream counts: scan + stream_counts (no same-address atomics)
       if (badf != ~0ull) atomicMin((unsigned long long *)&P.payload_err[s], (unsigned long long)badf);
       P.tile_exit[t] = exit_t;
       P.tile_base[t] = base;

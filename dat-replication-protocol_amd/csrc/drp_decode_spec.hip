@@ -1,0 +1,854 @@
+// drp_decode_spec.hip — gfx950 decode, speculate-and-verify form (the default path).
+//
+// Replaces the per-frame loop of decode.js (Decoder._consume / _onheader / _onchangedata /
+// _onchangeend / _onblobdata, decode.js:144-262) and messages.Change.decode
+// (messages/index.js:5), like decode_tiles (drp_decode.hip), but with far less work per byte.
+//
+// Frames carry no sync marker, so a tile's first frame start e_t depends on every byte before
+// it. decode_tiles resolves that exactly for every possible entry (lane DP + pointer doubling);
+// this kernel instead *predicts* each tile's exit and proves the prediction afterwards:
+//
+//   1. stage     One workgroup = one 8 KiB tile (128 threads x 64 B) + a 512 B halo, read
+//                from HBM once (dwordx4, coalesced) into LDS.
+//   2. spec      Every thread takes the first live position of its 64 B whose header chain
+//                survives KSTRONG frames ("strong" candidate). False chains in byte-random data
+//                die with ~98% probability per frame; the stream's own chain never dies. The
+//                threads' chains are linked (a thread continues the chain that enters it) by a
+//                few Jacobi rounds; the chain's exit past the tile is the tile's *claim*
+//                (or "identity" when no chain survives: the tile sits inside a long payload).
+//                The claim is published at once — it does not depend on the tile's entry.
+//   3. entry     Decoupled look-back over claims: e_t = the nearest predecessor claim that is
+//                not identity (or the stream entry). Helping publishes inclusive values.
+//   4. verify    The exact chain from e_t is walked (Jacobi again, seeded with the spec
+//                chain, so usually one round). Its exit must equal claim_t (or e_t for an
+//                identity claim); by induction from the stream entry every e_t is then exact.
+//                Any mismatch raises SPEC_MISS and the host re-runs the exact kernel
+//                (decode_tiles), so results never depend on the prediction.
+//   5. count     Exact frame count of the tile -> decoupled look-back (with helping) for the
+//                output base; frames are decoded from LDS into the SoA columns.
+//
+// Workgroups take tiles in stream order from an atomic ticket, so a tile only ever waits on
+// tiles already taken: no deadlock for any grid size. Cross-workgroup words are agent-scope
+// relaxed atomics whose values are self-validating (READY bit / value + 1).
+#include "drp_device.h"
+#include "drp_kernels.h"
+
+namespace drp {
+namespace spec {
+
+constexpr int NT = 128;                       // threads per workgroup
+constexpr uint32_t SEGB = 64;                 // bytes per thread
+constexpr uint32_t TILE = NT * SEGB;          // 8 KiB: the B = 128 tile geometry of tile_prefix
+constexpr uint32_t HALO = 512;
+constexpr uint32_t IMG = TILE + HALO;         // LDS image bytes (+32 slack)
+#ifndef DRP_VALIDATE_ALL
+#define DRP_VALIDATE_ALL 0  // 1: validate a candidate's own change even behind a 1-byte varint
+#endif
+#ifndef DRP_KSTRONG
+#define DRP_KSTRONG 4
+#endif
+constexpr int KSTRONG = DRP_KSTRONG;                    // frames a candidate chain must survive
+constexpr uint64_t RDY = 1ull << 63;          // published word: value | RDY
+constexpr uint64_t C_ID = 1ull << 62;         // claim: identity (no chain survives the tile)
+constexpr uint64_t M_ERR = 1ull << 60;        // with MARK_TERM: the chain ended at an error header
+constexpr uint64_t NONE = ~0ull;              // internal: no chain
+constexpr uint32_t SPIN = 1u << 22;
+constexpr uint32_t F_MISS = 1u << 12;         // overflow bit: prediction failed -> exact re-run
+constexpr uint32_t F_WAIT = 1u << 13;
+         // overflow bit: bounded wait expired -> exact re-run
+
+// header parse on a 16-byte window (same grammar as parse_hdr_lds)
+__device__ __forceinline__ Hdr parse_win(uint64_t w0, uint64_t w1, uint64_t p, uint64_t se) {
+  Hdr h;
+  h.succ = 0;
+  h.id = 0;
+  const uint64_t avail = se - p;
+  const uint32_t b0 = (uint32_t)(w0 & 0xFF);
+  if (b0 < 0x80u && avail >= 2) {  // one-byte length varint (the common case)
+    const uint32_t id = (uint32_t)((w0 >> 8) & 0xFF);
+    h.L = b0;
+    h.vlen = 1;
+    h.id = id;
+    if (id >= 3) { h.kind = H_ERR_TYPE; return h; }
+    if (id == 0) { h.kind = H_VALID; h.succ = p + 2; return h; }
+    if (b0 == 0) { h.kind = H_ERR_LEN; return h; }
+    if ((uint64_t)b0 > avail - 1) { h.kind = (id == 1) ? H_TAIL_CHANGE : H_TAIL_BLOB; return h; }
+    h.kind = H_VALID;
+    h.succ = p + 1 + b0;
+    return h;
+  }
+  uint64_t L;
+  const int k = win_varint(w0, w1, 0, avail, L);
+  h.L = L;
+  h.vlen = (uint32_t)(k > 0 ? k : 0);
+  if (k == 0) { h.kind = H_TAIL_HDR; return h; }
+  if (k < 0) { h.kind = (avail < 11) ? H_TAIL_HDR : H_ERR_VARINT; return h; }
+  if ((uint64_t)k >= avail) { h.kind = H_TAIL_HDR; return h; }
+  const uint32_t id = win_byte(w0, w1, (uint32_t)k);
+  h.id = id;
+  if (id >= 3) { h.kind = H_ERR_TYPE; return h; }
+  if (id == 0) { h.kind = H_VALID; h.succ = p + (uint64_t)k + 1; return h; }
+  if (L == 0) { h.kind = H_ERR_LEN; return h; }
+  if (L > avail - (uint64_t)k) { h.kind = (id == 1) ? H_TAIL_CHANGE : H_TAIL_BLOB; return h; }
+  h.kind = H_VALID;
+  h.succ = p + (uint64_t)k + L;
+  return h;
+}
+
+__device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t sh) {
+  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+__device__ __forceinline__ uint4 ld16(const uint8_t *g, uint64_t p, uint64_t se) {
+  if (p + 16 <= se) return *reinterpret_cast<const uint4 *>(g + p);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (uint32_t k = 0; k < 16; k++)
+    if (p + k < se) w[k >> 2] |= (uint32_t)g[p + k] << (8 * (k & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+struct Img {
+  const uint8_t *lds;  // LDS image: byte 0 = absolute position A
+  const uint8_t *g;    // the batch in HBM (16-byte aligned)
+  uint64_t A, se;
+  // header at absolute p < se: from LDS when its 16-byte window is inside the image,
+  // else from HBM (two aligned 16-byte loads; only chains probed past the halo get here)
+  __device__ __forceinline__ Hdr at(uint64_t p) const {
+    uint64_t w0, w1;
+    if (p + 16 <= A + IMG) {
+      lds_win16(lds, (uint32_t)(p - A), w0, w1);
+    } else {
+      const uint64_t a = p & ~15ull;
+      const uint4 u = ld16(g, a, se), v = ld16(g, a + 16, se);
+      const uint64_t q0 = ((uint64_t)u.y << 32) | u.x, q1 = ((uint64_t)u.w << 32) | u.z;
+      const uint64_t q2 = ((uint64_t)v.y << 32) | v.x, q3 = ((uint64_t)v.w << 32) | v.z;
+      const uint32_t o = (uint32_t)(p & 15);
+      if (o < 8) {
+        w0 = funnel(q0, q1, 8 * o);
+        w1 = funnel(q1, q2, 8 * o);
+      } else {
+        w0 = funnel(q1, q2, 8 * (o - 8));
+        w1 = funnel(q2, q3, 8 * (o - 8));
+      }
+    }
+    return parse_win(w0, w1, p, se);
+  }
+};
+
+__device__ __forceinline__ bool is_pos(uint64_t v) { return v < (1ull << 60); }
+__device__ __forceinline__ uint64_t term_of(const Hdr &h, uint64_t p) {
+  return MARK_TERM | (h.kind >= H_ERR_VARINT ? M_ERR : 0ull) | p;
+}
+
+// The chain from entry E through this thread's bytes [.., s1): returns the first chain position
+// >= s1 (or E itself when E >= s1 / is not a position), or MARK_TERM|q when the chain ends at
+// q (tail or error); n = frames delivered on the way (decode.js delivers id 1/2 and partial blobs).
+// Prediction-side plausibility of a valid frame at p (never used on the exact path): a change
+// frame behind a multi-byte length varint must hold a well-formed Change when it ends inside
+// the LDS image. Shadow headers whose varint swallows a real header's first bytes declare
+// ~10 KB+ "frames" whose payload runs on into the next frames' headers; real long frames
+// (4 KB values) cost one field walk.
+__device__ __forceinline__ bool plausible(const Img &m, uint64_t p, const Hdr &h, bool any_len) {
+  if (h.id != 1 || (!any_len && h.vlen < 2) || h.succ > m.A + IMG) return true;
+  const LdsReader rd{m.lds, m.A, umin64(m.A + IMG, m.se)};
+  const ChangeCols cc = decode_change(rd, p + h.vlen + 1, h.L - 1);
+  return !cc.err || cc.err == ERR_UNREACHABLE;
+}
+
+template <bool SPEC = false>
+__device__ __forceinline__ uint64_t walk(const Img &m, uint64_t E, uint64_t s1, uint32_t &n) {
+  n = 0;
+  if (!is_pos(E)) return E;
+  uint64_t p = E;
+  while (p < s1 && p < m.se) {
+    const Hdr h = m.at(p);
+    if (SPEC && h.kind == H_VALID && !plausible(m, p, h, false)) return MARK_TERM | M_ERR | p;
+    if (h.kind == H_VALID) {
+      n += h.id != 0;
+      p = h.succ;
+      continue;
+    }
+    n += h.kind == H_TAIL_BLOB;
+    return term_of(h, p);
+  }
+  return p;
+}
+
+// Candidate c is strong if its chain survives KSTRONG frames (or reaches the stream end / a
+// tail there after at least three frames) and its frames pass plausible(). far = its first
+// frame ends past the tile. LOCAL: steps stay inside the LDS image; a chain that leaves it
+// returns S_HBM (undecided) instead of reading HBM. On success also returns walk(c) for this
+// thread (exit past s1 and the frames delivered in the thread's bytes).
+enum : uint32_t { S_DEAD = 0, S_OK = 1, S_HBM = 2 };
+template <bool LOCAL>
+__device__ __forceinline__ uint32_t strong(const Img &m, uint64_t c, uint64_t s1, uint64_t &R, uint32_t &n,
+                                           bool &far) {
+  uint64_t p = c;
+  n = 0;
+  R = NONE;
+  far = false;
+#pragma unroll 1
+  for (int k = 0; k < KSTRONG; k++) {
+    if (p >= m.se) break;  // reached the stream end: survived
+    if (LOCAL && p + 16 > m.A + IMG) return S_HBM;
+    const Hdr h = m.at(p);
+    if (h.kind == H_VALID) {
+      if (k == 0) far = h.succ >= m.A + TILE;
+      if (!plausible(m, p, h, DRP_VALIDATE_ALL && k == 0)) return S_DEAD;
+      if (p < s1) n += h.id != 0;
+      p = h.succ;
+      if (R == NONE && p >= s1) R = p;
+      continue;
+    }
+    // errors kill the candidate; so does a tail soon after it: shadow headers with long
+    // varints declare lengths past the stream end, real tails only end a long chain
+    if (h.kind >= H_ERR_VARINT || k < 3) return S_DEAD;
+    if (R == NONE) {  // the tail is inside this thread's bytes
+      n += h.kind == H_TAIL_BLOB;
+      R = term_of(h, p);
+    }
+    return S_OK;
+  }
+  if (R == NONE) {  // many tiny frames: finish this thread's bytes
+    uint32_t n2;
+    R = walk<true>(m, p, s1, n2);
+    n += n2;
+  }
+  return S_OK;
+}
+
+// Link the threads' chains: thread l's entry is the exit of the latest thread before it whose
+// entry lies inside its own bytes (a "carrier"; threads in between are jumped over). Spec mode:
+// no carrier, or a carrier whose chain died at an error, restarts at the thread's own strong
+// candidate g. Verify mode: a virtual carrier before thread 0 exits at e_first, errors pass on.
+// One block-wide "latest carrier" scan per round; rounds repeat until no entry changes.
+template <bool VERIFY>
+__device__ __forceinline__ void link(const Img &m, uint64_t s1, uint64_t g, uint64_t e_first, uint64_t &E,
+                                     uint64_t &R, uint32_t &n, uint64_t *wl, uint32_t *fl, uint32_t *overflow,
+                                     bool *restart = nullptr) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  constexpr uint32_t NWV = NT / WAVE;
+  for (uint32_t round = 0;; round++) {
+    const bool carrier = is_pos(E) && E < s1;
+    uint64_t x = carrier ? R : NONE;  // inclusive "latest carrier exit" over the wave
+#pragma unroll
+    for (uint32_t d = 1; d < WAVE; d <<= 1) {
+      const uint64_t y = shfl_up64(x, d);
+      if (lane >= d && x == NONE) x = y;
+    }
+    if (lane == 63) wl[wid] = x;
+    __syncthreads();  // (A) wl of this round visible; fl reads of the last round are done
+    uint64_t prev = VERIFY ? e_first : NONE;  // latest carrier exit before this wave
+#pragma unroll
+    for (uint32_t w = 0; w < NWV; w++)
+      if (w < wid && wl[w] != NONE) prev = wl[w];
+    uint64_t ex = shfl_up64(x, 1);
+    if (lane == 0 || ex == NONE) ex = prev;
+    const bool rs = !VERIFY && (ex == NONE || ((ex & MARK_TERM) && (ex & M_ERR)));
+    const uint64_t En = VERIFY ? ex : (rs ? g : ex);
+    if (restart) *restart = rs;
+    const bool ch = En != E;
+    const uint64_t any = __ballot(ch);
+    if (lane == 0) fl[wid] = any != 0;
+    __syncthreads();  // (B) fl visible; wl reads of this round are done
+    uint32_t more = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NWV; w++) more |= fl[w];
+    if (!more) break;
+    if (round > NT + 2) {  // cannot happen: entries settle thread by thread
+      if (tid == 0) atomicOr(overflow, F_WAIT);
+      break;
+    }
+    if (ch) {
+      E = En;
+      R = walk<!VERIFY>(m, E, s1, n);
+    }
+  }
+}
+
+// block-wide reductions over the NT threads (two barriers; scratch: NT / WAVE words)
+__device__ __forceinline__ uint32_t block_max_u32(uint32_t v, uint32_t *xf) {
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (uint32_t k = 1; k < WAVE; k <<= 1) v = max(v, shfl_xor32(v, k));
+  if (lane == 0) xf[wid] = v;
+  __syncthreads();
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < NT / WAVE; w++) r = max(r, xf[w]);
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t *xf) {
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  v = wave_sum32(v);
+  if (lane == 0) xf[wid] = v;
+  __syncthreads();
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < NT / WAVE; w++) r += xf[w];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ uint64_t lane_min64(uint64_t v) {
+#pragma unroll
+  for (uint32_t k = 1; k < WAVE; k <<= 1) {
+    const uint64_t o = ((uint64_t)shfl_xor32((uint32_t)(v >> 32), k) << 32) | shfl_xor32((uint32_t)v, k);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// DRP_STATS=1: per-phase cycle sums of thread 0 in P.stats[40 + k] (profiling aid)
+#define PHASE(k)                                                          \
+  do {                                                                    \
+    if (P.stats && threadIdx.x == 0) {                                    \
+      const uint64_t now_ = __builtin_amdgcn_s_memtime();                 \
+      atomicAdd(&P.stats[40 + (k)], (unsigned long long)(now_ - tl_));    \
+      tl_ = now_;                                                         \
+    }                                                                     \
+  } while (0)
+
+// Tile geometry shared by both kernels.
+struct TileGeo {
+  uint64_t s, tf, so, se, A, e0;
+};
+__device__ __forceinline__ TileGeo tile_geo(const DecodeParams &P, uint64_t t) {
+  TileGeo G;
+  G.s = P.tile_stream ? P.tile_stream[t] : 0;
+  G.tf = P.tile_prefix[G.s];
+  G.so = P.stream_off[G.s];
+  G.se = P.stream_off[G.s + 1];
+  G.A = (G.so & ~(uint64_t)(TILE - 1)) + (t - G.tf) * TILE;
+  G.e0 = G.so + (P.entry ? P.entry[G.s] : 0ull);
+  return G;
+}
+
+__device__ __forceinline__ void stage(const DecodeParams &P, const TileGeo &G, uint8_t *buf) {
+  const uint32_t tid = threadIdx.x;
+  const uint64_t lb = G.A + (uint64_t)tid * SEGB;
+#pragma unroll
+  for (int k = 0; k < (int)(SEGB / 16); k++)
+    *reinterpret_cast<uint4 *>(buf + tid * SEGB + 16 * k) = ld16(P.bytes, lb + 16 * k, G.se);
+  if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = ld16(P.bytes, G.A + TILE + tid * 16, G.se);
+  if (tid < 2) *reinterpret_cast<uint4 *>(buf + IMG + tid * 16) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+}
+
+// Stage the tile (64 B per thread, coalesced dwordx4) and its halo into LDS; returns the
+// thread's live mask: positions in [max(so, A), se) whose bytes can start a header with
+// id <= 2 (a varint terminator followed by a byte <= 2, reached through a run of MSB bytes).
+__device__ __forceinline__ uint64_t stage_live(const DecodeParams &P, const TileGeo &G, uint8_t *buf) {
+  const uint32_t tid = threadIdx.x;
+  const uint64_t lb = G.A + (uint64_t)tid * SEGB;
+  uint4 v[SEGB / 16];
+#pragma unroll
+  for (int k = 0; k < (int)(SEGB / 16); k++) v[k] = ld16(P.bytes, lb + 16 * k, G.se);
+#pragma unroll
+  for (int k = 0; k < (int)(SEGB / 16); k++) *reinterpret_cast<uint4 *>(buf + tid * SEGB + 16 * k) = v[k];
+  if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = ld16(P.bytes, G.A + TILE + tid * 16, G.se);
+  if (tid < 2) *reinterpret_cast<uint4 *>(buf + IMG + tid * 16) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  uint32_t m16[5], s16[5];
+#pragma unroll
+  for (int k = 0; k < 4; k++) gather16(v[k], m16[k], s16[k]);
+  gather16(*reinterpret_cast<const uint4 *>(buf + tid * SEGB + SEGB), m16[4], s16[4]);
+  const uint64_t M0 = (uint64_t)m16[0] | ((uint64_t)m16[1] << 16) | ((uint64_t)m16[2] << 32) | ((uint64_t)m16[3] << 48);
+  const uint64_t S0 = (uint64_t)s16[0] | ((uint64_t)s16[1] << 16) | ((uint64_t)s16[2] << 32) | ((uint64_t)s16[3] << 48);
+  const uint64_t M1 = m16[4], S1 = s16[4];
+  uint64_t X[2], Mk[2];
+  X[0] = ~M0 & ((S0 >> 1) | (S1 << 63));
+  X[1] = ~M1 & (S1 >> 1);
+  Mk[0] = M0;
+  Mk[1] = M1;
+#pragma unroll
+  for (uint32_t d = 1; d <= 8; d <<= 1) {
+    const uint64_t x0 = (X[0] >> d) | (X[1] << (64 - d)), x1 = X[1] >> d;
+    X[0] |= Mk[0] & x0;
+    X[1] |= Mk[1] & x1;
+    if (d < 8) {
+      const uint64_t m0 = (Mk[0] >> d) | (Mk[1] << (64 - d)), m1 = Mk[1] >> d;
+      Mk[0] &= m0;
+      Mk[1] &= m1;
+    }
+  }
+  uint64_t live = X[0];
+  const uint64_t lo = G.so > lb ? G.so - lb : 0, hi = G.se > lb ? G.se - lb : 0;
+  if (lo >= 64 || hi == 0) live = 0;
+  else {
+    if (lo) live &= ~0ull << lo;
+    if (hi < 64) live &= (1ull << hi) - 1;
+  }
+  return live;
+}
+
+// ==== kernel 1: every tile's claim (entry-independent, no waiting) ===========================
+__global__ __launch_bounds__(NT) void spec_claims(DecodeParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+  __shared__ uint64_t xr[NT / WAVE];
+  __shared__ uint32_t xf[NT / WAVE];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u, wid = tid >> 6;
+  const uint64_t t = blockIdx.x;
+  uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
+  if (t >= P.tile_prefix[P.nstreams]) return;  // (whole workgroup)
+  const TileGeo G = tile_geo(P, t);
+  const uint64_t live = stage_live(P, G, buf);
+  const Img m{buf, P.bytes, G.A, G.se};
+  const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
+  PHASE(0);
+
+  // ---- strong candidate: the first live position whose chain survives, preferring chains
+  // that can be checked inside the LDS image (shadow headers whose varint swallows a real
+  // header jump ~10 KB+: checking them would cost a random HBM read each) ---------------------
+  uint64_t g = NONE, R = NONE;
+  uint32_t n = 0;
+  bool far = false;
+  uint64_t defer = 0;  // candidates whose check leaves the LDS image (decided in HBM if needed)
+  {
+    uint64_t bits = live;
+    while (bits) {
+      const uint32_t o = (uint32_t)__builtin_ctzll(bits);
+      bits &= bits - 1;
+      uint64_t r;
+      uint32_t k;
+      bool f;
+      const uint32_t st = strong<true>(m, lb + o, s1, r, k, f);
+      if (st == S_OK) {
+        g = lb + o;
+        R = r;
+        n = k;
+        far = f;
+        break;
+      }
+      if (st == S_HBM) defer |= 1ull << o;
+    }
+  }
+  // A chain that starts by jumping past the whole tile is trusted only when nothing later in
+  // the tile could start one: a shadow whose long jump happens to land on a real frame start
+  // survives any number of frames, but it jumps over the tile's real (dense) chain.
+  {
+    const uint64_t hm = __ballot(g != NONE);
+    if (lane == 0) xf[wid] = hm != 0;
+    __syncthreads();
+    bool later = lane < 63 && (hm >> (lane + 1)) != 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NT / WAVE; w++)
+      if (w > wid && xf[w]) later = true;
+    __syncthreads();
+    if (far && later) {
+      g = NONE;
+      R = NONE;
+      n = 0;
+    }
+  }
+  uint64_t E = g;
+  PHASE(1);
+  // ---- link the threads' chains ------------------------------------------------------------
+  link<false>(m, s1, g, NONE, E, R, n, xr, xf, P.overflow);
+  // A thread no chain reaches and without an LDS-decided candidate, with none later in the
+  // tile either, decides its deferred candidates in HBM (big frames: the chain from a real
+  // frame start leaves the image within a step or two), then the chains are linked again.
+  for (uint32_t it = 0; it < 3; it++) {
+    const uint64_t hm = __ballot(g != NONE);
+    if (lane == 0) xf[wid] = hm != 0;
+    __syncthreads();
+    bool later = lane < 63 && (hm >> (lane + 1)) != 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NT / WAVE; w++)
+      if (w > wid && xf[w]) later = true;
+    __syncthreads();
+    const bool need = E == NONE && defer && !later;
+    if (!block_max_u32(need ? 1u : 0u, xf)) break;
+    if (need) {
+      while (defer) {
+        const uint32_t o = (uint32_t)__builtin_ctzll(defer);
+        defer &= defer - 1;
+        uint64_t r;
+        uint32_t k;
+        bool f;
+        if (strong<false>(m, lb + o, s1, r, k, f) == S_OK) {
+          g = lb + o;
+          E = g;
+          R = r;
+          n = k;
+          break;
+        }
+      }
+    }
+    link<false>(m, s1, g, NONE, E, R, n, xr, xf, P.overflow);
+  }
+  PHASE(2);
+  // The chain's last frame may jump over threads that hold strong candidates: a shadow that
+  // joined the chain can jump far and land on a real frame start past the tile. Build the
+  // chain those candidates start as well and keep it when it is the denser one (>= 2
+  // frames where the first has one); a real long frame jumps over bytes with no candidate.
+  {
+    const bool carrier = is_pos(E) && E < s1;
+    const uint32_t js = block_max_u32(carrier ? tid + 1 : 0u, xf);  // last carrier + 1
+    const uint32_t after = block_max_u32(g != NONE && tid + 1 > js ? 1u : 0u, xf);
+    if (js && after) {
+      const uint64_t Ea = E, Ra = R;
+      const uint32_t na = n;
+      const bool mine = tid + 1 > js;
+      E = NONE;
+      R = NONE;
+      n = 0;
+      link<false>(m, s1, mine ? g : NONE, NONE, E, R, n, xr, xf, P.overflow);
+      const uint32_t nb = block_sum_u32(mine ? n : 0u, xf);
+      if (nb < 2 || !mine) {  // keep the first chain where the dense one does not apply
+        E = Ea;
+        R = Ra;
+        n = na;
+      }
+    }
+  }
+  PHASE(3);
+  P.ent[t * NT + tid] = is_pos(E) && E < s1 ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // seeds for kernel 2
+  if (tid == NT - 1) P.claim[t] = (R == NONE || ((R & MARK_TERM) && (R & M_ERR))) ? C_ID : R;
+}
+
+// ==== kernel 2: exact entries, verification, frame counts =====================================
+// e_t = the nearest claim before t that is not identity (or the stream entry); claims are final,
+// so nothing here waits. Publishes incl_e[t] = e_{t+1} for kernel 3 and for later tiles.
+__global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+  __shared__ uint64_t xr[NT / WAVE];
+  __shared__ uint32_t xf[NT / WAVE];
+  __shared__ uint64_t sh_e;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u, wid = tid >> 6;
+  const uint64_t t = blockIdx.x;
+  uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
+  if (t >= P.tile_prefix[P.nstreams]) return;  // (whole workgroup)
+  const TileGeo G = tile_geo(P, t);
+  const uint64_t live = stage_live(P, G, buf);
+  const Img m{buf, P.bytes, G.A, G.se};
+  const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
+  PHASE(8);
+  if (wid == 0) {
+    uint64_t e = G.e0;
+    if (t != G.tf) {
+      int64_t j0 = (int64_t)t - 1;
+      for (;;) {
+        const int64_t j = j0 - (int64_t)lane;
+        const bool virt = j < (int64_t)G.tf;
+        uint64_t ie = 0, cl = C_ID;
+        if (!virt) {
+          ie = ld_agent(&P.incl_e[j]);
+          if (!ie) cl = P.claim[j];
+        }
+        const uint64_t sm = __ballot(virt || ie || cl != C_ID);
+        if (sm) {
+          const uint32_t k = (uint32_t)__builtin_ctzll(sm);
+          e = readlane64(virt ? G.e0 : (ie ? (ie & ~RDY) : cl), k);
+          if (lane < k) st_agent(&P.incl_e[j], e | RDY);  // helping: identity tiles pass e on
+          break;
+        }
+        j0 -= WAVE;  // 64 identity claims: keep looking back
+      }
+    }
+    if (lane == 0) sh_e = e;
+  }
+  __syncthreads();
+  const uint64_t et = sh_e;
+  const uint64_t claim = P.claim[t];
+  if (tid == NT - 1) st_agent(&P.incl_e[t], (claim == C_ID ? et : claim) | RDY);
+  PHASE(9);
+  // the exact chain from e_t, seeded with the predicted chain's per-thread entries
+  const uint8_t sb = P.ent[t * NT + tid];
+  uint64_t E = sb < SEGB ? lb + sb : (live ? lb + (uint32_t)__builtin_ctzll(live) : NONE);
+  uint32_t n = 0;
+  uint64_t R = walk(m, E, s1, n);
+  link<true>(m, s1, NONE, et, E, R, n, xr, xf, P.overflow);
+  P.ent[t * NT + tid] = is_pos(E) && E < s1 ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // exact, for kernel 3
+  PHASE(10);
+  const uint32_t count_t = block_sum_u32(n, xf);
+  uint32_t nc = 0;  // change frames among them
+  if (n) {
+    uint64_t p = E;
+    while (p < s1 && p < G.se) {
+      const Hdr h = m.at(p);
+      nc += h.id == 1 && (h.kind == H_VALID);
+      if (h.kind != H_VALID) break;
+      p = h.succ;
+    }
+  }
+  const uint32_t nch_t = block_sum_u32(nc, xf);
+  // the last thread's R is the tile's exact exit; it must be what the claim predicted (an
+  // error on the exact chain never is: predictions restart after errors)
+  if (tid == NT - 1) {
+    const uint64_t exit_t = (R & MARK_TERM) ? (R & ~M_ERR) : R;
+    const uint64_t want = claim == C_ID ? et : claim;
+    if (exit_t != want || ((R & MARK_TERM) && (R & M_ERR))) {
+      atomicOr(P.overflow, F_MISS);
+      if (P.stats) {  // debug capture (DRP_STATS=1): the first misses
+        const unsigned long long k = atomicAdd(&P.stats[0], 1ull);
+        if (k < 5) {
+          P.stats[1 + 6 * k] = t;
+          P.stats[2 + 6 * k] = et;
+          P.stats[3 + 6 * k] = claim;
+          P.stats[4 + 6 * k] = R;
+        }
+      }
+    }
+    P.tile_exit[t] = exit_t;
+    P.tile_count[t] = count_t;
+    P.tile_nch[t] = nch_t;
+  }
+}
+
+// ==== scan: tile_base = exclusive prefix of tile_count (reduce, top, down-sweep) ================
+constexpr uint32_t SCAN_BLK = 1024, SCAN_PER = 4, SCAN_SPAN = SCAN_BLK * SCAN_PER;
+
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *sw, uint64_t &total) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (uint32_t d = 1; d < WAVE; d <<= 1) {
+    const uint64_t y = shfl_up64(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) sw[wid] = x;
+  __syncthreads();
+  uint64_t off = 0;
+  total = 0;
+  for (uint32_t w = 0; w < blockDim.x / WAVE; w++) {
+    if (w < wid) off += sw[w];
+    total += sw[w];
+  }
+  __syncthreads();
+  return off + x - v;
+}
+
+__global__ __launch_bounds__(SCAN_BLK) void scan_reduce(const uint64_t *cnt, const uint64_t *tile_prefix,
+                                                         uint64_t nstreams, uint64_t *bsum) {
+  __shared__ uint64_t sw[SCAN_BLK / WAVE];
+  const uint64_t nt = tile_prefix[nstreams];
+  const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_SPAN + threadIdx.x * SCAN_PER;
+  uint64_t v = 0;
+  for (uint32_t k = 0; k < SCAN_PER; k++)
+    if (i0 + k < nt) v += cnt[i0 + k];
+  uint64_t total;
+  (void)block_excl_scan64(v, sw, total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(SCAN_BLK) void scan_top(uint64_t *bsum, uint64_t nb) {
+  __shared__ uint64_t sw[SCAN_BLK / WAVE];
+  uint64_t carry = 0;
+  for (uint64_t c0 = 0; c0 < nb; c0 += SCAN_BLK) {
+    const uint64_t i = c0 + threadIdx.x;
+    const uint64_t v = i < nb ? bsum[i] : 0;
+    uint64_t total;
+    const uint64_t ex = block_excl_scan64(v, sw, total);
+    if (i < nb) bsum[i] = carry + ex;
+    carry += total;
+  }
+}
+
+__global__ __launch_bounds__(SCAN_BLK) void scan_down(const uint64_t *cnt, const uint64_t *tile_prefix,
+                                                       uint64_t nstreams, const uint64_t *bsum, uint64_t *base,
+                                                       uint64_t cap, uint32_t *overflow) {
+  __shared__ uint64_t sw[SCAN_BLK / WAVE];
+  const uint64_t nt = tile_prefix[nstreams];
+  const uint64_t i0 = (uint64_t)blockIdx.x * SCAN_SPAN + threadIdx.x * SCAN_PER;
+  uint64_t c[SCAN_PER], v = 0;
+  for (uint32_t k = 0; k < SCAN_PER; k++) {
+    c[k] = i0 + k < nt ? cnt[i0 + k] : 0;
+    v += c[k];
+  }
+  uint64_t total;
+  uint64_t o = bsum[blockIdx.x] + block_excl_scan64(v, sw, total);
+  for (uint32_t k = 0; k < SCAN_PER; k++) {
+    if (i0 + k < nt) {
+      base[i0 + k] = o;
+      if (i0 + k == nt - 1 && o + c[k] > cap) atomicOr(overflow, 1u);
+    }
+    o += c[k];
+  }
+}
+
+// ==== kernel 3: emission ========================================================================
+// Frame-major: the tile's frame starts go to an LDS list (thread order = stream order), then
+// thread i decodes frames i, i + NT, ... so every column store is a contiguous run.
+constexpr uint32_t LCAP = 1024;  // frames per tile listed in LDS (denser tiles emit per thread)
+
+__device__ __noinline__ ChangeCols decode_change_hbm(const uint8_t *g, uint64_t se, uint64_t po, uint64_t pl) {
+  const GlobalReader gr{g, se};
+  return decode_change(gr, po, pl);
+}
+
+__device__ __forceinline__ void emit_frame(const DecodeParams &P, const Img &m, uint64_t p, uint64_t f,
+                                           uint32_t &nch, uint32_t &nbl, uint64_t &badf) {
+  const Hdr h = m.at(p);
+  const uint64_t po = p + h.vlen + 1;
+  const uint64_t pl = h.L - 1;
+  if (h.id == 1) nch++; else nbl++;
+  if (f >= P.cap) return;
+  P.payload_off[f] = po;
+  P.payload_len[f] = pl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pl;
+  P.type[f] = (uint8_t)(h.id | (h.kind == H_TAIL_BLOB ? DRP_FRAME_PARTIAL : 0u));
+  if (h.id != 1) return;
+  const LdsReader rd{m.lds, m.A, umin64(m.A + IMG, m.se)};
+  ChangeCols c = decode_change(rd, po, pl);
+  if (c.err == ERR_UNREACHABLE) c = decode_change_hbm(P.bytes, m.se, po, pl);
+  P.key_off[f] = c.key_off;
+  P.key_len[f] = c.key_len;
+  P.subset_off[f] = c.subset_off;
+  P.subset_len[f] = c.subset_len;
+  P.value_off[f] = c.value_off;
+  P.value_len[f] = c.value_len;
+  P.change[f] = c.change;
+  P.from[f] = c.from;
+  P.to[f] = c.to;
+  uint32_t fl = c.flags;
+  if (c.err == DRP_ERR_REQUIRED) fl |= DRP_F_MISSING;
+  P.flags[f] = (uint8_t)fl;
+  if (c.err) badf = f < badf ? f : badf;
+}
+
+__global__ __launch_bounds__(NT) void emit_tiles(DecodeParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+  __shared__ uint16_t lst[LCAP];
+  __shared__ uint32_t wsum[NT / WAVE];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u, wid = tid >> 6;
+  const uint64_t t = blockIdx.x;
+  uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
+  if (t >= P.tile_prefix[P.nstreams]) return;  // (whole workgroup)
+  const TileGeo G = tile_geo(P, t);
+  const uint64_t se = G.se, A = G.A;
+  stage(P, G, buf);
+  const Img m{buf, P.bytes, A, se};
+  const uint64_t lb = A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
+  const uint64_t base = P.tile_base[t];
+  const uint8_t eb = P.ent[t * NT + tid];  // exact entry of this thread's bytes (kernel 2)
+  const uint64_t E = eb < SEGB ? lb + eb : NONE;
+  PHASE(11);
+  uint32_t n = 0;
+  (void)walk(m, E, s1, n);
+  const uint32_t ni = wave_incl_scan32(n);
+  if (lane == 63) wsum[wid] = ni;
+  __syncthreads();
+  uint32_t woff = 0, count_t = 0;
+#pragma unroll
+  for (int w = 0; w < NT / WAVE; w++) {
+    if ((uint32_t)w < wid) woff += wsum[w];
+    count_t += wsum[w];
+  }
+  PHASE(12);
+  uint32_t nch = 0, nbl = 0;
+  uint64_t badf = ~0ull;
+  const bool listed = count_t <= LCAP;
+  // this thread's frames, in order: list them (or, for very dense tiles, emit them here)
+  if (n) {
+    uint32_t i = woff + ni - n;
+    uint64_t p = E;
+    while (p < s1 && p < se) {
+      const Hdr h = m.at(p);
+      if (h.kind != H_VALID && h.kind != H_TAIL_BLOB) break;
+      if (h.id != 0) {
+        if (listed) lst[i] = (uint16_t)(p - A);
+        else emit_frame(P, m, p, base + i, nch, nbl, badf);
+        i++;
+      }
+      if (h.kind != H_VALID) break;
+      p = h.succ;
+    }
+  }
+  if (listed) {
+    __syncthreads();
+    for (uint32_t i = tid; i < count_t; i += NT) emit_frame(P, m, A + lst[i], base + i, nch, nbl, badf);
+  }
+  PHASE(13);
+  (void)nch;
+  (void)nbl;
+  badf = lane_min64(badf);
+  if (lane == 0 && badf != ~0ull) atomicMin((unsigned long long *)&P.payload_err[G.s], (unsigned long long)badf);
+}
+
+// per-stream change / blob counts (one thread per stream)
+__global__ void stream_counts_kernel(const uint64_t *tile_prefix, uint64_t nstreams, const uint64_t *count,
+                                     const uint64_t *base, const uint64_t *nch, const uint64_t *nch_base,
+                                     uint64_t *scount) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nstreams) return;
+  const uint64_t tf = tile_prefix[s], tl = tile_prefix[s + 1];
+  uint64_t ch = 0, fr = 0;
+  if (tl > tf) {
+    ch = nch_base[tl - 1] + nch[tl - 1] - nch_base[tf];
+    fr = base[tl - 1] + count[tl - 1] - base[tf];
+  }
+  scount[2 * s] = ch;
+  scount[2 * s + 1] = fr - ch;
+}
+
+// tile -> stream (one thread per tile; binary search over tile_prefix)
+__global__ void tile_stream_kernel(const uint64_t *tile_prefix, uint64_t nstreams, uint64_t nt_max,
+                                   uint32_t *tile_stream) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nt_max) return;
+  const uint64_t ntiles = tile_prefix[nstreams];
+  if (t >= ntiles) return;
+  uint64_t lo = 0, hi = nstreams;
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (tile_prefix[mid] <= t) lo = mid; else hi = mid;
+  }
+  tile_stream[t] = (uint32_t)lo;
+}
+
+}  // namespace spec
+}  // namespace drp
+
+using namespace drp;
+
+extern "C" hipError_t drp_launch_tile_scan(const uint64_t *in, const uint64_t *tile_prefix, uint64_t nstreams,
+                                           uint64_t nt_max, uint64_t *tmp, uint64_t *out, uint64_t cap,
+                                           uint32_t *overflow, hipStream_t st) {
+  if (nt_max == 0) return hipSuccess;
+  const uint32_t nb = (uint32_t)((nt_max + spec::SCAN_SPAN - 1) / spec::SCAN_SPAN);
+  hipLaunchKernelGGL(spec::scan_reduce, dim3(nb), dim3(spec::SCAN_BLK), 0, st, in, tile_prefix, nstreams, tmp);
+  hipLaunchKernelGGL(spec::scan_top, dim3(1), dim3(spec::SCAN_BLK), 0, st, tmp, (uint64_t)nb);
+  hipLaunchKernelGGL(spec::scan_down, dim3(nb), dim3(spec::SCAN_BLK), 0, st, in, tile_prefix, nstreams,
+                     (const uint64_t *)tmp, out, cap, overflow);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t drp_launch_stream_counts(const uint64_t *tile_prefix, uint64_t nstreams, const uint64_t *count,
+                                               const uint64_t *base, const uint64_t *nch, const uint64_t *nch_base,
+                                               uint64_t *scount, hipStream_t st) {
+  if (nstreams == 0) return hipSuccess;
+  const uint32_t blk = 256;
+  hipLaunchKernelGGL(spec::stream_counts_kernel, dim3((uint32_t)((nstreams + blk - 1) / blk)), dim3(blk), 0, st,
+                     tile_prefix, nstreams, count, base, nch, nch_base, scount);
+  return hipGetLastError();
+}
+
+extern "C" uint32_t drp_spec_tile_bytes(void) { return spec::TILE; }
+extern "C" uint32_t drp_spec_retry_mask(void) { return spec::F_MISS | spec::F_WAIT; }
+
+extern "C" hipError_t drp_launch_decode_spec(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
+                                             uint32_t *tile_stream, uint64_t *scan_tmp, hipStream_t st) {
+  if (nt_max == 0) return hipSuccess;
+  DecodeParams Q = *P;
+  Q.tile_stream = nullptr;
+  if (nstreams > 1) {
+    const uint32_t blk = 256;
+    hipLaunchKernelGGL(spec::tile_stream_kernel, dim3((uint32_t)((nt_max + blk - 1) / blk)), dim3(blk), 0, st,
+                       P->tile_prefix, nstreams, nt_max, tile_stream);
+    Q.tile_stream = tile_stream;
+  }
+  const uint32_t grid = (uint32_t)nt_max;
+  hipLaunchKernelGGL(spec::spec_claims, dim3(grid), dim3(spec::NT), 0, st, Q);
+  hipLaunchKernelGGL(spec::verify_counts, dim3(grid), dim3(spec::NT), 0, st, Q);
+  hipError_t e = drp_launch_tile_scan(Q.tile_count, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_base, Q.cap,
+                                     Q.overflow, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(spec::emit_tiles, dim3(grid), dim3(spec::NT), 0, st, Q);
+  e = drp_launch_tile_scan(Q.tile_nch, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_nch_base, ~0ull, Q.overflow, st);
+  if (e != hipSuccess) return e;
+  return drp_launch_stream_counts(Q.tile_prefix, nstreams, Q.tile_count, Q.tile_base, Q.tile_nch, Q.tile_nch_base,
+                                  Q.scount, st);
+}

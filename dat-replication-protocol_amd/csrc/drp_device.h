@@ -327,6 +327,22 @@ bad:
   return c;
 }
 
+// ---- byte-class bit masks (live-position scan) ------------------------------------
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+// bit k of the result = MSB of byte k of x
+__device__ __forceinline__ uint32_t msb4(uint32_t x) {
+  return (((x >> 7) & 0x01010101u) * 0x01020408u) >> 24;
+}
+// MSB of each byte set iff that byte <= 2
+__device__ __forceinline__ uint32_t le2(uint32_t x) {
+  return ~(((x & 0x7F7F7F7Fu) + 0x7D7D7D7Du) | x) & 0x80808080u;
+}
+__device__ __forceinline__ void gather16(const uint4 v, uint32_t &m16, uint32_t &s16) {
+  m16 = msb4(v.x) | (msb4(v.y) << 4) | (msb4(v.z) << 8) | (msb4(v.w) << 12);
+  s16 = msb4(le2(v.x)) | (msb4(le2(v.y)) << 4) | (msb4(le2(v.z)) << 8) | (msb4(le2(v.w)) << 12);
+}
+
 // ---- wave helpers -------------------------------------------------------------------
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 

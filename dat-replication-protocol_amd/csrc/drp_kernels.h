@@ -40,6 +40,15 @@ struct DecodeParams {
   uint32_t *counter;
   uint32_t *overflow;  // bit 0 capacity, bit 1 bounded wait expired, bit 2 inconsistent walk
   uint32_t strict;     // look-back uses exact inclusive exits only (test hook)
+  // speculate-and-verify kernel (drp_decode_spec.hip): per-tile words, value | READY or value + 1
+  uint64_t *claim;     // predicted exit of tile t (or identity)
+  uint64_t *incl_e;    // entry of tile t + 1
+  uint64_t *agg_n;     // exact frames of tile t + 1
+  uint64_t *incl_n;    // frames of tiles <= t + 1
+  const uint32_t *tile_stream;  // tile -> stream (null: one stream)
+  uint8_t *ent;                 // [tile][thread]: entry offset in the thread's 64 B, 0xFF none
+  uint64_t *tile_nch;           // change frames of tile t (per-stream counts come from a scan:
+  uint64_t *tile_nch_base;      //  same-address atomics per tile serialise across the XCDs)
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
   unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
 };
@@ -62,6 +71,17 @@ hipError_t drp_launch_tile_prefix(uint32_t B, const uint64_t *stream_off, uint64
                                   uint64_t *tile_prefix, hipStream_t st);
 hipError_t drp_launch_decode(uint32_t B, const drp::DecodeParams *P, uint32_t grid, hipStream_t st);
 uint32_t drp_decode_waves_per_group(void);  // tiles (waves) per workgroup; grid counts groups
+uint32_t drp_spec_tile_bytes(void);
+uint32_t drp_spec_retry_mask(void);
+hipError_t drp_launch_decode_spec(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
+                                  uint32_t *tile_stream, uint64_t *scan_tmp, hipStream_t st);
+// exclusive scan of a per-tile u64 array over all tiles; flags capacity overflow of the total
+hipError_t drp_launch_tile_scan(const uint64_t *in, const uint64_t *tile_prefix, uint64_t nstreams, uint64_t nt_max,
+                                uint64_t *tmp, uint64_t *out, uint64_t cap, uint32_t *overflow, hipStream_t st);
+// per-stream change / blob counts from the per-tile counts and their scans
+hipError_t drp_launch_stream_counts(const uint64_t *tile_prefix, uint64_t nstreams, const uint64_t *count,
+                                    const uint64_t *base, const uint64_t *nch, const uint64_t *nch_base,
+                                    uint64_t *scount, hipStream_t st);
 hipError_t drp_launch_finalize(const uint8_t *bytes, const uint64_t *stream_off, uint64_t nstreams,
                                const uint64_t *tile_prefix, const uint64_t *tile_exit,
                                const uint64_t *tile_base, const uint64_t *tile_count,

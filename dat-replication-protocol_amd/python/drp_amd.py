@@ -21,7 +21,7 @@ TAIL_NONE, TAIL_HEADER, TAIL_CHANGE, TAIL_BLOB = 0, 1, 2, 3
 
 EXPORTS = [
     "drp_abi_version", "drp_open", "drp_close", "drp_stream", "drp_synchronize",
-    "drp_last_timing", "drp_set_tile", "drp_set_strict", "drp_decode_scratch_bytes",
+    "drp_last_timing", "drp_set_tile", "drp_set_strict", "drp_set_exact", "drp_decode_scratch_bytes",
     "drp_decode_device", "drp_decode_batch", "drp_encode_size", "drp_encode_device",
     "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results",
 ]
@@ -83,6 +83,7 @@ def lib():
         L.drp_last_timing.argtypes = [P, C.POINTER(Timing)]
         L.drp_set_tile.argtypes = [P, U32]
         L.drp_set_strict.argtypes = [P, C.c_int]
+        L.drp_set_exact.argtypes = [P, C.c_int]
         L.drp_decode_scratch_bytes.argtypes = [P, U64, U64]
         L.drp_decode_scratch_bytes.restype = U64
         L.drp_decode_device.argtypes = [P, P, U64, P, P, U64, C.POINTER(Frames),
@@ -97,7 +98,7 @@ def lib():
         L.drp_index_scan.argtypes = [P, P, U64, P]
         L.drp_stream_stats_from_results.argtypes = [P, P, P, U64, P]
         for f in ["drp_open", "drp_synchronize", "drp_last_timing", "drp_set_tile",
-                  "drp_set_strict", "drp_decode_device", "drp_decode_batch", "drp_encode_size",
+                  "drp_set_strict", "drp_set_exact", "drp_decode_device", "drp_decode_batch", "drp_encode_size",
                   "drp_encode_device", "drp_encode_batch", "drp_index_scan",
                   "drp_stream_stats_from_results"]:
             getattr(L, f).restype = C.c_int
@@ -169,6 +170,10 @@ class Ctx:
 
     def set_strict(self, on):
         _chk("drp_set_strict", self.L.drp_set_strict(self.h, 1 if on else 0))
+
+    def set_exact(self, on):
+        """Force the exact decode kernel (else: speculate-and-verify with exact fallback)."""
+        _chk("drp_set_exact", self.L.drp_set_exact(self.h, 1 if on else 0))
 
     def set_tile(self, tile):
         _chk("drp_set_tile", self.L.drp_set_tile(self.h, tile))

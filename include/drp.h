@@ -153,6 +153,10 @@ int drp_synchronize(drp_ctx *ctx);
 int drp_last_timing(drp_ctx *ctx, drp_timing *out);
 /* Tunables (0 = default 8192). tile_bytes is 4096 or 8192 (64 lanes x 64 or 128 bytes). */
 int drp_set_tile(drp_ctx *ctx, uint32_t tile_bytes);
+/* 1: always run the exact decode kernel (per-tile transfer functions); 0 (default): run the
+ * speculate-and-verify kernel and fall back to the exact one when a prediction fails.
+ * Results are identical either way; drp_timing.strict_reruns reports a fallback. */
+int drp_set_exact(drp_ctx *ctx, int exact);
 /* Look-back composes exact inclusive exits only, never the per-tile maps agg_t. Test hook. */
 int drp_set_strict(drp_ctx *ctx, int strict);
 /* Device scratch bytes needed to decode `n` bytes split into `nstreams` streams. */
