@@ -225,13 +225,14 @@ def main():
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
-    dec_ms = []
+    dec_ms, fallbacks = [], 0
     t0 = time.perf_counter()
     ev0.record(ext)
     for _ in range(args.steps):
         step()
         t = ctx.timing()
         dec_ms.append(t.decode_ms)
+        fallbacks += t.strict_reruns
     ev1.record(ext)
     torch.cuda.synchronize(dev)
     if dist:
@@ -255,6 +256,9 @@ def main():
     b_dec = nframes * FRAME + 13 * nframes + 49 * nframes  # W + 13F + 49C, this GPU
     achieved = b_dec / dec_avg_s / 1e9
     tile = args.tile or 8192
+    exact = os.environ.get("DRP_DECODE") == "exact"
+    kname = (f"decode_tiles<{tile // 64}>" if exact else
+             "speculative decode: spec_claims + verify_counts + tile scans + emit_tiles")
     if args.workload == "c2":
         workload = {"workload": "C2: 100M Change frames x 86 B (64 B values), one 8.6 GB stream per GPU",
                     "frames_per_gpu": nframes, "wire_bytes_per_gpu": nframes * FRAME,
@@ -283,8 +287,9 @@ def main():
             "config": workload,
             "wire_GBps": wire_total / elapsed / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profile(tile, nframes),
-                         "kernel": f"decode_tiles<{tile // 64}>", "kernel_ms": dec_avg_s * 1e3,
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profile(kname, nframes),
+                         "kernel": kname, "kernel_ms": dec_avg_s * 1e3,
+                         "exact_fallbacks": fallbacks,
                          "bytes_per_launch": b_dec,
                          "bytes_model": "W + 13*frames + 49*changes (86+13+49 = 148 B/frame)"},
             "step_ms_hip_events": ev_ms / args.steps,
@@ -298,17 +303,17 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def traffic_from_profile(tile, nframes):
-    """HBM bytes per decode launch from the committed rocprofv3 PMC summary of this kernel
-    build (FETCH_SIZE x2 + WRITE_SIZE per frame, guide §HBM, measured on a C2 launch by
-    scripts/gpu_pmc.sh), times this launch's frames; None if absent or for another tile."""
+def traffic_from_profile(kname, nframes):
+    """HBM bytes per decode from the committed rocprofv3 PMC summary of this decode path
+    (FETCH_SIZE x2 + WRITE_SIZE per frame summed over its kernels, guide §HBM, measured on a
+    C2 launch by scripts/gpu_pmc.sh), times this launch's frames; None if absent or stale."""
     p = os.path.join(ROOT, "profiles", "pmc_decode.json")
     try:
         with open(p) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if d.get("tile_bytes") != tile:
+    if d.get("kernel") != kname:
         return None
     return d["hbm_bytes_per_frame"] * nframes if d.get("hbm_bytes_per_frame") else None
 

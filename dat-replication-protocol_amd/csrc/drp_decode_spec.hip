@@ -44,6 +44,9 @@ constexpr uint32_t IMG = TILE + HALO;         // LDS image bytes (+32 slack)
 #ifndef DRP_VALIDATE_ALL
 #define DRP_VALIDATE_ALL 0  // 1: validate a candidate's own change even behind a 1-byte varint
 #endif
+#ifndef DRP_K1_WAVES
+#define DRP_K1_WAVES 1  // min waves per SIMD for the claims kernel
+#endif
 #ifndef DRP_KSTRONG
 #define DRP_KSTRONG 4
 #endif
@@ -383,10 +386,17 @@ __device__ __forceinline__ uint64_t stage_live(const DecodeParams &P, const Tile
 }
 
 // ==== kernel 1: every tile's claim (entry-independent, no waiting) ===========================
-__global__ __launch_bounds__(NT) void spec_claims(DecodeParams P) {
+constexpr uint32_t LLCAP = 1024;  // live positions per tile checked through the LDS list
+constexpr uint16_t NX_NEAR = 0xFFFD, NX_FAR = 0xFFFE, NX_DEAD = 0xFFFF;
+
+__global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint64_t xr[NT / WAVE];
   __shared__ uint32_t xf[NT / WAVE];
+  __shared__ uint64_t lmw[NT];
+  __shared__ uint16_t loff[NT];
+  __shared__ uint16_t lpos[LLCAP], lnx[LLCAP];
+  __shared__ uint8_t lal[LLCAP];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wid = tid >> 6;
   const uint64_t t = blockIdx.x;
@@ -405,7 +415,82 @@ __global__ __launch_bounds__(NT) void spec_claims(DecodeParams P) {
   uint32_t n = 0;
   bool far = false;
   uint64_t defer = 0;  // candidates whose check leaves the LDS image (decided in HBM if needed)
-  {
+  // Survival of every live position of the tile, load-balanced: the positions go to an LDS
+  // list, each is parsed once (its successor's list index, or "out"), then KSTRONG - 1 rounds
+  // of look-ups propagate death back along the chains. lal: 0 dead, 1 strong, 2 undecided (the
+  // chain leaves the LDS image: checked in HBM only if a restart needs it, see below).
+  const uint32_t cnt = (uint32_t)__builtin_popcountll(live);
+  const uint32_t cpre = wave_incl_scan32(cnt);
+  if (lane == 63) xf[wid] = cpre;
+  lmw[tid] = live;
+  __syncthreads();
+  uint32_t off = cpre - cnt, total = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < NT / WAVE; w++) {
+    if (w < wid) off += xf[w];
+    total += xf[w];
+  }
+  loff[tid] = (uint16_t)off;
+  __syncthreads();  // (xf is reused below)
+  if (total <= LLCAP) {
+    {
+      uint64_t bits = live;
+      uint32_t i = off;
+      while (bits) {
+        lpos[i++] = (uint16_t)(tid * SEGB + (uint32_t)__builtin_ctzll(bits));
+        bits &= bits - 1;
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < total; i += NT) {
+      const uint64_t p = G.A + lpos[i];
+      const Hdr h = m.at(p);
+      uint16_t code = NX_DEAD;
+      uint8_t a = 0;
+      if (h.kind == H_VALID && plausible(m, p, h, false)) {
+        if (h.succ >= G.se) {
+          code = NX_NEAR;  // the stream end: survived
+          a = 1;
+        } else if (h.succ >= G.A + TILE) {
+          code = NX_FAR;   // past the tile: undecided (a restart that needs it checks in HBM)
+          a = 2;
+        } else {
+          const uint32_t q = (uint32_t)(h.succ - G.A), th = q / SEGB, b = q % SEGB;
+          const uint64_t lw = lmw[th];
+          if ((lw >> b) & 1ull) {
+            code = (uint16_t)(loff[th] + __builtin_popcountll(lw & ((1ull << b) - 1)));
+            a = 1;
+          }
+        }
+      }
+      lnx[i] = code;
+      lal[i] = a;
+    }
+    __syncthreads();
+    for (int r = 1; r < KSTRONG; r++) {
+      for (uint32_t i = tid; i < total; i += NT) {
+        const uint16_t v = lnx[i];
+        if (lal[i] == 1 && v < NX_NEAR) {
+          const uint8_t b = lal[v];
+          if (b != 1) lal[i] = b;  // dead or undecided downstream
+        }
+      }
+      __syncthreads();
+    }
+    // this thread's first strong position; undecided ones are deferred
+    for (uint32_t i = off; i < off + cnt; i++) {
+      const uint8_t a = lal[i];
+      if (a == 1) {
+        g = G.A + lpos[i];
+        break;
+      }
+      if (a == 2) defer |= 1ull << (lpos[i] - tid * SEGB);
+    }
+    if (g != NONE) {
+      far = m.at(g).succ >= G.A + TILE;
+      R = walk<true>(m, g, s1, n);
+    }
+  } else {  // very dense tile: per-thread checks
     uint64_t bits = live;
     while (bits) {
       const uint32_t o = (uint32_t)__builtin_ctzll(bits);

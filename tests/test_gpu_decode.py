@@ -155,3 +155,27 @@ def test_encode_matches_oracle(ctx):
     np.testing.assert_array_equal(d["change"], c["change"])
     np.testing.assert_array_equal(d["from"], c["from"])
     np.testing.assert_array_equal(d["flags"], c["flags"])
+
+
+@pytest.mark.parametrize("shape", ["c2", "c3", "c5", "random"])
+def test_speculative_matches_exact(ctx, shape):
+    """The default decode (speculate-and-verify kernels) and the exact kernel give identical
+    columns; on clean C2-shaped streams the prediction must hold everywhere (no exact re-run)."""
+    from _gpu import assert_same
+    rng = random.Random(77)
+    wire = {"c2": lambda: S.c2_stream(300_000, seed=8).tobytes(),
+            "c3": lambda: S.c3_stream(rng, 2, frames_per_unit=1000),
+            "c5": lambda: S.c5_stream(rng, 2000),
+            "random": lambda: S.random_stream(rng, 5000, blob_p=0.05, blob_max=30000)}[shape]()
+    spec = ctx.decode_batch(wire)
+    reruns = ctx.timing().strict_reruns
+    ctx.set_exact(True)
+    try:
+        exact = ctx.decode_batch(wire)
+        assert ctx.timing().strict_reruns == 0
+    finally:
+        ctx.set_exact(False)
+    assert_same(spec, exact, shape)
+    assert_same(spec, O.decode_batch(wire, chunk=65536), shape)
+    if shape == "c2":
+        assert reruns == 0, "prediction failed on a clean C2 stream"
