@@ -1,7 +1,8 @@
 """Summarises the rocprofv3 --pmc passes of scripts/gpu_pmc.sh (gpurun_out/pmc/<pass>/...csv)
 into profiles/pmc_decode.json: per-launch averages of the decode kernel's counters and the
 HBM bytes per frame that bench.py reports as roofline.traffic (FETCH_SIZE doubled on gfx950,
-MI355X_MICROARCH.md §HBM, plus WRITE_SIZE). Usage: python scripts/pmc_summary.py frames tile"""
+MI355X_MICROARCH.md §HBM, plus WRITE_SIZE). Usage: python scripts/pmc_summary.py frames tile [spec|exact]
+(spec: the counters of every kernel of the speculative decode, per-kernel averages summed)."""
 import collections
 import csv
 import glob
@@ -12,8 +13,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 frames, tile = int(sys.argv[1]), int(sys.argv[2])
-kern = f"decode_tiles<{tile // 64}"
-tot = collections.defaultdict(float)
+mode = sys.argv[3] if len(sys.argv) > 3 else "spec"
+kern = "drp::spec::" if mode == "spec" else f"decode_tiles<{tile // 64}"
+tot = collections.defaultdict(float)   # (kernel, counter) -> sum
 disp = collections.defaultdict(set)
 os.makedirs(os.path.join(ROOT, "profiles", "pmc_r1"), exist_ok=True)
 for name in ["sq1", "sq2", "fetch", "write"]:
@@ -23,13 +25,17 @@ for name in ["sq1", "sq2", "fetch", "write"]:
     shutil.copy(fs[0], os.path.join(ROOT, "profiles", "pmc_r1", name + ".csv"))
     for r in csv.DictReader(open(fs[0])):
         if kern in r["Kernel_Name"]:
-            tot[r["Counter_Name"]] += float(r["Counter_Value"])
-            disp[r["Counter_Name"]].add(r["Dispatch_Id"])
-avg = {k: v / len(disp[k]) for k, v in tot.items()}
+            key = (r["Kernel_Name"].split("(")[0], r["Counter_Name"])
+            tot[key] += float(r["Counter_Value"])
+            disp[key].add(r["Dispatch_Id"])
+avg = collections.defaultdict(float)  # per decode: per-kernel averages summed over the kernels
+for key, v in tot.items():
+    avg[key[1]] += v / len(disp[key])
 fetch = avg.get("FETCH_SIZE", 0.0) * 1024 * 2
 write = avg.get("WRITE_SIZE", 0.0) * 1024
 out = {
-    "kernel": f"decode_tiles<{tile // 64}, false>",
+    "kernel": (f"decode_tiles<{tile // 64}>" if mode == "exact" else
+               "speculative decode: spec_claims + verify_counts + tile scans + emit_tiles"),
     "tile_bytes": tile,
     "workload": f"C2, {frames:,} frames (bench.py --frames {frames}), per dispatch",
     "frames": frames,
