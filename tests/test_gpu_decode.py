@@ -34,18 +34,22 @@ def test_golden_streams(ctx):
         assert_same(ctx.decode_batch(wire), O.decode_batch(wire), v["source"])
 
 
-@pytest.mark.parametrize("tile", [4096, 8192])
+@pytest.mark.parametrize("kernel", ["speculative", "exact4096", "exact8192"])
 @pytest.mark.parametrize("seed", range(4))
-def test_random_streams(ctx, tile, seed):
+def test_random_streams(ctx, kernel, seed):
+    """Both decode kernels (the tile size only applies to the exact one)."""
     from _gpu import assert_same
-    ctx.set_tile(tile)
+    if kernel != "speculative":
+        ctx.set_exact(True)
+        ctx.set_tile(int(kernel[5:]))
     try:
         rng = random.Random(seed)
         wire = S.random_stream(rng, 3000)
         wire = wire[:rng.randint(len(wire) // 2, len(wire))]
-        assert_same(ctx.decode_batch(wire), O.decode_batch(wire), f"seed{seed}/tile{tile}")
+        assert_same(ctx.decode_batch(wire), O.decode_batch(wire), f"seed{seed}/{kernel}")
     finally:
         ctx.set_tile(0)
+        ctx.set_exact(False)
 
 
 def test_strict_equals_lookback(ctx):
