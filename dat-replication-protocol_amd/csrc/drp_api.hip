@@ -194,7 +194,7 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.scount = o; o += al(2 * ns * 8);
   L.ctrl = o; o += 256;
   L.tstream = o; o += al(L.ntiles_max * 4);    // tile -> stream (speculative kernel)
-  L.ent = o; o += al(L.ntiles_max * 128);      // per-thread entries (speculative kernel)
+  L.ent = o; o += al(L.ntiles_max * 128 * 3);  // per-thread entries + counts (speculative kernel)
   L.scan_tmp = o; o += al((L.ntiles_max / 4096 + 2) * 8);  // tile scans: block sums
   L.total = o;
   return L;
@@ -405,6 +405,8 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.counter = ctrl;
   P.overflow = ctrl + 1;
   P.ent = c->scratch.at<uint8_t>(L.ent);
+  P.ent_n = P.ent + NT * 128;
+  P.ent_c = P.ent_n + NT * 128;
   P.tile_nch = tiles + 3 * NT;
   P.tile_nch_base = tiles + 4 * NT;
   unsigned long long *dstats = nullptr;

@@ -528,9 +528,10 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
     }
   }
   uint64_t E = g;
+  bool rs = false;  // this thread restarts the chain (no chain enters it, or the entering one died)
   PHASE(1);
   // ---- link the threads' chains ------------------------------------------------------------
-  link<false>(m, s1, g, NONE, E, R, n, xr, xf, P.overflow);
+  link<false>(m, s1, g, NONE, E, R, n, xr, xf, P.overflow, &rs);
   // A thread no chain reaches and without an LDS-decided candidate, with none later in the
   // tile either, decides its deferred candidates in HBM (big frames: the chain from a real
   // frame start leaves the image within a step or two), then the chains are linked again.
@@ -561,7 +562,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
         }
       }
     }
-    link<false>(m, s1, g, NONE, E, R, n, xr, xf, P.overflow);
+    link<false>(m, s1, g, NONE, E, R, n, xr, xf, P.overflow, &rs);
   }
   PHASE(2);
   // The chain's last frame may jump over threads that hold strong candidates: a shadow that
@@ -575,21 +576,38 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
     if (js && after) {
       const uint64_t Ea = E, Ra = R;
       const uint32_t na = n;
+      const bool rsa = rs;
       const bool mine = tid + 1 > js;
       E = NONE;
       R = NONE;
       n = 0;
-      link<false>(m, s1, mine ? g : NONE, NONE, E, R, n, xr, xf, P.overflow);
+      link<false>(m, s1, mine ? g : NONE, NONE, E, R, n, xr, xf, P.overflow, &rs);
       const uint32_t nb = block_sum_u32(mine ? n : 0u, xf);
       if (nb < 2 || !mine) {  // keep the first chain where the dense one does not apply
         E = Ea;
         R = Ra;
         n = na;
+        rs = rsa;
       }
     }
   }
   PHASE(3);
-  P.ent[t * NT + tid] = is_pos(E) && E < s1 ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // seeds for kernel 2
+  // per-thread record for kernel 2: entry offset (| 0x40 when the thread restarts the chain,
+  // 0xFF none), frames and change frames delivered from it
+  {
+    const bool carrier = is_pos(E) && E < s1;
+    uint32_t nc = 0;
+    for (uint64_t p = carrier ? E : s1; p < s1 && p < G.se;) {
+      const Hdr h = m.at(p);
+      if (h.kind != H_VALID) break;
+      nc += h.id == 1;
+      p = h.succ;
+    }
+    const uint64_t ix = t * NT + tid;
+    P.ent[ix] = carrier ? (uint8_t)((E - lb) | (rs ? 0x40u : 0u)) : (uint8_t)0xFF;
+    P.ent_n[ix] = (uint8_t)n;
+    P.ent_c[ix] = (uint8_t)nc;
+  }
   if (tid == NT - 1) P.claim[t] = (R == NONE || ((R & MARK_TERM) && (R & M_ERR))) ? C_ID : R;
 }
 
@@ -607,8 +625,6 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
   if (t >= P.tile_prefix[P.nstreams]) return;  // (whole workgroup)
   const TileGeo G = tile_geo(P, t);
-  const uint64_t live = stage_live(P, G, buf);
-  const Img m{buf, P.bytes, G.A, G.se};
   const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
   PHASE(8);
   if (wid == 0) {
@@ -640,40 +656,74 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   const uint64_t claim = P.claim[t];
   if (tid == NT - 1) st_agent(&P.incl_e[t], (claim == C_ID ? et : claim) | RDY);
   PHASE(9);
-  // the exact chain from e_t, seeded with the predicted chain's per-thread entries
-  const uint8_t sb = P.ent[t * NT + tid];
-  uint64_t E = sb < SEGB ? lb + sb : (live ? lb + (uint32_t)__builtin_ctzll(live) : NONE);
-  uint32_t n = 0;
-  uint64_t R = walk(m, E, s1, n);
-  link<true>(m, s1, NONE, et, E, R, n, xr, xf, P.overflow);
-  P.ent[t * NT + tid] = is_pos(E) && E < s1 ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // exact, for kernel 3
-  PHASE(10);
-  const uint32_t count_t = block_sum_u32(n, xf);
-  uint32_t nc = 0;  // change frames among them
-  if (n) {
-    uint64_t p = E;
-    while (p < s1 && p < G.se) {
-      const Hdr h = m.at(p);
-      nc += h.id == 1 && (h.kind == H_VALID);
-      if (h.kind != H_VALID) break;
-      p = h.succ;
-    }
+  // Fast check from kernel 1's per-thread records (no tile bytes): when the thread holding e_t
+  // has e_t as its predicted entry and no later thread restarted the predicted chain, the
+  // walks from there on are the exact walks (same entries, and no prediction-only deaths), so
+  // the predicted entries, counts and exit are exact.
+  const uint64_t ix = t * NT + tid;
+  const uint8_t eb = P.ent[ix];
+  const bool inside = is_pos(et) && et < G.A + TILE;
+  const uint32_t k = inside ? (uint32_t)((et - G.A) / SEGB) : NT;
+  uint32_t bad = 0;
+  if (inside) {
+    if (tid == k && ((eb & 0x80) || (eb & 63) != (uint32_t)((et - G.A) % SEGB))) bad = 1;
+    if (tid > k && eb != 0xFF && (eb & 0x40)) bad = 1;
+    if (claim == C_ID) bad = 1;
   }
-  const uint32_t nch_t = block_sum_u32(nc, xf);
-  // the last thread's R is the tile's exact exit; it must be what the claim predicted (an
-  // error on the exact chain never is: predictions restart after errors)
-  if (tid == NT - 1) {
-    const uint64_t exit_t = (R & MARK_TERM) ? (R & ~M_ERR) : R;
+  const bool fast = !block_max_u32(bad, xf);
+  uint32_t count_t, nch_t;
+  uint64_t exit_t;
+  bool miss;
+  if (fast) {
+    const bool mine = tid >= k && eb != 0xFF;
+    count_t = block_sum_u32(mine ? P.ent_n[ix] : 0u, xf);
+    nch_t = block_sum_u32(mine ? P.ent_c[ix] : 0u, xf);
+    if (tid < k) P.ent[ix] = 0xFF;
+    exit_t = inside ? claim : et;  // pass-through tiles keep the entry
+    miss = !inside && claim != C_ID;
+  } else {
+    const uint64_t live = stage_live(P, G, buf);
+    const Img m{buf, P.bytes, G.A, G.se};
+    // the exact chain from e_t, seeded with the predicted chain's per-thread entries
+    uint64_t E = !(eb & 0x80) ? lb + (eb & 63) : (live ? lb + (uint32_t)__builtin_ctzll(live) : NONE);
+    uint32_t n = 0;
+    uint64_t R = walk(m, E, s1, n);
+    link<true>(m, s1, NONE, et, E, R, n, xr, xf, P.overflow);
+    P.ent[ix] = is_pos(E) && E < s1 ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // exact, for kernel 3
+    count_t = block_sum_u32(n, xf);
+    uint32_t nc = 0;  // change frames among them
+    if (n) {
+      uint64_t p = E;
+      while (p < s1 && p < G.se) {
+        const Hdr h = m.at(p);
+        nc += h.id == 1 && (h.kind == H_VALID);
+        if (h.kind != H_VALID) break;
+        p = h.succ;
+      }
+    }
+    nch_t = block_sum_u32(nc, xf);
+    // the last thread's R is the tile's exact exit; it must be what the claim predicted (an
+    // error on the exact chain never is: predictions restart after errors)
+    xr[0] = 0;
+    __syncthreads();
+    if (tid == NT - 1) xr[0] = R;
+    __syncthreads();
+    const uint64_t Rl = xr[0];
+    exit_t = (Rl & MARK_TERM) ? (Rl & ~M_ERR) : Rl;
     const uint64_t want = claim == C_ID ? et : claim;
-    if (exit_t != want || ((R & MARK_TERM) && (R & M_ERR))) {
+    miss = exit_t != want || ((Rl & MARK_TERM) && (Rl & M_ERR));
+  }
+  PHASE(10);
+  if (tid == NT - 1) {
+    if (miss) {
       atomicOr(P.overflow, F_MISS);
       if (P.stats) {  // debug capture (DRP_STATS=1): the first misses
-        const unsigned long long k = atomicAdd(&P.stats[0], 1ull);
-        if (k < 5) {
-          P.stats[1 + 6 * k] = t;
-          P.stats[2 + 6 * k] = et;
-          P.stats[3 + 6 * k] = claim;
-          P.stats[4 + 6 * k] = R;
+        const unsigned long long q = atomicAdd(&P.stats[0], 1ull);
+        if (q < 5) {
+          P.stats[1 + 6 * q] = t;
+          P.stats[2 + 6 * q] = et;
+          P.stats[3 + 6 * q] = claim;
+          P.stats[4 + 6 * q] = exit_t;
         }
       }
     }
@@ -809,7 +859,7 @@ __global__ __launch_bounds__(NT) void emit_tiles(DecodeParams P) {
   const uint64_t lb = A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
   const uint64_t base = P.tile_base[t];
   const uint8_t eb = P.ent[t * NT + tid];  // exact entry of this thread's bytes (kernel 2)
-  const uint64_t E = eb < SEGB ? lb + eb : NONE;
+  const uint64_t E = !(eb & 0x80) ? lb + (eb & 63) : NONE;
   PHASE(11);
   uint32_t n = 0;
   (void)walk(m, E, s1, n);

@@ -47,6 +47,7 @@ struct DecodeParams {
   uint64_t *incl_n;    // frames of tiles <= t + 1
   const uint32_t *tile_stream;  // tile -> stream (null: one stream)
   uint8_t *ent;                 // [tile][thread]: entry offset in the thread's 64 B, 0xFF none
+  uint8_t *ent_n, *ent_c;       // [tile][thread]: frames / change frames from that entry
   uint64_t *tile_nch;           // change frames of tile t (per-stream counts come from a scan:
   uint64_t *tile_nch_base;      //  same-address atomics per tile serialise across the XCDs)
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
