@@ -319,6 +319,7 @@ struct TileGeo {
 __device__ __forceinline__ TileGeo tile_geo(const DecodeParams &P, uint64_t t) {
   TileGeo G;
   G.s = P.tile_stream ? P.tile_stream[t] : 0;
+  if (G.s >= P.nstreams) G.s = P.nstreams - 1;  // (t past the last tile: read before the exit check)
   G.tf = P.tile_prefix[G.s];
   G.so = P.stream_off[G.s];
   G.se = P.stream_off[G.s + 1];
@@ -327,13 +328,33 @@ __device__ __forceinline__ TileGeo tile_geo(const DecodeParams &P, uint64_t t) {
   return G;
 }
 
-__device__ __forceinline__ void stage(const DecodeParams &P, const TileGeo &G, uint8_t *buf) {
+// The tile's bytes (64 per thread) and halo, loaded with no per-load branch when the whole
+// image lies inside the batch buffer (bytes past the stream end are then the next stream's or
+// padding: every parser bounds-checks against the stream end, and the live mask drops them);
+// near the buffer end, guarded loads zero-fill. One uniform branch, so all loads are in flight
+// together instead of one bounds-checked load at a time.
+__device__ __forceinline__ void load_image(const DecodeParams &P, const TileGeo &G, uint4 (&v)[SEGB / 16], uint4 &h) {
   const uint32_t tid = threadIdx.x;
   const uint64_t lb = G.A + (uint64_t)tid * SEGB;
+  if (G.A + IMG <= P.nbytes) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(P.bytes + lb);
 #pragma unroll
-  for (int k = 0; k < (int)(SEGB / 16); k++)
-    *reinterpret_cast<uint4 *>(buf + tid * SEGB + 16 * k) = ld16(P.bytes, lb + 16 * k, G.se);
-  if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = ld16(P.bytes, G.A + TILE + tid * 16, G.se);
+    for (int k = 0; k < (int)(SEGB / 16); k++) v[k] = q[k];
+    h = tid < HALO / 16 ? *reinterpret_cast<const uint4 *>(P.bytes + G.A + TILE + tid * 16) : make_uint4(0, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int k = 0; k < (int)(SEGB / 16); k++) v[k] = ld16(P.bytes, lb + 16 * k, G.se);
+    h = tid < HALO / 16 ? ld16(P.bytes, G.A + TILE + tid * 16, G.se) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void stage(const DecodeParams &P, const TileGeo &G, uint8_t *buf) {
+  const uint32_t tid = threadIdx.x;
+  uint4 v[SEGB / 16], h;
+  load_image(P, G, v, h);
+#pragma unroll
+  for (int k = 0; k < (int)(SEGB / 16); k++) *reinterpret_cast<uint4 *>(buf + tid * SEGB + 16 * k) = v[k];
+  if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = h;
   if (tid < 2) *reinterpret_cast<uint4 *>(buf + IMG + tid * 16) = make_uint4(0, 0, 0, 0);
   __syncthreads();
 }
@@ -344,12 +365,11 @@ __device__ __forceinline__ void stage(const DecodeParams &P, const TileGeo &G, u
 __device__ __forceinline__ uint64_t stage_live(const DecodeParams &P, const TileGeo &G, uint8_t *buf) {
   const uint32_t tid = threadIdx.x;
   const uint64_t lb = G.A + (uint64_t)tid * SEGB;
-  uint4 v[SEGB / 16];
-#pragma unroll
-  for (int k = 0; k < (int)(SEGB / 16); k++) v[k] = ld16(P.bytes, lb + 16 * k, G.se);
+  uint4 v[SEGB / 16], hv;
+  load_image(P, G, v, hv);
 #pragma unroll
   for (int k = 0; k < (int)(SEGB / 16); k++) *reinterpret_cast<uint4 *>(buf + tid * SEGB + 16 * k) = v[k];
-  if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = ld16(P.bytes, G.A + TILE + tid * 16, G.se);
+  if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = hv;
   if (tid < 2) *reinterpret_cast<uint4 *>(buf + IMG + tid * 16) = make_uint4(0, 0, 0, 0);
   __syncthreads();
   uint32_t m16[5], s16[5];
@@ -401,8 +421,9 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   const uint32_t lane = tid & 63u, wid = tid >> 6;
   const uint64_t t = blockIdx.x;
   uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
-  if (t >= P.tile_prefix[P.nstreams]) return;  // (whole workgroup)
-  const TileGeo G = tile_geo(P, t);
+  const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
+  if (t >= ntiles) return;  // (whole workgroup)
   const uint64_t live = stage_live(P, G, buf);
   const Img m{buf, P.bytes, G.A, G.se};
   const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
@@ -623,8 +644,9 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   const uint32_t lane = tid & 63u, wid = tid >> 6;
   const uint64_t t = blockIdx.x;
   uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
-  if (t >= P.tile_prefix[P.nstreams]) return;  // (whole workgroup)
-  const TileGeo G = tile_geo(P, t);
+  const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
+  if (t >= ntiles) return;  // (whole workgroup)
   const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
   PHASE(8);
   if (wid == 0) {
@@ -851,8 +873,9 @@ __global__ __launch_bounds__(NT) void emit_tiles(DecodeParams P) {
   const uint32_t lane = tid & 63u, wid = tid >> 6;
   const uint64_t t = blockIdx.x;
   uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
-  if (t >= P.tile_prefix[P.nstreams]) return;  // (whole workgroup)
-  const TileGeo G = tile_geo(P, t);
+  const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
+  if (t >= ntiles) return;  // (whole workgroup)
   const uint64_t se = G.se, A = G.A;
   stage(P, G, buf);
   const Img m{buf, P.bytes, A, se};
