@@ -144,7 +144,8 @@ __device__ __forceinline__ uint64_t term_of(const Hdr &h, uint64_t p) {
 
 // The chain from entry E through this thread's bytes [.., s1): returns the first chain position
 // >= s1 (or E itself when E >= s1 / is not a position), or MARK_TERM|q when the chain ends at
-// q (tail or error); n = frames delivered on the way (decode.js delivers id 1/2 and partial blobs).
+// q (tail or error); n = frames delivered on the way (decode.js delivers id 1/2 and partial blobs)
+// in the low 16 bits, change frames among them in the high 16 bits (<= 32 each per thread).
 // Prediction-side plausibility of a valid frame at p (never used on the exact path): a change
 // frame behind a multi-byte length varint must hold a well-formed Change when it ends inside
 // the LDS image. Shadow headers whose varint swallows a real header's first bytes declare
@@ -166,7 +167,7 @@ __device__ __forceinline__ uint64_t walk(const Img &m, uint64_t E, uint64_t s1, 
     const Hdr h = m.at(p);
     if (SPEC && h.kind == H_VALID && !plausible(m, p, h, false)) return MARK_TERM | M_ERR | p;
     if (h.kind == H_VALID) {
-      n += h.id != 0;
+      n += (h.id != 0) + ((h.id == 1) << 16);
       p = h.succ;
       continue;
     }
@@ -197,7 +198,7 @@ __device__ __forceinline__ uint32_t strong(const Img &m, uint64_t c, uint64_t s1
     if (h.kind == H_VALID) {
       if (k == 0) far = h.succ >= m.A + TILE;
       if (!plausible(m, p, h, DRP_VALIDATE_ALL && k == 0)) return S_DEAD;
-      if (p < s1) n += h.id != 0;
+      if (p < s1) n += (h.id != 0) + ((h.id == 1) << 16);
       p = h.succ;
       if (R == NONE && p >= s1) R = p;
       continue;
@@ -464,10 +465,11 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
     }
     __syncthreads();
     for (uint32_t i = tid; i < total; i += NT) {
-      const uint64_t p = G.A + lpos[i];
+      const uint64_t p = G.A + (lpos[i] & 0x7FFFu);
       const Hdr h = m.at(p);
       uint16_t code = NX_DEAD;
       uint8_t a = 0;
+      if (h.kind == H_VALID && h.succ >= G.A + TILE) lpos[i] |= 0x8000u;  // first frame leaves the tile
       if (h.kind == H_VALID && plausible(m, p, h, false)) {
         if (h.succ >= G.se) {
           code = NX_NEAR;  // the stream end: survived
@@ -502,15 +504,13 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
     for (uint32_t i = off; i < off + cnt; i++) {
       const uint8_t a = lal[i];
       if (a == 1) {
-        g = G.A + lpos[i];
+        g = G.A + (lpos[i] & 0x7FFFu);
+        far = (lpos[i] & 0x8000u) != 0;
         break;
       }
-      if (a == 2) defer |= 1ull << (lpos[i] - tid * SEGB);
+      if (a == 2) defer |= 1ull << ((lpos[i] & 0x7FFFu) - tid * SEGB);
     }
-    if (g != NONE) {
-      far = m.at(g).succ >= G.A + TILE;
-      R = walk<true>(m, g, s1, n);
-    }
+    if (g != NONE) R = walk<true>(m, g, s1, n);
   } else {  // very dense tile: per-thread checks
     uint64_t bits = live;
     while (bits) {
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
       R = NONE;
       n = 0;
       link<false>(m, s1, mine ? g : NONE, NONE, E, R, n, xr, xf, P.overflow, &rs);
-      const uint32_t nb = block_sum_u32(mine ? n : 0u, xf);
+      const uint32_t nb = block_sum_u32(mine ? (n & 0xFFFFu) : 0u, xf);
       if (nb < 2 || !mine) {  // keep the first chain where the dense one does not apply
         E = Ea;
         R = Ra;
@@ -617,17 +617,10 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   // 0xFF none), frames and change frames delivered from it
   {
     const bool carrier = is_pos(E) && E < s1;
-    uint32_t nc = 0;
-    for (uint64_t p = carrier ? E : s1; p < s1 && p < G.se;) {
-      const Hdr h = m.at(p);
-      if (h.kind != H_VALID) break;
-      nc += h.id == 1;
-      p = h.succ;
-    }
     const uint64_t ix = t * NT + tid;
     P.ent[ix] = carrier ? (uint8_t)((E - lb) | (rs ? 0x40u : 0u)) : (uint8_t)0xFF;
-    P.ent_n[ix] = (uint8_t)n;
-    P.ent_c[ix] = (uint8_t)nc;
+    P.ent_n[ix] = carrier ? (uint8_t)(n & 0xFFFFu) : (uint8_t)0;
+    P.ent_c[ix] = carrier ? (uint8_t)(n >> 16) : (uint8_t)0;
   }
   if (tid == NT - 1) P.claim[t] = (R == NONE || ((R & MARK_TERM) && (R & M_ERR))) ? C_ID : R;
 }
@@ -712,18 +705,8 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     uint64_t R = walk(m, E, s1, n);
     link<true>(m, s1, NONE, et, E, R, n, xr, xf, P.overflow);
     P.ent[ix] = is_pos(E) && E < s1 ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // exact, for kernel 3
-    count_t = block_sum_u32(n, xf);
-    uint32_t nc = 0;  // change frames among them
-    if (n) {
-      uint64_t p = E;
-      while (p < s1 && p < G.se) {
-        const Hdr h = m.at(p);
-        nc += h.id == 1 && (h.kind == H_VALID);
-        if (h.kind != H_VALID) break;
-        p = h.succ;
-      }
-    }
-    nch_t = block_sum_u32(nc, xf);
+    count_t = block_sum_u32(n & 0xFFFFu, xf);
+    nch_t = block_sum_u32(n >> 16, xf);
     // the last thread's R is the tile's exact exit; it must be what the claim predicted (an
     // error on the exact chain never is: predictions restart after errors)
     xr[0] = 0;
@@ -886,6 +869,7 @@ __global__ __launch_bounds__(NT) void emit_tiles(DecodeParams P) {
   PHASE(11);
   uint32_t n = 0;
   (void)walk(m, E, s1, n);
+  n &= 0xFFFFu;  // frames (walk packs change frames above)
   const uint32_t ni = wave_incl_scan32(n);
   if (lane == 63) wsum[wid] = ni;
   __syncthreads();
