@@ -282,6 +282,38 @@ __device__ __forceinline__ uint32_t block_max_u32(uint32_t v, uint32_t *xf) {
   __syncthreads();
   return r;
 }
+// two maxima with one exchange (scratch: 2 * NT / WAVE words)
+__device__ __forceinline__ void block_max2_u32(uint32_t &a, uint32_t &b, uint32_t *xf) {
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (uint32_t k = 1; k < WAVE; k <<= 1) {
+    a = max(a, shfl_xor32(a, k));
+    b = max(b, shfl_xor32(b, k));
+  }
+  if (lane == 0) {
+    xf[wid] = a;
+    xf[NT / WAVE + wid] = b;
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t w = 0; w < NT / WAVE; w++) {
+    a = max(a, xf[w]);
+    b = max(b, xf[NT / WAVE + w]);
+  }
+  __syncthreads();
+}
+// bits strictly above bit j of the 128-bit mask (m0 low, m1 high) exist
+__device__ __forceinline__ bool any_above(uint64_t m0, uint64_t m1, uint32_t j) {
+  if (j >= 64) return j < 127 && (m1 >> (j - 63)) != 0;
+  return m1 != 0 || (j < 63 && (m0 >> (j + 1)) != 0);
+}
+// bits at or above bit j exist
+__device__ __forceinline__ bool any_from(uint64_t m0, uint64_t m1, uint32_t j) {
+  if (j >= 128) return false;
+  if (j >= 64) return (m1 >> (j - 64)) != 0;
+  return m1 != 0 || (m0 >> j) != 0;
+}
+
 __device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t *xf) {
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   v = wave_sum32(v);
@@ -416,6 +448,8 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   __shared__ uint32_t xf[NT / WAVE];
   __shared__ uint64_t lmw[NT];
   __shared__ uint16_t loff[NT];
+  __shared__ uint32_t xf2[2 * NT / WAVE];
+  __shared__ uint64_t xm[2 * NT / WAVE];  // candidate masks: [w] strong, [NWV + w] strong and far
   __shared__ uint16_t lpos[LLCAP], lnx[LLCAP];
   __shared__ uint8_t lal[LLCAP];
   const uint32_t tid = threadIdx.x;
@@ -532,17 +566,24 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   }
   // A chain that starts by jumping past the whole tile is trusted only when nothing later in
   // the tile could start one: a shadow whose long jump happens to land on a real frame start
-  // survives any number of frames, but it jumps over the tile's real (dense) chain.
+  // survives any number of frames, but it jumps over the tile's real (dense) chain. The
+  // tile-wide candidate masks (128 bits) are exchanged once; the survivors' mask S is then
+  // known to every thread without further barriers.
+  static_assert(NT == 2 * WAVE, "candidate masks are two words");
+  uint64_t S0, S1;
   {
-    const uint64_t hm = __ballot(g != NONE);
-    if (lane == 0) xf[wid] = hm != 0;
+    const uint64_t hm = __ballot(g != NONE), fm = __ballot(g != NONE && far);
+    if (lane == 0) {
+      xm[wid] = hm;
+      xm[2 + wid] = fm;
+    }
     __syncthreads();
-    bool later = lane < 63 && (hm >> (lane + 1)) != 0;
-#pragma unroll
-    for (uint32_t w = 0; w < NT / WAVE; w++)
-      if (w > wid && xf[w]) later = true;
-    __syncthreads();
-    if (far && later) {
+    const uint64_t H0 = xm[0], H1 = xm[1], F0 = xm[2], F1 = xm[3];
+    const uint64_t L1 = H1 ? ((1ull << (63 - __builtin_clzll(H1))) - 1) : 0ull;  // below the top bit
+    const uint64_t L0 = H1 ? ~0ull : (H0 ? ((1ull << (63 - __builtin_clzll(H0))) - 1) : 0ull);
+    S0 = H0 & ~(F0 & L0);
+    S1 = H1 & ~(F1 & L1);
+    if (far && any_above(H0, H1, tid)) {
       g = NONE;
       R = NONE;
       n = 0;
@@ -556,18 +597,14 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   // A thread no chain reaches and without an LDS-decided candidate, with none later in the
   // tile either, decides its deferred candidates in HBM (big frames: the chain from a real
   // frame start leaves the image within a step or two), then the chains are linked again.
-  for (uint32_t it = 0; it < 3; it++) {
-    const uint64_t hm = __ballot(g != NONE);
-    if (lane == 0) xf[wid] = hm != 0;
-    __syncthreads();
-    bool later = lane < 63 && (hm >> (lane + 1)) != 0;
-#pragma unroll
-    for (uint32_t w = 0; w < NT / WAVE; w++)
-      if (w > wid && xf[w]) later = true;
-    __syncthreads();
-    const bool need = E == NONE && defer && !later;
-    if (!block_max_u32(need ? 1u : 0u, xf)) break;
-    if (need) {
+  // The first test rides on the reduction that finds the last carrier.
+  uint32_t need = (E == NONE && defer && !any_above(S0, S1, tid)) ? 1u : 0u;
+  uint32_t js = (is_pos(E) && E < s1) ? tid + 1 : 0u;  // last carrier + 1
+  block_max2_u32(need, js, xf2);
+  bool moved = false;
+  for (uint32_t it = 0; need && it < 3; it++) {
+    moved = true;
+    if (E == NONE && defer && !any_above(S0, S1, tid)) {
       while (defer) {
         const uint32_t o = (uint32_t)__builtin_ctzll(defer);
         defer &= defer - 1;
@@ -584,6 +621,9 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
       }
     }
     link<false>(m, s1, g, NONE, E, R, n, xr, xf, P.overflow, &rs);
+    need = (E == NONE && defer && !any_above(S0, S1, tid)) ? 1u : 0u;
+    js = (is_pos(E) && E < s1) ? tid + 1 : 0u;
+    block_max2_u32(need, js, xf2);
   }
   PHASE(2);
   // The chain's last frame may jump over threads that hold strong candidates: a shadow that
@@ -591,9 +631,12 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   // chain those candidates start as well and keep it when it is the denser one (>= 2
   // frames where the first has one); a real long frame jumps over bytes with no candidate.
   {
-    const bool carrier = is_pos(E) && E < s1;
-    const uint32_t js = block_max_u32(carrier ? tid + 1 : 0u, xf);  // last carrier + 1
-    const uint32_t after = block_max_u32(g != NONE && tid + 1 > js ? 1u : 0u, xf);
+    bool after;
+    if (!moved) {
+      after = any_from(S0, S1, js);  // survivors at or after the last carrier + 1
+    } else {  // candidates changed in HBM: count them again
+      after = block_max_u32(g != NONE && tid + 1 > js ? 1u : 0u, xf) != 0;
+    }
     if (js && after) {
       const uint64_t Ea = E, Ra = R;
       const uint32_t na = n;
