@@ -47,6 +47,9 @@ constexpr uint32_t IMG = TILE + HALO;         // LDS image bytes (+32 slack)
 #ifndef DRP_K1_WAVES
 #define DRP_K1_WAVES 1  // min waves per SIMD for the claims kernel
 #endif
+#ifndef DRP_LIST_PLAUSIBLE
+#define DRP_LIST_PLAUSIBLE 0  // 1: the list stage also checks Change payloads (the chain walks always do)
+#endif
 #ifndef DRP_KSTRONG
 #define DRP_KSTRONG 4
 #endif
@@ -504,7 +507,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
       uint16_t code = NX_DEAD;
       uint8_t a = 0;
       if (h.kind == H_VALID && h.succ >= G.A + TILE) lpos[i] |= 0x8000u;  // first frame leaves the tile
-      if (h.kind == H_VALID && plausible(m, p, h, false)) {
+      if (h.kind == H_VALID && (DRP_LIST_PLAUSIBLE == 0 || plausible(m, p, h, false))) {
         if (h.succ >= G.se) {
           code = NX_NEAR;  // the stream end: survived
           a = 1;
