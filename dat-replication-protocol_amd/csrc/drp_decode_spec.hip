@@ -739,7 +739,10 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     const bool mine = tid >= k && eb != 0xFF;
     count_t = block_sum_u32(mine ? P.ent_n[ix] : 0u, xf);
     nch_t = block_sum_u32(mine ? P.ent_c[ix] : 0u, xf);
-    if (tid < k) P.ent[ix] = 0xFF;
+    if (tid < k) {
+      P.ent[ix] = 0xFF;
+      P.ent_n[ix] = 0;
+    }
     exit_t = inside ? claim : et;  // pass-through tiles keep the entry
     miss = !inside && claim != C_ID;
   } else {
@@ -750,7 +753,9 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     uint32_t n = 0;
     uint64_t R = walk(m, E, s1, n);
     link<true>(m, s1, NONE, et, E, R, n, xr, xf, P.overflow);
-    P.ent[ix] = is_pos(E) && E < s1 ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // exact, for kernel 3
+    const bool carrier = is_pos(E) && E < s1;
+    P.ent[ix] = carrier ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // exact, for kernel 3
+    P.ent_n[ix] = carrier ? (uint8_t)(n & 0xFFFFu) : (uint8_t)0;
     count_t = block_sum_u32(n & 0xFFFFu, xf);
     nch_t = block_sum_u32(n >> 16, xf);
     // the last thread's R is the tile's exact exit; it must be what the claim predicted (an
@@ -913,9 +918,7 @@ __global__ __launch_bounds__(NT) void emit_tiles(DecodeParams P) {
   const uint8_t eb = P.ent[t * NT + tid];  // exact entry of this thread's bytes (kernel 2)
   const uint64_t E = !(eb & 0x80) ? lb + (eb & 63) : NONE;
   PHASE(11);
-  uint32_t n = 0;
-  (void)walk(m, E, s1, n);
-  n &= 0xFFFFu;  // frames (walk packs change frames above)
+  const uint32_t n = (eb & 0x80) ? 0u : P.ent_n[t * NT + tid];  // exact frames from E (kernel 2)
   const uint32_t ni = wave_incl_scan32(n);
   if (lane == 63) wsum[wid] = ni;
   __syncthreads();
