@@ -45,10 +45,13 @@ constexpr uint32_t IMG = TILE + HALO;         // LDS image bytes (+32 slack)
 #define DRP_VALIDATE_ALL 0  // 1: validate a candidate's own change even behind a 1-byte varint
 #endif
 #ifndef DRP_K1_WAVES
-#define DRP_K1_WAVES 1  // min waves per SIMD for the claims kernel
+#define DRP_K1_WAVES 5  // min waves per SIMD for the claims kernel (LDS allows 5; 1.55 -> 1.34 ms at 20M frames)
 #endif
 #ifndef DRP_LIST_PLAUSIBLE
 #define DRP_LIST_PLAUSIBLE 0  // 1: the list stage also checks Change payloads (the chain walks always do)
+#endif
+#ifndef DRP_EMIT_WAVES
+#define DRP_EMIT_WAVES 5  // min waves per SIMD for the emit kernel (0.88 -> 0.79 ms at 20M frames)
 #endif
 #ifndef DRP_KSTRONG
 #define DRP_KSTRONG 4
@@ -154,11 +157,22 @@ __device__ __forceinline__ uint64_t term_of(const Hdr &h, uint64_t p) {
 // the LDS image. Shadow headers whose varint swallows a real header's first bytes declare
 // ~10 KB+ "frames" whose payload runs on into the next frames' headers; real long frames
 // (4 KB values) cost one field walk.
+#ifndef DRP_PLAUS_CALL
+#define DRP_PLAUS_CALL 0  // 1: one out-of-line Change check (fewer SGPR spills, but measured 4% slower)
+#endif
+#if DRP_PLAUS_CALL
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+bool change_ok(const uint8_t *lds, uint64_t A, uint64_t se, uint64_t po, uint64_t pl) {
+  const LdsReader rd{lds, A, umin64(A + IMG, se)};
+  const ChangeCols cc = decode_change(rd, po, pl);
+  return !cc.err || cc.err == ERR_UNREACHABLE;
+}
 __device__ __forceinline__ bool plausible(const Img &m, uint64_t p, const Hdr &h, bool any_len) {
   if (h.id != 1 || (!any_len && h.vlen < 2) || h.succ > m.A + IMG) return true;
-  const LdsReader rd{m.lds, m.A, umin64(m.A + IMG, m.se)};
-  const ChangeCols cc = decode_change(rd, p + h.vlen + 1, h.L - 1);
-  return !cc.err || cc.err == ERR_UNREACHABLE;
+  return change_ok(m.lds, m.A, m.se, p + h.vlen + 1, h.L - 1);
 }
 
 template <bool SPEC = false>
@@ -228,8 +242,16 @@ __device__ __forceinline__ uint32_t strong(const Img &m, uint64_t c, uint64_t s1
 // no carrier, or a carrier whose chain died at an error, restarts at the thread's own strong
 // candidate g. Verify mode: a virtual carrier before thread 0 exits at e_first, errors pass on.
 // One block-wide "latest carrier" scan per round; rounds repeat until no entry changes.
+#ifndef DRP_LINK_CALL
+#define DRP_LINK_CALL 0
+#endif
 template <bool VERIFY>
-__device__ __forceinline__ void link(const Img &m, uint64_t s1, uint64_t g, uint64_t e_first, uint64_t &E,
+#if DRP_LINK_CALL
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+void link(const Img &m, uint64_t s1, uint64_t g, uint64_t e_first, uint64_t &E,
                                      uint64_t &R, uint32_t &n, uint64_t *wl, uint32_t *fl, uint32_t *overflow,
                                      bool *restart = nullptr) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
@@ -899,7 +921,7 @@ __device__ __forceinline__ void emit_frame(const DecodeParams &P, const Img &m, 
   if (c.err) badf = f < badf ? f : badf;
 }
 
-__global__ __launch_bounds__(NT) void emit_tiles(DecodeParams P) {
+__global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint16_t lst[LCAP];
   __shared__ uint32_t wsum[NT / WAVE];
