@@ -464,7 +464,10 @@ __device__ __forceinline__ uint64_t stage_live(const DecodeParams &P, const Tile
 }
 
 // ==== kernel 1: every tile's claim (entry-independent, no waiting) ===========================
-constexpr uint32_t LLCAP = 1024;  // live positions per tile checked through the LDS list
+#ifndef DRP_LLCAP
+#define DRP_LLCAP 1024
+#endif
+constexpr uint32_t LLCAP = DRP_LLCAP;  // live positions per tile checked through the LDS list
 constexpr uint16_t NX_NEAR = 0xFFFD, NX_FAR = 0xFFFE, NX_DEAD = 0xFFFF;
 
 __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) {
