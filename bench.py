@@ -160,13 +160,132 @@ def verify_c4(o, res, counts, base, lo, dev):
         assert torch.equal(base[lo:lo + len(counts)] - base[lo], exp), "global index"
 
 
+C5_VALUE = 4096
+
+
+def varint_len(x):
+    """LEB128 length of non-negative int64 values below 2^35 (varint@3 encode)."""
+    return 1 + (x >= 1 << 7).long() + (x >= 1 << 14).long() + (x >= 1 << 21).long() + (x >= 1 << 28).long()
+
+
+def c5_on_device(n, seed, dev):
+    """C5: n Changes with 4096 random value bytes, key length U[1,256] and
+    change/from/to U[0,2^32), as encoder columns over one device heap (key then value per row).
+    Returns the columns, the heap and the expected frame sizes (encode.js:102-137 layout)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    key_len = torch.randint(1, 257, (n,), generator=g, device=dev, dtype=torch.int64)
+    nums = torch.randint(0, 1 << 32, (3, n), generator=g, device=dev, dtype=torch.int64)
+    row = key_len + C5_VALUE
+    key_off = torch.cumsum(row, 0) - row
+    heap = torch.randint(0, 256, (int(row.sum()),), generator=g, device=dev, dtype=torch.uint8)
+    cols = {"key_off": key_off, "key_len": key_len.to(torch.int32),
+            "subset_off": torch.zeros(n, dtype=torch.int64, device=dev),
+            "subset_len": torch.zeros(n, dtype=torch.int32, device=dev),
+            "value_off": key_off + key_len,
+            "value_len": torch.full((n,), C5_VALUE, dtype=torch.int32, device=dev),
+            "change": nums[0].contiguous(), "from": nums[1].contiguous(), "to": nums[2].contiguous(),
+            "flags": torch.full((n,), 2, dtype=torch.uint8, device=dev)}
+    payload = (1 + varint_len(key_len) + key_len) + (3 + varint_len(nums).sum(0)) + \
+        (1 + varint_len(torch.full_like(key_len, C5_VALUE)) + C5_VALUE)
+    frame = varint_len(payload + 1) + 1 + payload
+    return cols, heap, frame
+
+
+def verify_c5(cols, heap, wire, o, res, n, dev, samples=256):
+    """Round-trip properties at full size: every decoded column equals the encoder's input and
+    sampled key/value bytes in the wire equal the heap's (bit-exact)."""
+    r = drp_amd.StreamResult.from_buffer_copy(res.cpu().numpy().tobytes()[:C.sizeof(drp_amd.StreamResult)])
+    assert (r.frames, r.changes, r.err_code, r.tail_kind, r.consumed) == (n, n, 0, 0, wire.numel()), \
+        (r.frames, r.err_code, r.tail_kind, r.consumed)
+    o = {k: v[:n] for k, v in o.items()}
+    for k in ["change", "from", "to"]:
+        assert torch.equal(o[k], cols[k]), k
+    for k in ["key_len", "value_len"]:
+        assert torch.equal(o[k], cols[k]), k
+    assert bool((o["flags"] == 2).all()) and bool((o["subset_len"] == 0).all()) and bool((o["type"] == 1).all())
+    g = torch.Generator(device="cpu")
+    g.manual_seed(5)
+    for i in torch.randint(0, n, (samples,), generator=g).tolist():
+        po = int(o["payload_off"][i])
+        for off_w, off_h, ln in [(int(o["key_off"][i]), int(cols["key_off"][i]), int(cols["key_len"][i])),
+                                 (int(o["value_off"][i]), int(cols["value_off"][i]), C5_VALUE)]:
+            assert torch.equal(wire[po + off_w:po + off_w + ln], heap[off_h:off_h + ln]), i
+
+
+def main_c5(args, dev):
+    """--workload c5: batched encode -> decode round trip of 1M Changes with 4 KB values per
+    step on one GPU (BASELINE configs[4]); value = Changes round-tripped per second."""
+    n = args.c5_changes
+    cols, heap, frame = c5_on_device(n, seed=55, dev=dev)
+    W = int(frame.sum())
+    out = torch.empty(W + 64, dtype=torch.uint8, device=dev)
+    foff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    wire = out[:W]
+    stream_off = torch.tensor([0, W], dtype=torch.int64, device=dev)
+    cap = n + 64
+    outs = alloc_outputs(cap, dev)
+    res = torch.zeros(C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+    ctx = drp_amd.Ctx(dev.index)
+    ext = torch.cuda.ExternalStream(ctx.stream, device=dev)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    enc_ms, dec_ms = [], []
+
+    def step(timed):
+        evs[0].record(ext)
+        ctx.encode_device(cols, heap, n, foff, out, W + 64)
+        evs[1].record(ext)
+        ctx.decode_device(wire, stream_off, None, outs, cap, res)
+        evs[2].record(ext)
+        if timed:
+            torch.cuda.synchronize(dev)
+            enc_ms.append(evs[0].elapsed_time(evs[1]))
+            dec_ms.append(evs[1].elapsed_time(evs[2]))
+
+    for _ in range(max(1, args.warmup)):
+        step(False)
+    torch.cuda.synchronize(dev)
+    assert int(foff[n]) == W, (int(foff[n]), W)
+    assert torch.equal(foff[1:] - foff[:-1], frame), "frame sizes differ from the encode.js layout"
+    verify_c5(cols, heap, wire, outs, res, n, dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    H = int(heap.numel())
+    e, d = float(np.mean(enc_ms)) / 1e3, float(np.mean(dec_ms)) / 1e3
+    b_enc, b_dec = 49 * n + H + W, W + 13 * n + 49 * n
+    out_line = {
+        "metric": "round-tripped Change frames/sec (batched encode + decode), 1 MI355X",
+        "value": n * args.steps / elapsed, "unit": "frames/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: C5 columns + heap generated on device (seeded), resident in HBM",
+        "config": {"workload": f"C5: {n} Changes, 4096 B values, key U[1,256], change/from/to U[0,2^32)",
+                   "wire_bytes": W, "heap_bytes": H},
+        "wire_GBps": 2 * W * args.steps / elapsed / 1e9,
+        "roofline": {"bound": "hbm", "achieved": (b_enc + b_dec) / (e + d) / 1e9, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": (b_enc + b_dec) / (e + d) / 1e9 / HBM_PEAK_GBPS,
+                     "traffic": None, "kernel": "encode (enc_size, enc_scan, enc_write) + speculative decode",
+                     "bytes_model": "encode 49*C + H + W, decode W + 13*F + 49*C"},
+        "encode": {"ms": e * 1e3, "GBps": b_enc / e / 1e9, "frac": b_enc / e / 1e9 / HBM_PEAK_GBPS},
+        "decode": {"ms": d * 1e3, "GBps": b_dec / d / 1e9, "frac": b_dec / d / 1e9 / HBM_PEAK_GBPS,
+                   "exact_fallbacks": ctx.timing().strict_reruns, "repair_passes": ctx.timing().spec_repairs},
+    }
+    print(json.dumps(out_line), flush=True)
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--frames", type=int, default=100_000_000, help="C2 frames per GPU")
-    ap.add_argument("--workload", choices=["c2", "c4"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2")
+    ap.add_argument("--c5-changes", type=int, default=1_000_000, help="C5 Changes per step")
     ap.add_argument("--streams", type=int, default=8192, help="C4 streams across all GPUs")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -187,6 +306,9 @@ def main():
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
 
+    if args.workload == "c5":
+        assert not dist, "c5 is a one-GPU round-trip workload"
+        return main_c5(args, dev)
     if args.workload == "c2":
         nframes = args.frames
         wire = c2_on_device(nframes, seed=1234 + rank, dev=dev)
@@ -225,7 +347,7 @@ def main():
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
-    dec_ms, fallbacks = [], 0
+    dec_ms, fallbacks, repairs = [], 0, 0
     t0 = time.perf_counter()
     ev0.record(ext)
     for _ in range(args.steps):
@@ -233,6 +355,7 @@ def main():
         t = ctx.timing()
         dec_ms.append(t.decode_ms)
         fallbacks += t.strict_reruns
+        repairs += t.spec_repairs
     ev1.record(ext)
     torch.cuda.synchronize(dev)
     if dist:
@@ -289,7 +412,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profile(kname, nframes),
                          "kernel": kname, "kernel_ms": dec_avg_s * 1e3,
-                         "exact_fallbacks": fallbacks,
+                         "exact_fallbacks": fallbacks, "repair_passes": repairs,
                          "bytes_per_launch": b_dec,
                          "bytes_model": "W + 13*frames + 49*changes (86+13+49 = 148 B/frame)"},
             "step_ms_hip_events": ev_ms / args.steps,

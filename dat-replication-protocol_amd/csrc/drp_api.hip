@@ -317,6 +317,7 @@ int run_decode_exact(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const ui
   hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
   c->timing.total_ms = ms;
   c->timing.finalize_ms = 0;
+  c->timing.spec_repairs = 0;
   c->timing.strict_reruns = 0;
   TRACE("decode done: tiles=%u flags=%u", h[0], h[1]);
   if (dstats) {
@@ -348,6 +349,8 @@ int run_decode_exact(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const ui
 
 // The default decode: speculate-and-verify kernel (drp_decode_spec.hip). Returns DRP_E_RETRY
 // when a prediction failed (or a bounded wait expired): the caller then runs the exact kernel.
+constexpr int kSpecRepairPasses = 6;
+
 int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
                     const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
                     uint64_t cap, drp_stream_result *res) {
@@ -416,14 +419,40 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     P.stats = dstats;
   }
   CHK(hipEventRecord(c->ev[1], st));
-  CHK(drp_launch_decode_spec(&P, NT, ns, tstream, sgscan, st));
-  CHK(hipEventRecord(c->ev[2], st));
-  CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
-                          scount, fr->type, co->flags, cap, res, st));
-  CHK(hipEventRecord(c->ev[3], st));
+  // claims + verification, then the prediction check on the host (one flag word) before any
+  // output is written: a failed prediction is repaired in place first. Verify patched the
+  // missed tiles' claims, so verify runs again (each pass fixes at least the first missed tile,
+  // whose entry is exact) until a pass has no miss. Only when that does not settle within a
+  // few passes (e.g. a protocol error on the exact chain) does the caller run the exact kernel.
+  CHK(drp_launch_spec_head(&P, NT, ns, tstream, st));
   uint32_t h[2];
   CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
+  const uint32_t miss = drp_spec_miss_bit();
+  int pass = 0;
+  if ((h[1] & drp_spec_retry_mask()) == miss) {
+    for (; pass < kSpecRepairPasses && (h[1] & miss); pass++) {
+      CHK(hipMemsetAsync(P.incl_e, 0, NT * 8, st));
+      CHK(hipMemsetAsync(P.overflow, 0, 4, st));
+      CHK(drp_launch_spec_verify(&P, NT, ns, tstream, st));
+      CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
+      CHK(hipStreamSynchronize(st));
+    }
+    TRACE("decode_spec: %d repair pass(es), flags=%#x", pass, h[1]);
+  }
+  const bool retry = (h[1] & drp_spec_retry_mask()) != 0;
+  if (!retry) {
+    CHK(drp_launch_spec_tail(&P, NT, ns, tstream, sgscan, st));
+    CHK(hipEventRecord(c->ev[2], st));
+    CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
+                            scount, fr->type, co->flags, cap, res, st));
+  } else {
+    CHK(hipEventRecord(c->ev[2], st));
+  }
+  CHK(hipEventRecord(c->ev[3], st));
+  CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  if (retry) h[1] |= miss;
   float ms = 0;
   hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
   c->timing.decode_ms = ms;
@@ -431,6 +460,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   c->timing.total_ms = ms;
   c->timing.finalize_ms = 0;
   c->timing.strict_reruns = 0;
+  c->timing.spec_repairs = (uint32_t)pass;
   TRACE("decode_spec done: tiles=%u flags=%#x", h[0], h[1]);
   if (dstats) {
     unsigned long long hs[56];
@@ -443,7 +473,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
                                "k2_stage", "k2_entry", "k2_link", "k3_stage", "k3_link", "k3_emit"};
     for (int k = 0; k < 14; k++)
       if (ph[k][0]) fprintf(stderr, " %s=%.0f", ph[k], (double)hs[40 + k] / (double)(h[0] ? h[0] : 1));
-    fprintf(stderr, " (avg cycles per tile)\n");
+    fprintf(stderr, " repairs=%d (avg cycles per tile)\n", pass);
     (void)hipFree(dstats);
   }
   if (h[1] & drp_spec_retry_mask()) return DRP_E_RETRY;

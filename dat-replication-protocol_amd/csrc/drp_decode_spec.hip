@@ -769,7 +769,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
       P.ent_n[ix] = 0;
     }
     exit_t = inside ? claim : et;  // pass-through tiles keep the entry
-    miss = !inside && claim != C_ID;
+    miss = !inside && claim != C_ID && claim != et;  // (a chain that rejoined the stream's one)
   } else {
     const uint64_t live = stage_live(P, G, buf);
     const Img m{buf, P.bytes, G.A, G.se};
@@ -781,6 +781,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     const bool carrier = is_pos(E) && E < s1;
     P.ent[ix] = carrier ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // exact, for kernel 3
     P.ent_n[ix] = carrier ? (uint8_t)(n & 0xFFFFu) : (uint8_t)0;
+    P.ent_c[ix] = carrier ? (uint8_t)(n >> 16) : (uint8_t)0;  // (a repair pass may take the fast check)
     count_t = block_sum_u32(n & 0xFFFFu, xf);
     nch_t = block_sum_u32(n >> 16, xf);
     // the last thread's R is the tile's exact exit; it must be what the claim predicted (an
@@ -798,6 +799,11 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   if (tid == NT - 1) {
     if (miss) {
       atomicOr(P.overflow, F_MISS);
+      // repair: the claim becomes the exit of the chain from this pass's entry. The first
+      // missed tile's entry is exact (induction), so each verify pass fixes at least that tile;
+      // the host re-runs verify until a pass has no miss (claims are only written on a miss,
+      // so a miss-free pass saw a constant claim array and its proof holds).
+      P.claim[t] = inside ? exit_t : C_ID;
       if (P.stats) {  // debug capture (DRP_STATS=1): the first misses
         const unsigned long long q = atomicAdd(&P.stats[0], 1ull);
         if (q < 5) {
@@ -1044,6 +1050,51 @@ extern "C" hipError_t drp_launch_stream_counts(const uint64_t *tile_prefix, uint
 
 extern "C" uint32_t drp_spec_tile_bytes(void) { return spec::TILE; }
 extern "C" uint32_t drp_spec_retry_mask(void) { return spec::F_MISS | spec::F_WAIT; }
+
+extern "C" uint32_t drp_spec_miss_bit(void) { return spec::F_MISS; }
+
+// Claims and verification only (the host checks the prediction before anything is emitted).
+extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
+                                           uint32_t *tile_stream, hipStream_t st) {
+  if (nt_max == 0) return hipSuccess;
+  DecodeParams Q = *P;
+  Q.tile_stream = nullptr;
+  if (nstreams > 1) {
+    const uint32_t blk = 256;
+    hipLaunchKernelGGL(spec::tile_stream_kernel, dim3((uint32_t)((nt_max + blk - 1) / blk)), dim3(blk), 0, st,
+                       P->tile_prefix, nstreams, nt_max, tile_stream);
+    Q.tile_stream = tile_stream;
+  }
+  hipLaunchKernelGGL(spec::spec_claims, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  return hipGetLastError();
+}
+
+// One more verify pass over the repaired claims (the caller clears incl_e and the flags first).
+extern "C" hipError_t drp_launch_spec_verify(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
+                                             uint32_t *tile_stream, hipStream_t st) {
+  if (nt_max == 0) return hipSuccess;
+  DecodeParams Q = *P;
+  Q.tile_stream = nstreams > 1 ? tile_stream : nullptr;
+  hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  return hipGetLastError();
+}
+
+// Everything after verification: output bases, emission, change-count bases, stream counts.
+extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
+                                           uint32_t *tile_stream, uint64_t *scan_tmp, hipStream_t st) {
+  if (nt_max == 0) return hipSuccess;
+  DecodeParams Q = *P;
+  Q.tile_stream = nstreams > 1 ? tile_stream : nullptr;
+  hipError_t e = drp_launch_tile_scan(Q.tile_count, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_base, Q.cap,
+                                      Q.overflow, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(spec::emit_tiles, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  e = drp_launch_tile_scan(Q.tile_nch, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_nch_base, ~0ull, Q.overflow, st);
+  if (e != hipSuccess) return e;
+  return drp_launch_stream_counts(Q.tile_prefix, nstreams, Q.tile_count, Q.tile_base, Q.tile_nch, Q.tile_nch_base,
+                                  Q.scount, st);
+}
 
 extern "C" hipError_t drp_launch_decode_spec(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                              uint32_t *tile_stream, uint64_t *scan_tmp, hipStream_t st) {

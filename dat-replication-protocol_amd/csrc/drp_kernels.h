@@ -74,6 +74,13 @@ hipError_t drp_launch_decode(uint32_t B, const drp::DecodeParams *P, uint32_t gr
 uint32_t drp_decode_waves_per_group(void);  // tiles (waves) per workgroup; grid counts groups
 uint32_t drp_spec_tile_bytes(void);
 uint32_t drp_spec_retry_mask(void);
+uint32_t drp_spec_miss_bit(void);
+hipError_t drp_launch_spec_head(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
+                                uint32_t *tile_stream, hipStream_t st);
+hipError_t drp_launch_spec_verify(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
+                                  uint32_t *tile_stream, hipStream_t st);
+hipError_t drp_launch_spec_tail(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
+                                uint32_t *tile_stream, uint64_t *scan_tmp, hipStream_t st);
 hipError_t drp_launch_decode_spec(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                   uint32_t *tile_stream, uint64_t *scan_tmp, hipStream_t st);
 // exclusive scan of a per-tile u64 array over all tiles; flags capacity overflow of the total

@@ -60,7 +60,7 @@ class StreamStats(C.Structure):
 
 class Timing(C.Structure):
     _fields_ = [("decode_ms", C.c_float), ("finalize_ms", C.c_float), ("total_ms", C.c_float),
-                ("strict_reruns", U32), ("reserved", U32)]
+                ("strict_reruns", U32), ("spec_repairs", U32)]
 
 
 _lib = None
@@ -217,6 +217,17 @@ class Ctx:
         _chk("drp_decode_device", rc)
 
     # ---- encode -----------------------------------------------------------------------
+    def encode_device(self, cols_t, heap_t, n, frame_off_t, out_t, cap):
+        """Device encode over torch CUDA tensors (asynchronous, on this ctx's stream): cols_t
+        holds the drp_change_src columns (int64 offsets, int32 lengths, int64 numbers, uint8
+        flags); frame_off_t (int64, n + 1) receives the frame offsets, out_t (uint8) the wire."""
+        tp = lambda t: C.c_void_p(t.data_ptr())
+        src = ChangeSrc(*[tp(cols_t[k]) for k in ["key_off", "key_len", "subset_off", "subset_len",
+                                                  "value_off", "value_len", "change", "from", "to",
+                                                  "flags"]])
+        _chk("drp_encode_device", self.L.drp_encode_device(self.h, C.byref(src), tp(heap_t), n,
+                                                           tp(frame_off_t), tp(out_t), cap))
+
     def encode_batch(self, heap, cols):
         n = len(cols["key_len"])
         h = np.frombuffer(bytes(heap), np.uint8) if not isinstance(heap, np.ndarray) else heap

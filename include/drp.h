@@ -139,8 +139,8 @@ typedef struct drp_timing {
   float decode_ms;   /* main decode kernel */
   float finalize_ms; /* per-stream finalize kernel */
   float total_ms;    /* memset + decode + finalize (+ strict re-run if any) */
-  uint32_t strict_reruns;
-  uint32_t reserved;
+  uint32_t strict_reruns; /* 1: the speculative decode fell back to the exact kernel */
+  uint32_t spec_repairs;  /* verify passes that repaired failed predictions in place */
 } drp_timing;
 
 /* ---- context ------------------------------------------------------------- */

@@ -2,6 +2,13 @@
 import os
 import sys
 
+import torch  # noqa: E402
+
+# torch's HIP runtime initialises before libdrp's (the order bench.py uses): a process that
+# loads libdrp first then fails torch's lazy device init ("no ROCm-capable device")
+if torch.cuda.is_available():
+    torch.cuda.init()
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "dat-replication-protocol_amd", "python"))
 import drp_amd  # noqa: E402,F401

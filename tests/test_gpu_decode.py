@@ -183,3 +183,35 @@ def test_speculative_matches_exact(ctx, shape):
     assert_same(spec, O.decode_batch(wire, chunk=65536), shape)
     if shape == "c2":
         assert reruns == 0, "prediction failed on a clean C2 stream"
+
+
+def test_c5_device_round_trip(ctx):
+    """C5 shape through the device entry points: drp_encode_device -> drp_decode_device; frame
+    sizes match the encode.js layout, decoded columns equal the encoder input, sampled key and
+    value bytes equal the heap (the same checks bench.py --workload c5 runs at full size)."""
+    import ctypes as C
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from _gpu import drp_amd
+    dev = torch.device("cuda", 0)
+    n = 20_000
+    cols, heap, frame = bench.c5_on_device(n, seed=3, dev=dev)
+    W = int(frame.sum())
+    out = torch.zeros(W + 64, dtype=torch.uint8, device=dev)
+    foff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ctx.encode_device(cols, heap, n, foff, out, W + 64)
+    outs = bench.alloc_outputs(n + 64, dev)
+    res = torch.zeros(C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+    wire = out[:W]
+    ctx.decode_device(wire, torch.tensor([0, W], dtype=torch.int64, device=dev), None, outs, n + 64, res)
+    torch.cuda.synchronize(dev)
+    assert int(foff[n]) == W and torch.equal(foff[1:] - foff[:-1], frame)
+    bench.verify_c5(cols, heap, wire, outs, res, n, dev, samples=64)
+    # and the wire equals the CPU restatement of encode.js on the same columns
+    hc = heap.cpu().numpy()
+    cc = {k: v.cpu().numpy() for k, v in cols.items()}
+    cc = {k: (v.astype(np.uint64) if k in ("key_off", "subset_off", "value_off", "change", "from", "to")
+              else v.astype(np.uint32) if k.endswith("_len") else v) for k, v in cc.items()}
+    assert wire.cpu().numpy().tobytes() == O.encode_changes(hc.tobytes(), cc)
