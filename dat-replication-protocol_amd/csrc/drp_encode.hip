@@ -94,8 +94,52 @@ __global__ __launch_bounds__(SCAN_BLK) void enc_addbase_kernel(EncodeParams P) {
   if (i < P.n) P.frame_off[i] += P.block_sum[blockIdx.x];
 }
 
+__device__ __forceinline__ uint64_t enc_funnel(uint64_t lo, uint64_t hi, uint32_t sh) {
+  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+
+// Wave copy of n bytes: byte head up to 16-byte alignment of dst, then one aligned 16-byte
+// store per lane per step whose bytes come from the two aligned 16-byte source blocks that
+// cover them (funnel shift by the wave-uniform source misalignment), then a byte tail. The
+// second block of the last step lies in the aligned 16 bytes that hold the last source byte,
+// so no load leaves the source's pages.
 __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t lane) {
-  for (uint64_t k = lane; k < n; k += 64) dst[k] = src[k];
+  if (n < 128) {
+    for (uint64_t k = lane; k < n; k += 64) dst[k] = src[k];
+    return;
+  }
+  const uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15);
+  if (lane < head) dst[lane] = src[lane];
+  dst += head;
+  src += head;
+  n -= head;
+  const uint64_t nb = n >> 4;
+  const uint32_t sh = (uint32_t)((uintptr_t)src & 15);
+  const uint4 *sa = reinterpret_cast<const uint4 *>(src - sh);
+  uint4 *da = reinterpret_cast<uint4 *>(dst);
+  for (uint64_t b = lane; b < nb; b += 64) {
+    const uint4 lo = sa[b];
+    uint4 out;
+    if (sh == 0) {
+      out = lo;
+    } else {
+      const uint4 hi = sa[b + 1];
+      const uint64_t q0 = ((uint64_t)lo.y << 32) | lo.x, q1 = ((uint64_t)lo.w << 32) | lo.z;
+      const uint64_t q2 = ((uint64_t)hi.y << 32) | hi.x, q3 = ((uint64_t)hi.w << 32) | hi.z;
+      uint64_t w0, w1;
+      if (sh < 8) {
+        w0 = enc_funnel(q0, q1, 8 * sh);
+        w1 = enc_funnel(q1, q2, 8 * sh);
+      } else {
+        w0 = enc_funnel(q1, q2, 8 * (sh - 8));
+        w1 = enc_funnel(q2, q3, 8 * (sh - 8));
+      }
+      out = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+    }
+    da[b] = out;
+  }
+  const uint32_t tail = (uint32_t)(n & 15);
+  if (lane < tail) dst[(nb << 4) + lane] = src[(nb << 4) + lane];
 }
 
 // one wave per frame (grid-stride over frames)
