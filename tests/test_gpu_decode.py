@@ -215,3 +215,13 @@ def test_c5_device_round_trip(ctx):
     cc = {k: (v.astype(np.uint64) if k in ("key_off", "subset_off", "value_off", "change", "from", "to")
               else v.astype(np.uint32) if k.endswith("_len") else v) for k, v in cc.items()}
     assert wire.cpu().numpy().tobytes() == O.encode_changes(hc.tobytes(), cc)
+
+
+def test_c3_many_blobs(ctx):
+    """C3 shape at 40 MiB: 1 MiB random blobs between C2 runs; every column bit-exact vs the
+    oracle's 64 KiB-chunked decode, and neither a repair nor a fallback changes the result."""
+    from _gpu import assert_same
+    wire = S.c3_stream(random.Random(12), 40, frames_per_unit=1000)
+    g = ctx.decode_batch(wire)
+    assert g["nframes"] == 40 * 1001 and g["err_code"] == 0
+    assert_same(g, O.decode_batch(wire, chunk=65536), "c3x40")
