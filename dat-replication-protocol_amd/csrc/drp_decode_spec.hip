@@ -200,6 +200,9 @@ __device__ __forceinline__ uint64_t walk(const Img &m, uint64_t E, uint64_t s1, 
 // returns S_HBM (undecided) instead of reading HBM. On success also returns walk(c) for this
 // thread (exit past s1 and the frames delivered in the thread's bytes).
 enum : uint32_t { S_DEAD = 0, S_OK = 1, S_HBM = 2 };
+#ifndef DRP_KSTRONG_HBM
+#define DRP_KSTRONG_HBM 4
+#endif
 template <bool LOCAL>
 __device__ __forceinline__ uint32_t strong(const Img &m, uint64_t c, uint64_t s1, uint64_t &R, uint32_t &n,
                                            bool &far) {
@@ -207,8 +210,9 @@ __device__ __forceinline__ uint32_t strong(const Img &m, uint64_t c, uint64_t s1
   n = 0;
   R = NONE;
   far = false;
+  constexpr int K = LOCAL ? KSTRONG : DRP_KSTRONG_HBM;  // frames a deferred candidate survives in HBM
 #pragma unroll 1
-  for (int k = 0; k < KSTRONG; k++) {
+  for (int k = 0; k < K; k++) {
     if (p >= m.se) break;  // reached the stream end: survived
     if (LOCAL && p + 16 > m.A + IMG) return S_HBM;
     const Hdr h = m.at(p);
