@@ -22,8 +22,10 @@
 //   4. verify    The exact chain from e_t is walked (Jacobi again, seeded with the spec
 //                chain, so usually one round). Its exit must equal claim_t (or e_t for an
 //                identity claim); by induction from the stream entry every e_t is then exact.
-//                Any mismatch raises SPEC_MISS and the host re-runs the exact kernel
-//                (decode_tiles), so results never depend on the prediction.
+//                Any mismatch raises SPEC_MISS; the missed tile's claim becomes its
+//                verified exit and the host re-runs verification (repair passes) before
+//                anything is emitted, falling back to the exact kernel (decode_tiles) only
+//                when that does not settle, so results never depend on the prediction.
 //   5. count     Exact frame count of the tile -> decoupled look-back (with helping) for the
 //                output base; frames are decoded from LDS into the SoA columns.
 //
@@ -1100,26 +1102,3 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
                                   Q.scount, st);
 }
 
-extern "C" hipError_t drp_launch_decode_spec(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
-                                             uint32_t *tile_stream, uint64_t *scan_tmp, hipStream_t st) {
-  if (nt_max == 0) return hipSuccess;
-  DecodeParams Q = *P;
-  Q.tile_stream = nullptr;
-  if (nstreams > 1) {
-    const uint32_t blk = 256;
-    hipLaunchKernelGGL(spec::tile_stream_kernel, dim3((uint32_t)((nt_max + blk - 1) / blk)), dim3(blk), 0, st,
-                       P->tile_prefix, nstreams, nt_max, tile_stream);
-    Q.tile_stream = tile_stream;
-  }
-  const uint32_t grid = (uint32_t)nt_max;
-  hipLaunchKernelGGL(spec::spec_claims, dim3(grid), dim3(spec::NT), 0, st, Q);
-  hipLaunchKernelGGL(spec::verify_counts, dim3(grid), dim3(spec::NT), 0, st, Q);
-  hipError_t e = drp_launch_tile_scan(Q.tile_count, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_base, Q.cap,
-                                     Q.overflow, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(spec::emit_tiles, dim3(grid), dim3(spec::NT), 0, st, Q);
-  e = drp_launch_tile_scan(Q.tile_nch, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_nch_base, ~0ull, Q.overflow, st);
-  if (e != hipSuccess) return e;
-  return drp_launch_stream_counts(Q.tile_prefix, nstreams, Q.tile_count, Q.tile_base, Q.tile_nch, Q.tile_nch_base,
-                                  Q.scount, st);
-}

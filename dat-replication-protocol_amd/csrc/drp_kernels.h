@@ -81,8 +81,6 @@ hipError_t drp_launch_spec_verify(const drp::DecodeParams *P, uint64_t nt_max, u
                                   uint32_t *tile_stream, hipStream_t st);
 hipError_t drp_launch_spec_tail(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                 uint32_t *tile_stream, uint64_t *scan_tmp, hipStream_t st);
-hipError_t drp_launch_decode_spec(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
-                                  uint32_t *tile_stream, uint64_t *scan_tmp, hipStream_t st);
 // exclusive scan of a per-tile u64 array over all tiles; flags capacity overflow of the total
 hipError_t drp_launch_tile_scan(const uint64_t *in, const uint64_t *tile_prefix, uint64_t nstreams, uint64_t nt_max,
                                 uint64_t *tmp, uint64_t *out, uint64_t cap, uint32_t *overflow, hipStream_t st);
