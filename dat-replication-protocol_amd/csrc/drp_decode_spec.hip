@@ -762,14 +762,38 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     if (tid > k && eb != 0xFF && (eb & 0x40)) bad = 1;
     if (claim == C_ID) bad = 1;
   }
-  const bool fast = !block_max_u32(bad, xf);
+  // one exchange: any thread disagrees (max), and the fast path's frame and change counts
+  const bool mine = tid >= k && eb != 0xFF;
+  uint32_t cnt_f = mine ? P.ent_n[ix] : 0u, cnt_c = mine ? P.ent_c[ix] : 0u;
+  {
+    cnt_f = wave_sum32(cnt_f);
+    cnt_c = wave_sum32(cnt_c);
+#pragma unroll
+    for (uint32_t d = 1; d < WAVE; d <<= 1) bad = max(bad, shfl_xor32(bad, d));
+    if (lane == 0) {
+      xr[wid] = ((uint64_t)cnt_c << 32) | cnt_f;
+      xf[wid] = bad;
+    }
+    __syncthreads();
+    uint64_t acc = 0;
+    uint32_t b = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NT / WAVE; w++) {
+      acc += xr[w];
+      b = max(b, xf[w]);
+    }
+    __syncthreads();
+    cnt_f = (uint32_t)acc;
+    cnt_c = (uint32_t)(acc >> 32);
+    bad = b;
+  }
+  const bool fast = !bad;
   uint32_t count_t, nch_t;
   uint64_t exit_t;
   bool miss;
   if (fast) {
-    const bool mine = tid >= k && eb != 0xFF;
-    count_t = block_sum_u32(mine ? P.ent_n[ix] : 0u, xf);
-    nch_t = block_sum_u32(mine ? P.ent_c[ix] : 0u, xf);
+    count_t = cnt_f;
+    nch_t = cnt_c;
     if (tid < k) {
       P.ent[ix] = 0xFF;
       P.ent_n[ix] = 0;
