@@ -142,6 +142,9 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
   if (lane < tail) dst[(nb << 4) + lane] = src[(nb << 4) + lane];
 }
 
+#ifndef DRP_ENC_WAVES
+#define DRP_ENC_WAVES 65536  // waves of the write kernel (grid-stride over frames)
+#endif
 // one wave per frame (grid-stride over frames)
 __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
   const uint32_t lane = lane_id();
@@ -254,7 +257,7 @@ extern "C" hipError_t drp_launch_encode(const EncodeParams *Pp, hipStream_t st) 
   hipLaunchKernelGGL(enc_blocksum_kernel, dim3(1), dim3(SCAN_BLK), 0, st, P, nblk);
   hipLaunchKernelGGL(enc_addbase_kernel, dim3((uint32_t)nblk), dim3(SCAN_BLK), 0, st, P);
   if (P.out) {
-    uint64_t waves = P.n < 65536 ? P.n : 65536;
+    uint64_t waves = P.n < DRP_ENC_WAVES ? P.n : DRP_ENC_WAVES;  // one frame per wave at a time
     uint32_t grid = (uint32_t)((waves * 64 + 255) / 256);
     hipLaunchKernelGGL(enc_write_kernel, dim3(grid), dim3(256), 0, st, P);
   }
