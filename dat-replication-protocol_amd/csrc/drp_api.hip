@@ -208,9 +208,11 @@ uint64_t drp_decode_scratch_bytes(drp_ctx *c, uint64_t n, uint64_t nstreams) {
 
 namespace {
 
-int run_decode_exact(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
-               const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
-               uint64_t cap, drp_stream_result *res) {
+constexpr int kWaitExpired = -100;  // internal: a bounded look-back spin gave up (retryable)
+
+int run_decode_exact_once(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
+                          const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
+                          uint64_t cap, drp_stream_result *res) {
   if (ns == 0) return DRP_OK;
   if (((uintptr_t)bytes & 15) != 0) return DRP_E_INVAL;
   const DecLayout L = dec_layout(c->B, nbytes, ns);
@@ -342,9 +344,28 @@ int run_decode_exact(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const ui
     }
     hipFree(dtrace);
   }
-  if (h[1] & ~1u) return DRP_E_HIP;  // bounded wait expired / inconsistent walk inside the kernel
+  if (h[1] & ~1u) return kWaitExpired;  // bounded wait expired / inconsistent walk inside the kernel
   if (h[1]) return DRP_E_CAPACITY;
   return DRP_OK;
+}
+
+// A bounded spin that expires (a preempted or slow predecessor wave) is not an input error:
+// the kernel's scratch is reset on entry, so the call is re-run once before reporting it.
+int run_decode_exact(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
+                     const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
+                     uint64_t cap, drp_stream_result *res) {
+  int r = run_decode_exact_once(c, bytes, nbytes, stream_off, entry, ns, fr, co, cap, res);
+  uint32_t retries = 0;
+  if (r == kWaitExpired) {
+    const float ms = c->timing.decode_ms, tot = c->timing.total_ms;
+    TRACE("decode_exact: bounded wait expired, re-running once");
+    r = run_decode_exact_once(c, bytes, nbytes, stream_off, entry, ns, fr, co, cap, res);
+    c->timing.decode_ms += ms;
+    c->timing.total_ms += tot;
+    retries = 1;
+  }
+  c->timing.exact_retries = retries;
+  return r == kWaitExpired ? DRP_E_HIP : r;
 }
 
 // The default decode: speculate-and-verify kernel (drp_decode_spec.hip). Returns DRP_E_RETRY
@@ -460,6 +481,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   c->timing.total_ms = ms;
   c->timing.finalize_ms = 0;
   c->timing.strict_reruns = 0;
+  c->timing.exact_retries = 0;
   c->timing.spec_repairs = (uint32_t)pass;
   TRACE("decode_spec done: tiles=%u flags=%#x", h[0], h[1]);
   if (dstats) {
@@ -649,8 +671,8 @@ int drp_decode_batch(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *ca
   return rc;
 }
 
-int drp_encode_device(drp_ctx *c, const drp_change_src *src, const uint8_t *heap, uint64_t n,
-                      uint64_t *frame_off, uint8_t *out, uint64_t cap) {
+int drp_encode_device(drp_ctx *c, const drp_change_src *src, const uint8_t *heap, uint64_t heap_bytes,
+                      uint64_t n, uint64_t *frame_off, uint8_t *out, uint64_t cap) {
   if (!c || !src || !frame_off) return DRP_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
   const uint64_t nblk = (n + 1023) / 1024;
@@ -658,6 +680,7 @@ int drp_encode_device(drp_ctx *c, const drp_change_src *src, const uint8_t *heap
   EncodeParams P;
   P.src = *src;
   P.heap = heap;
+  P.heap_bytes = heap_bytes;
   P.n = n;
   P.frame_off = frame_off;
   P.out = out;
@@ -719,7 +742,7 @@ int drp_encode_size(drp_ctx *c, const drp_change_src *src, uint64_t n, uint64_t 
   if (rc) return rc;
   if (!c->out_stage.ensure((n + 1) * 8)) return DRP_E_NOMEM;
   uint64_t *foff = c->out_stage.at<uint64_t>(0);
-  rc = drp_encode_device(c, &dsrc, dheap, n, foff, nullptr, ~0ull);
+  rc = drp_encode_device(c, &dsrc, dheap, ~0ull, n, foff, nullptr, ~0ull);  // sizes only: no heap read
   if (rc) return rc;
   CHK(hipMemcpyAsync(wire_bytes, foff + n, 8, hipMemcpyDeviceToHost, c->st));
   CHK(hipStreamSynchronize(c->st));
@@ -739,11 +762,15 @@ int drp_encode_batch(drp_ctx *c, const drp_change_src *src, const uint8_t *heap,
   if (!c->out_stage.ensure(fo_bytes + (odev ? 0 : cap + 64))) return DRP_E_NOMEM;
   uint64_t *foff = c->out_stage.at<uint64_t>(0);
   uint8_t *dout = odev ? out : c->out_stage.at<uint8_t>(fo_bytes);
-  rc = drp_encode_device(c, &dsrc, dheap, n, foff, dout, cap);
+  rc = drp_encode_device(c, &dsrc, dheap, heap_bytes, n, foff, dout, cap);
   if (rc) return rc;
   uint64_t total = 0;
   CHK(hipMemcpyAsync(&total, foff + n, 8, hipMemcpyDeviceToHost, c->st));
   CHK(hipStreamSynchronize(c->st));
+  if (total == ~0ull) {  // a row's key/subset/value range is outside the heap
+    *written = 0;
+    return DRP_E_INVAL;
+  }
   *written = total;
   if (total > cap) return DRP_E_CAPACITY;
   if (!odev && total) {

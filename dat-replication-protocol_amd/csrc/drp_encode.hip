@@ -41,6 +41,12 @@ __device__ __forceinline__ uint64_t payload_len(const drp_change_src &s, uint64_
 }
 
 constexpr uint32_t SCAN_BLK = 1024;
+constexpr uint32_t ENC_F_RANGE = 2u;  // overflow bit: a row's heap range leaves the heap
+
+// [off, off + len) inside [0, heap_bytes) without wrapping
+__device__ __forceinline__ bool in_heap(uint64_t off, uint32_t len, uint64_t heap_bytes) {
+  return (uint64_t)len <= heap_bytes && off <= heap_bytes - len;
+}
 
 __global__ __launch_bounds__(SCAN_BLK) void enc_size_kernel(EncodeParams P) {
   __shared__ uint64_t part[SCAN_BLK];
@@ -49,6 +55,12 @@ __global__ __launch_bounds__(SCAN_BLK) void enc_size_kernel(EncodeParams P) {
   if (i < P.n) {
     const uint64_t pl = payload_len(P.src, i);
     sz = vlen64(pl + 1) + 1 + pl;
+    const drp_change_src &s = P.src;
+    const uint32_t fl = s.flags[i];
+    bool ok = in_heap(s.key_off[i], s.key_len[i], P.heap_bytes);
+    if (fl & DRP_F_SUBSET) ok = ok && in_heap(s.subset_off[i], s.subset_len[i], P.heap_bytes);
+    if (fl & DRP_F_VALUE) ok = ok && in_heap(s.value_off[i], s.value_len[i], P.heap_bytes);
+    if (!ok) atomicOr(P.overflow, ENC_F_RANGE);
   }
   part[threadIdx.x] = sz;
   __syncthreads();
@@ -84,8 +96,10 @@ __global__ __launch_bounds__(SCAN_BLK) void enc_blocksum_kernel(EncodeParams P, 
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    P.frame_off[P.n] = carry;
-    if (carry > P.cap) atomicOr(P.overflow, 1u);
+    // a row outside the heap poisons the total (UINT64_MAX > any cap): nothing is written
+    const bool range_bad = (__hip_atomic_load(P.overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ENC_F_RANGE) != 0;
+    P.frame_off[P.n] = range_bad ? ~0ull : carry;
+    if (range_bad || carry > P.cap) atomicOr(P.overflow, 1u);
   }
 }
 
@@ -187,7 +201,7 @@ __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
       off += s.key_len[i];
     }
     {
-      uint8_t t[36];
+      uint8_t t[48];  // 3 tags + 3 u64 varints (<= 10 B each) + value tag + u32 length varint = 39 B
       uint32_t m = 0;
       t[m++] = 0x18;
       m += venc(s.change[i], t + m);

@@ -57,12 +57,13 @@ struct DecodeParams {
 struct EncodeParams {
   drp_change_src src;
   const uint8_t *heap;
+  uint64_t heap_bytes;  // rows whose key/subset/value range leaves [0, heap_bytes) are rejected
   uint64_t n;
   uint64_t *frame_off;  // [n+1] exclusive prefix of frame sizes (written)
   uint8_t *out;
   uint64_t cap;
   uint64_t *block_sum;  // per-block partial sums (scan scratch)
-  uint32_t *overflow;
+  uint32_t *overflow;  // bit 0 output capacity, bit 1 a row's heap range is out of bounds
 };
 
 }  // namespace drp

@@ -60,7 +60,7 @@ class StreamStats(C.Structure):
 
 class Timing(C.Structure):
     _fields_ = [("decode_ms", C.c_float), ("finalize_ms", C.c_float), ("total_ms", C.c_float),
-                ("strict_reruns", U32), ("spec_repairs", U32)]
+                ("strict_reruns", U32), ("spec_repairs", U32), ("exact_retries", U32), ("reserved", U32)]
 
 
 _lib = None
@@ -92,7 +92,7 @@ def lib():
                                        C.POINTER(Changes), U64, C.POINTER(U64), C.POINTER(U64),
                                        C.POINTER(U32), C.POINTER(U32)]
         L.drp_encode_size.argtypes = [P, C.POINTER(ChangeSrc), U64, C.POINTER(U64)]
-        L.drp_encode_device.argtypes = [P, C.POINTER(ChangeSrc), P, U64, P, P, U64]
+        L.drp_encode_device.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, P, U64]
         L.drp_encode_batch.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, U64,
                                        C.POINTER(U64)]
         L.drp_index_scan.argtypes = [P, P, U64, P]
@@ -168,6 +168,27 @@ class Ctx:
     def stream(self):
         return self.L.drp_stream(self.h)
 
+    # libdrp launches on its own non-blocking HIP stream: work torch queued on its current
+    # stream (allocations, fills, copies producing our inputs) must be ordered before a
+    # libdrp call, and torch must not read libdrp outputs before libdrp's stream is done.
+    def _ext(self, dev):
+        import torch
+        ext = getattr(self, "_ext_stream", None)
+        if ext is None or ext.device != dev:
+            ext = torch.cuda.ExternalStream(self.stream, device=dev)
+            self._ext_stream = ext
+        return ext
+
+    def order_after_torch(self, t):
+        """libdrp's stream waits for the work queued so far on torch's current stream."""
+        import torch
+        self._ext(t.device).wait_stream(torch.cuda.current_stream(t.device))
+
+    def order_torch_after(self, t):
+        """torch's current stream waits for the work queued so far on libdrp's stream."""
+        import torch
+        torch.cuda.current_stream(t.device).wait_stream(self._ext(t.device))
+
     def set_strict(self, on):
         _chk("drp_set_strict", self.L.drp_set_strict(self.h, 1 if on else 0))
 
@@ -212,9 +233,11 @@ class Ctx:
         tp = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
         fr, co = _structs(outs, tp)
         ns = stream_off_t.numel() - 1
+        self.order_after_torch(wire_t)
         rc = self.L.drp_decode_device(self.h, tp(wire_t), wire_t.numel(), tp(stream_off_t),
                                       tp(entry_t), ns, C.byref(fr), C.byref(co), cap, tp(results_t))
         _chk("drp_decode_device", rc)
+        self.order_torch_after(wire_t)
 
     # ---- encode -----------------------------------------------------------------------
     def encode_device(self, cols_t, heap_t, n, frame_off_t, out_t, cap):
@@ -225,8 +248,10 @@ class Ctx:
         src = ChangeSrc(*[tp(cols_t[k]) for k in ["key_off", "key_len", "subset_off", "subset_len",
                                                   "value_off", "value_len", "change", "from", "to",
                                                   "flags"]])
-        _chk("drp_encode_device", self.L.drp_encode_device(self.h, C.byref(src), tp(heap_t), n,
-                                                           tp(frame_off_t), tp(out_t), cap))
+        self.order_after_torch(heap_t)
+        _chk("drp_encode_device", self.L.drp_encode_device(self.h, C.byref(src), tp(heap_t), heap_t.numel(),
+                                                           n, tp(frame_off_t), tp(out_t), cap))
+        self.order_torch_after(heap_t)
 
     def encode_batch(self, heap, cols):
         n = len(cols["key_len"])

@@ -57,6 +57,7 @@ def global_index_device(ctx, table):
     n = table.shape[0]
     base = torch.empty(n, dtype=torch.int64, device=table.device)
     if n:
+        ctx.order_after_torch(table)  # the gather / cat / copy producing `table` ran on torch's stream
         _chk("drp_index_scan", ctx.L.drp_index_scan(ctx.h, C.c_void_p(table.data_ptr()), n,
                                                     C.c_void_p(base.data_ptr())))
         _chk("drp_synchronize", ctx.L.drp_synchronize(ctx.h))
@@ -70,6 +71,7 @@ def local_stats_device(ctx, results_t, stream_off_t):
     if n:
         from drp_amd import _chk
 
+        ctx.order_after_torch(stats)  # the zero fill of `stats` ran on torch's stream
         _chk("drp_stream_stats_from_results",
              ctx.L.drp_stream_stats_from_results(ctx.h, C.c_void_p(results_t.data_ptr()),
                                                  C.c_void_p(stream_off_t.data_ptr()), n,

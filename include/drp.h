@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DRP_ABI_VERSION 1
+#define DRP_ABI_VERSION 2
 
 /* ---- return codes -------------------------------------------------------- */
 #define DRP_OK 0
@@ -141,6 +141,8 @@ typedef struct drp_timing {
   float total_ms;    /* memset + decode + finalize (+ strict re-run if any) */
   uint32_t strict_reruns; /* 1: the speculative decode fell back to the exact kernel */
   uint32_t spec_repairs;  /* verify passes that repaired failed predictions in place */
+  uint32_t exact_retries; /* 1: the exact kernel's bounded look-back wait expired and it was re-run */
+  uint32_t reserved;
 } drp_timing;
 
 /* ---- context ------------------------------------------------------------- */
@@ -191,10 +193,11 @@ int drp_decode_batch(drp_ctx *ctx, const uint8_t *bytes, uint64_t n, drp_carry *
 /* Wire size of encoding rows [0,n) as change frames (varint(len+1) 0x01 payload). */
 int drp_encode_size(drp_ctx *ctx, const drp_change_src *src, uint64_t n, uint64_t *wire_bytes);
 /* Device pointers; asynchronous. frame_off[n+1] (device scratch, written) receives the
- * exclusive prefix of frame sizes; *wire_bytes is written to device memory. */
-int drp_encode_device(drp_ctx *ctx, const drp_change_src *src, const uint8_t *heap, uint64_t n,
-                      uint64_t *frame_off, uint8_t *out, uint64_t cap);
-/* Synchronous; host or device pointers. */
+ * exclusive prefix of frame sizes (frame_off[n] = wire bytes). A row whose key/subset/value
+ * range leaves [0, heap_bytes) sets frame_off[n] = UINT64_MAX and nothing is written. */
+int drp_encode_device(drp_ctx *ctx, const drp_change_src *src, const uint8_t *heap, uint64_t heap_bytes,
+                      uint64_t n, uint64_t *frame_off, uint8_t *out, uint64_t cap);
+/* Synchronous; host or device pointers. DRP_E_INVAL if a row's range leaves the heap. */
 int drp_encode_batch(drp_ctx *ctx, const drp_change_src *src, const uint8_t *heap,
                      uint64_t heap_bytes, uint64_t n, uint8_t *out, uint64_t cap,
                      uint64_t *written);

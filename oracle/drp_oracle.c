@@ -439,11 +439,9 @@ static void dec_write(oracle_dec *d, const uint8_t *data, uint64_t len) {
   d->abs = base + len;
 }
 
-/* Batch view used by the parity tests and the CPU baseline: feed bytes[0,n) in
- * `chunk`-byte writes (0 = one write) starting with `blob_remaining` bytes of an open
- * blob, and report SoA frames + tail exactly as drp_decode_batch does. */
-ORACLE_API int oracle_decode_batch(const uint8_t *bytes, uint64_t n, uint64_t chunk,
-                                   uint64_t blob_remaining, uint64_t cap, uint64_t *payload_off,
+/* Shared body of oracle_decode_batch / oracle_decode_writes. */
+static int decode_writes(const uint8_t *bytes, uint64_t n, const uint64_t *sizes, uint64_t nsizes,
+                         uint64_t blob_remaining, uint64_t cap, uint64_t *payload_off,
                                    uint32_t *plen, uint8_t *type, uint32_t *key_off,
                                    uint32_t *key_len, uint32_t *subset_off, uint32_t *subset_len,
                                    uint32_t *value_off, uint32_t *value_len, uint64_t *change,
@@ -478,10 +476,12 @@ ORACLE_API int oracle_decode_batch(const uint8_t *bytes, uint64_t n, uint64_t ch
     d.blob_frame = 0;
     emit_frame(&d, DRP_TYPE_BLOB | DRP_FRAME_CONT, 0, blob_remaining);
   }
-  if (chunk == 0) chunk = n ? n : 1;
-  for (uint64_t o = 0; o < n && !d.destroyed; o += chunk) {
-    uint64_t l = n - o < chunk ? n - o : chunk;
+  /* one _write per piece; sizes are cycled (a 0 entry means "the rest of the batch") */
+  for (uint64_t o = 0, k = 0; o < n && !d.destroyed; k++) {
+    uint64_t want = sizes[k % nsizes];
+    uint64_t l = (want == 0 || n - o < want) ? n - o : want;
     dec_write(&d, bytes + o, l);
+    o += l;
   }
   uint64_t consumed = n, tail = DRP_TAIL_NONE, brem = 0;
   if (!d.destroyed) {
@@ -510,6 +510,35 @@ ORACLE_API int oracle_decode_batch(const uint8_t *bytes, uint64_t n, uint64_t ch
   out[7] = d.changes;
   out[8] = d.blobs;
   return d.overflow ? DRP_E_CAPACITY : DRP_OK;
+}
+
+/* Batch view used by the parity tests and the CPU baseline: feed bytes[0,n) in
+ * `chunk`-byte writes (0 = one write) starting with `blob_remaining` bytes of an open
+ * blob, and report SoA frames + tail exactly as drp_decode_batch does. */
+ORACLE_API int oracle_decode_batch(const uint8_t *bytes, uint64_t n, uint64_t chunk,
+                                   uint64_t blob_remaining, uint64_t cap, uint64_t *payload_off,
+                                   uint32_t *plen, uint8_t *type, uint32_t *key_off,
+                                   uint32_t *key_len, uint32_t *subset_off, uint32_t *subset_len,
+                                   uint32_t *value_off, uint32_t *value_len, uint64_t *change,
+                                   uint64_t *from, uint64_t *to, uint8_t *flags, uint64_t *out) {
+  return decode_writes(bytes, n, &chunk, 1, blob_remaining, cap, payload_off, plen, type, key_off,
+                       key_len, subset_off, subset_len, value_off, value_len, change, from, to, flags,
+                       out);
+}
+
+/* The same with an explicit list of write sizes (cycled; 0 = the rest): a stream written the
+ * way a fixture of the reference was (tests/golden/ref_framing.json). */
+ORACLE_API int oracle_decode_writes(const uint8_t *bytes, uint64_t n, const uint64_t *sizes,
+                                    uint64_t nsizes, uint64_t blob_remaining, uint64_t cap,
+                                    uint64_t *payload_off, uint32_t *plen, uint8_t *type,
+                                    uint32_t *key_off, uint32_t *key_len, uint32_t *subset_off,
+                                    uint32_t *subset_len, uint32_t *value_off, uint32_t *value_len,
+                                    uint64_t *change, uint64_t *from, uint64_t *to, uint8_t *flags,
+                                    uint64_t *out) {
+  if (!sizes || !nsizes) return DRP_E_INVAL;
+  return decode_writes(bytes, n, sizes, nsizes, blob_remaining, cap, payload_off, plen, type,
+                       key_off, key_len, subset_off, subset_len, value_off, value_len, change, from,
+                       to, flags, out);
 }
 
 ORACLE_API uint64_t oracle_change_struct_size(void) { return sizeof(oracle_change); }

@@ -34,6 +34,9 @@ def lib():
         _lib.oracle_decode_batch.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64,
                                              C.c_uint64] + [C.c_void_p] * 14
         _lib.oracle_decode_batch.restype = C.c_int
+        _lib.oracle_decode_writes.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64,
+                                              C.c_uint64] + [C.c_void_p] * 14
+        _lib.oracle_decode_writes.restype = C.c_int
     return _lib
 
 
@@ -77,8 +80,9 @@ def alloc_outputs(cap):
     return o
 
 
-def decode_batch(wire, chunk=0, blob_remaining=0, cap=None, outs=None):
-    """Run the decode.js restatement over `wire` written in `chunk`-byte pieces."""
+def decode_batch(wire, chunk=0, blob_remaining=0, cap=None, outs=None, writes=None):
+    """Run the decode.js restatement over `wire` written in `chunk`-byte pieces (or in the
+    cycled list of piece sizes `writes`, 0 = the rest)."""
     if outs is not None:
         cap = len(outs["type"])
     if cap is None:
@@ -87,11 +91,14 @@ def decode_batch(wire, chunk=0, blob_remaining=0, cap=None, outs=None):
     o = outs if outs is not None else alloc_outputs(cap)
     meta = np.zeros(9, np.uint64)
     p = lambda a: a.ctypes.data_as(C.c_void_p)
-    rc = lib().oracle_decode_batch(p(w), len(wire), chunk, blob_remaining, cap, p(o["payload_off"]),
-                                   p(o["payload_len"]), p(o["type"]), p(o["key_off"]),
-                                   p(o["key_len"]), p(o["subset_off"]), p(o["subset_len"]),
-                                   p(o["value_off"]), p(o["value_len"]), p(o["change"]),
-                                   p(o["from"]), p(o["to"]), p(o["flags"]), p(meta))
+    cols = [p(o["payload_off"]), p(o["payload_len"]), p(o["type"]), p(o["key_off"]), p(o["key_len"]),
+            p(o["subset_off"]), p(o["subset_len"]), p(o["value_off"]), p(o["value_len"]), p(o["change"]),
+            p(o["from"]), p(o["to"]), p(o["flags"]), p(meta)]
+    if writes is not None:
+        ws = np.ascontiguousarray(writes, dtype=np.uint64)
+        rc = lib().oracle_decode_writes(p(w), len(wire), p(ws), len(ws), blob_remaining, cap, *cols)
+    else:
+        rc = lib().oracle_decode_batch(p(w), len(wire), chunk, blob_remaining, cap, *cols)
     assert rc == 0, rc
     n = int(meta[0])
     # a malformed Change (err 4/5) stays in the table at index err_frame

@@ -1,5 +1,5 @@
 """Synthetic replication streams shaped like BASELINE.json's configs (seeded)."""
-import random  # noqa: F401  (callers pass random.Random instances)
+import random
 
 import numpy as np
 
@@ -91,3 +91,53 @@ def c3_stream(rng, units, frames_per_unit=1000, blob_len=1 << 20, seed=3):
         out.append(c2_stream(frames_per_unit, seed=seed + u, start=u * frames_per_unit).tobytes())
         out.append(frame(rng.randbytes(blob_len), 2))
     return b"".join(out)
+
+
+C1_ALPHABET = b"abcdefghijklmnopqrstuvwxyz0123456789"
+
+
+def c1_changes(n=10000, seed=11):
+    """C1: n Changes, key 32 random [a-z0-9] chars, change=i+1, from=i, to=i+1,
+    value 64 random bytes (seeded)."""
+    rng = np.random.default_rng(seed)
+    keys = rng.integers(0, len(C1_ALPHABET), size=(n, 32))
+    vals = rng.integers(0, 256, size=(n, 64), dtype=np.uint8)
+    alpha = np.frombuffer(C1_ALPHABET, np.uint8)
+    return [{"key": alpha[keys[i]].tobytes().decode(), "change": i + 1, "from": i, "to": i + 1,
+             "value": vals[i].tobytes()} for i in range(n)]
+
+
+C1_BLOB = b"hello world\n"
+
+
+def c1_ops(n=10000, blob_after=5000, seed=11):
+    """The C1 encoder call sequence: changes 0..blob_after-1, then e.blob(12) written with
+    "hello world\\n" and ended, then the remaining changes (issued while the blob is still
+    open, so encode.js:104-107 queues them behind it)."""
+    ch = c1_changes(n, seed)
+    ops = [dict(op="change", **c) for c in ch[:blob_after]]
+    ops.append({"op": "blob", "len": len(C1_BLOB), "writes": [C1_BLOB]})
+    ops += [dict(op="change", **c) for c in ch[blob_after:]]
+    ops.append({"op": "finalize"})
+    return ops
+
+
+def c3_edge_stream(j, blob_len=70000, tail_frames=40, seed=21):
+    """A C2 prefix padded so that a blob header (3-byte varint + id) starts j bytes before the
+    64 KiB write edge, then the blob payload and more C2 frames (C3's chunk-edge case)."""
+    pre = c2_stream(760, seed=seed).tobytes()  # 65360 bytes
+    target = 65536 - j - len(pre)
+    # a change frame of exactly `target` bytes: 2 header bytes + key/number fields + value
+    vlen = target
+    while len(frame(change_payload(b"pad", 1, 2, 3, value=bytes(vlen)))) > target:
+        vlen -= 1
+    pad = frame(change_payload(b"pad", 1, 2, 3, value=(bytes(range(256)) * (vlen // 256 + 1))[:vlen]))
+    assert len(pad) == target, (len(pad), target)
+    rng = np.random.default_rng(seed + j)
+    blob = frame(rng.integers(0, 256, size=blob_len, dtype=np.uint8).tobytes(), 2)
+    return pre + pad + blob + c2_stream(tail_frames, seed=seed + 100, start=760).tobytes()
+
+
+def random_stream_seeded(seed, nframes):
+    """random_stream with a fresh seeded generator (fixture recipes)."""
+    return random_stream(random.Random(seed), nframes, blob_p=0.05, blob_max=5000, subset_p=0.2)

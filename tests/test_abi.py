@@ -38,7 +38,8 @@ def test_binding_matches_header():
     sys.path.insert(0, os.path.join(ROOT, "dat-replication-protocol_amd", "python"))
     import drp_amd
     assert sorted(drp_amd.EXPORTS) == declared()
-    assert drp_amd.lib().drp_abi_version() == 1
+    want = int(re.search(r"#define DRP_ABI_VERSION (\d+)", open(HDR).read()).group(1))
+    assert drp_amd.lib().drp_abi_version() == want
 
 
 def test_open_without_gpu_fails_cleanly():

@@ -29,7 +29,7 @@ def test_package_loads_without_gpu_use():
             % (os.path.join(ROOT, "dat-replication-protocol_amd"),
                os.path.join(ROOT, "dat-replication-protocol_amd", "lib", "drp.node")))
     out = json.loads(subprocess.check_output([NODE, "-e", code], text=True, timeout=60))
-    assert out == ["function", "function", ["abiVersion", "decode", "encode", "open"], 1]
+    assert out == ["function", "function", ["abiVersion", "decode", "encode", "open"], 2]
 
 
 def oracle_events(wire):
