@@ -91,11 +91,41 @@ def verify_c2(o, res, nframes, dev):
     assert not bad, f"decoded columns differ from the generator: {bad}"
 
 
-def cpu_baseline(min_seconds=10.0, sample_frames=2_000_000):
-    """The C restatement of decode.js (oracle/, 1 thread) over a C2 sample in 64 KiB writes."""
+def host_cores():
+    """Cores this process may use: the box's CPU share (OMP_NUM_THREADS is set to it there),
+    never more than the affinity mask."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    want = int(os.environ.get("OMP_NUM_THREADS") or avail)
+    return max(1, min(want, avail))
+
+
+def calibration(port_frames_per_s):
+    """BASELINE.md "Calibration": the reference JS (decode.js in place) over the C restatement,
+    both timed on one core of the build container (profiles/calibration_ref_js.json, from
+    scripts/calibrate_reference.py); applied to the port's rate on this host it estimates what
+    the reference itself would decode here (it cannot run on the GPU box)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "calibration_ref_js.json")) as f:
+            c = json.load(f)
+    except (OSError, ValueError):
+        return None
+    r = c["ratio_ref_js_over_port"]
+    return {"ratio_ref_js_over_port": r, "reference_js_equiv_frames_per_s": port_frames_per_s * r,
+            "measured": {"reference_js_frames_per_s": c["reference_js"]["frames_per_s"],
+                         "port_frames_per_s": c["port_c"]["frames_per_s"], "where": "build container, 1 core",
+                         "workload": c["workload"]}}
+
+
+def _oracle_modules():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
     import _streams as S
+    return O, S
+
+
+def cpu_baseline(min_seconds=10.0, sample_frames=2_000_000):
+    """The C restatement of decode.js (oracle/, 1 thread) over a C2 sample in 64 KiB writes."""
+    O, S = _oracle_modules()
     wire = S.c2_stream(sample_frames, seed=7).tobytes()
     outs = O.alloc_outputs(sample_frames + 16)
     O.decode_batch(wire, chunk=65536, outs=outs)
@@ -105,11 +135,96 @@ def cpu_baseline(min_seconds=10.0, sample_frames=2_000_000):
         assert r["nframes"] == sample_frames
         reps += 1
     dt = time.perf_counter() - t0
-    return {"value": reps * sample_frames / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+    v = reps * sample_frames / dt
+    return {"value": v, "unit": "frames/s", "cores": 1, "kind": "port",
             "wire_GBps": reps * len(wire) / dt / 1e9,
             "sample": f"C2 sample of {sample_frames} frames ({len(wire)} B) decoded {reps}x in 64 KiB "
                       f"writes by oracle/drp_oracle.c (decode.js + protocol-buffers@2 restatement), "
-                      f"{dt:.1f} s on 1 host core"}
+                      f"{dt:.1f} s on 1 host core",
+            "calibration": calibration(v)}
+
+
+def cpu_baseline_streams(min_seconds=10.0, streams_per_core=2, seed=4):
+    """C4 on every host core (BASELINE.md plan): one thread per core, each decoding its own
+    independent C4 streams (U[8192,16384] C2 frames) with the C restatement in 64 KiB writes
+    (ctypes releases the GIL, so the threads run in parallel)."""
+    import threading
+    O, S = _oracle_modules()
+    cores = host_cores()
+    rng = np.random.default_rng(seed)
+    counts = rng.integers(8192, 16385, size=cores * streams_per_core)
+    work = [[S.c2_stream(int(n), seed=seed * 1000 + k).tobytes()
+             for k, n in enumerate(counts[c * streams_per_core:(c + 1) * streams_per_core])] for c in range(cores)]
+    done = [0] * cores
+    t_end = [0.0]
+
+    def run(c):
+        outs = O.alloc_outputs(16385 + 16)
+        while time.perf_counter() < t_end[0]:
+            for w in work[c]:
+                r = O.decode_batch(w, chunk=65536, outs=outs)
+                done[c] += r["nframes"]
+
+    t0 = time.perf_counter()
+    t_end[0] = t0 + min_seconds
+    ts = [threading.Thread(target=run, args=(c,)) for c in range(cores)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dt = time.perf_counter() - t0
+    v = sum(done) / dt
+    return {"value": v, "unit": "frames/s", "cores": cores, "kind": "port",
+            "wire_GBps": v * FRAME / 1e9,
+            "sample": f"C4 sample: {len(counts)} independent streams of U[8192,16384] C2 frames, "
+                      f"{streams_per_core} per thread, {cores} threads, decoded repeatedly in 64 KiB writes "
+                      f"by oracle/drp_oracle.c for {dt:.1f} s",
+            "calibration": calibration(v / cores)}
+
+
+def cpu_baseline_c5(min_seconds=10.0, rows_per_core=4000, seed=55):
+    """C5 round trip on every host core: each thread encodes its own C5-shaped rows (4096 B
+    values, key U[1,256], change/from/to U[0,2^32)) with the C restatement of encode.js +
+    protocol-buffers@2 and decodes the wire back in 64 KiB writes."""
+    import threading
+    O, S = _oracle_modules()
+    cores = host_cores()
+    rng = np.random.default_rng(seed)
+    jobs = []
+    for c in range(cores):
+        kl = rng.integers(1, 257, size=rows_per_core).astype(np.uint32)
+        row = kl.astype(np.uint64) + C5_VALUE
+        ko = np.cumsum(row) - row
+        heap = rng.integers(0, 256, size=int(row.sum()), dtype=np.uint8).tobytes()
+        nums = rng.integers(0, 1 << 32, size=(3, rows_per_core), dtype=np.uint64)
+        cols = {"key_off": ko.astype(np.uint64), "key_len": kl, "subset_off": np.zeros(rows_per_core, np.uint64),
+                "subset_len": np.zeros(rows_per_core, np.uint32), "value_off": (ko + kl).astype(np.uint64),
+                "value_len": np.full(rows_per_core, C5_VALUE, np.uint32), "change": nums[0], "from": nums[1],
+                "to": nums[2], "flags": np.full(rows_per_core, 2, np.uint8)}
+        jobs.append((heap, cols))
+    done = [0] * cores
+    t_end = [0.0]
+
+    def run(c):
+        heap, cols = jobs[c]
+        outs = O.alloc_outputs(rows_per_core + 16)
+        while time.perf_counter() < t_end[0]:
+            wire = O.encode_changes(heap, cols)
+            r = O.decode_batch(wire, chunk=65536, outs=outs)
+            assert r["nframes"] == rows_per_core
+            done[c] += rows_per_core
+
+    t0 = time.perf_counter()
+    t_end[0] = t0 + min_seconds
+    ts = [threading.Thread(target=run, args=(c,)) for c in range(cores)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dt = time.perf_counter() - t0
+    return {"value": sum(done) / dt, "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"C5 sample: {rows_per_core} rows per thread, {cores} threads, encode -> decode "
+                      f"(64 KiB writes) by oracle/drp_oracle.c repeatedly for {dt:.1f} s"}
 
 
 def h2d_rate(dev, nbytes=1 << 30):
@@ -274,6 +389,8 @@ def main_c5(args, dev):
         "decode": {"ms": d * 1e3, "GBps": b_dec / d / 1e9, "frac": b_dec / d / 1e9 / HBM_PEAK_GBPS,
                    "exact_fallbacks": ctx.timing().strict_reruns, "repair_passes": ctx.timing().spec_repairs},
     }
+    if not args.no_cpu:
+        out_line["cpu_baseline"] = cpu_baseline_c5()
     print(json.dumps(out_line), flush=True)
     ctx.close()
 
@@ -293,7 +410,20 @@ def main():
                     "several ranks on one GPU")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: re-launch under torch.distributed.run before anything touches
+        # the GPU (this process never initialises HIP), and exit with its status
+        import socket
+        import subprocess
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
@@ -382,15 +512,17 @@ def main():
     exact = os.environ.get("DRP_DECODE") == "exact"
     kname = (f"decode_tiles<{tile // 64}>" if exact else
              "speculative decode: spec_claims + verify_counts + tile scans + emit_tiles")
+    gather = "; RCCL all-gather of 32 B stream stats + index scan" if dist else "; no collective (1 GPU)"
     if args.workload == "c2":
-        workload = {"workload": "C2: 100M Change frames x 86 B (64 B values), one 8.6 GB stream per GPU",
+        workload = {"workload": f"C2: {nframes / 1e6:g}M Change frames x 86 B (64 B values), one "
+                                f"{nframes * FRAME / 1e9:.2f} GB stream per GPU",
                     "frames_per_gpu": nframes, "wire_bytes_per_gpu": nframes * FRAME,
-                    "parallelism": f"replicas: one stream per GPU, {world} GPU(s); RCCL all-gather of stream stats"}
+                    "parallelism": f"replicas: one stream per GPU, {world} GPU(s){gather}"}
     else:
         workload = {"workload": f"C4: {nstreams_total} independent streams of U[8192,16384] C2 frames, "
                                 f"contiguous shards over {world} GPU(s)",
                     "frames_node": frames_node, "streams": nstreams_total,
-                    "parallelism": f"stream shards, {world} GPU(s); RCCL all-gather of 32 B stream stats + index scan"}
+                    "parallelism": f"stream shards, {world} GPU(s){gather}"}
     workload["tile_bytes"] = tile
 
     if rank == 0:
@@ -418,7 +550,11 @@ def main():
             "step_ms_hip_events": ev_ms / args.steps,
         }
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline()
+            if args.workload == "c2":
+                out["cpu_baseline"] = cpu_baseline()
+                out["cpu_baseline_all_cores"] = cpu_baseline_streams()
+            else:
+                out["cpu_baseline"] = cpu_baseline_streams()
             out["h2d"] = h2d_rate(dev)
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -7,7 +7,7 @@
 - an entry that is none of the keys Y_{t-1}: a blob longer than a tile lands in the middle of
   a later tile, so phase 2 walks that tile serially;
 - mixtures of the above with ordinary Change frames, cut at arbitrary points.
-Each is compared bit-exact with the oracle at both tile sizes.
+Each is compared bit-exact with the oracle on both decode paths.
 """
 import random
 
@@ -53,13 +53,18 @@ def _cases():
 CASES = list(_cases())
 
 
-@pytest.mark.parametrize("tile", [4096, 8192])
+@pytest.mark.parametrize("kernel", ["speculative", "exact4096", "exact8192"])
 @pytest.mark.parametrize("name", [n for n, _ in CASES])
-def test_adversarial(ctx, tile, name):
+def test_adversarial(ctx, kernel, name):
+    """The default path (speculate, repair, fall back) and the exact kernel at both of its
+    tile sizes (the speculative kernels have one fixed 8 KiB tile)."""
     from _gpu import assert_same
     wire = dict(CASES)[name]
-    ctx.set_tile(tile)
+    if kernel != "speculative":
+        ctx.set_exact(True)
+        ctx.set_tile(int(kernel[5:]))
     try:
-        assert_same(ctx.decode_batch(wire), O.decode_batch(wire), f"{name}/tile{tile}")
+        assert_same(ctx.decode_batch(wire), O.decode_batch(wire), f"{name}/{kernel}")
     finally:
         ctx.set_tile(0)
+        ctx.set_exact(False)

@@ -106,27 +106,21 @@ def test_errors_and_tails(ctx, seed):
 
 
 def test_batches_with_carry(ctx):
-    """Split a stream into batches at random points and carry state like the JS layer."""
+    """Split a stream into batches at random points and carry state like the JS layer; every
+    frame's offset, length, type and Change columns equal the oracle's one-write decode."""
+    from _gpu import COL_KEYS, stream_decode
     rng = random.Random(21)
     wire = S.random_stream(rng, 2000, blob_p=0.1, blob_max=5000)
     ref = O.decode_batch(wire)
-    pos, carry_bytes, blob_rem = 0, b"", 0
-    frames = []
-    while pos < len(wire):
-        step = rng.choice([1, 7, 100, 4096, 30000])
-        chunk = wire[pos:pos + step]
-        batch = carry_bytes + chunk
-        base = pos - len(carry_bytes)
-        g = ctx.decode_batch(batch, blob_remaining=blob_rem)
-        assert g["err_code"] == 0
-        for k in range(g["nframes"]):
-            frames.append((int(g["type"][k]) & 0x7F, base + int(g["payload_off"][k])))
-        carry_bytes = batch[g["consumed"]:] if g["tail"] in (1, 2) else b""
-        blob_rem = g["blob_remaining"]
-        pos += len(chunk)
-    merged = [(t & 0x3F, o) for t, o in frames if not (t & 0x40)]
-    exp = [(int(t) & 0x3F, int(o)) for t, o in zip(ref["type"], ref["payload_off"])]
-    assert merged == exp
+    frames, err = stream_decode(ctx, wire, [rng.choice([1, 7, 100, 4096, 30000]) for _ in range(4000)])
+    assert err is None
+    got = [f for f in frames if not (f["type"] & 0x40)]  # blob continuations merge into their blob
+    assert len(got) == ref["nframes"]
+    for k, f in enumerate(got):
+        assert (f["type"] & 0x3F, f["off"], f["len"]) == \
+            (int(ref["type"][k]) & 0x3F, int(ref["payload_off"][k]), int(ref["payload_len"][k])), k
+        if f["type"] & 0x3F == 1:
+            assert [f[c] for c in COL_KEYS] == [int(ref[c][k]) for c in COL_KEYS], k
 
 
 def _random_cols(rng, n):
@@ -255,3 +249,29 @@ def test_repair_path_c5(ctx):
     bench.verify_c5(cols, heap, wire, outs, res, n, dev, samples=64)
     assert t.strict_reruns == 0
     assert t.spec_repairs > 0, "no tile missed: this test no longer exercises the repair path"
+
+
+def test_encode_rejects_out_of_range_rows(ctx):
+    """A row whose key/subset/value range leaves the heap is DRP_E_INVAL, not a device fault
+    (drp.h: every call returns a code)."""
+    from _gpu import drp_amd
+    heap, c = _random_cols(random.Random(4), 50)
+    for col, bad in [("key_off", len(heap) + 1), ("value_len", 1 << 31), ("subset_off", 2**64 - 2)]:
+        cc = {k: v.copy() for k, v in c.items()}
+        if col == "subset_off":
+            cc["flags"][17] |= 1
+        cc[col][17] = bad
+        with pytest.raises(drp_amd.DrpError) as e:
+            ctx.encode_batch(heap, cc)
+        assert e.value.rc == drp_amd.DRP_E_INVAL, col
+    assert ctx.encode_batch(heap, c) == O.encode_changes(heap, c)  # the context is still usable
+
+
+def test_encode_max_width_varints(ctx):
+    """change/from/to at 2^64 - 1 (10-byte varints) beside a value: 39 bytes of field prefixes
+    in one frame, equal to the oracle's encoding (the C ABI takes any uint64)."""
+    heap, c = _random_cols(random.Random(5), 64)
+    for k in ["change", "from", "to"]:
+        c[k][:] = np.uint64(2**64 - 1)
+    c["flags"][:] |= 2
+    assert ctx.encode_batch(heap, c) == O.encode_changes(heap, c)

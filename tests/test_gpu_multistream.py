@@ -38,13 +38,17 @@ def _streams(rng, n):
     return out
 
 
-@pytest.mark.parametrize("tile", [4096, 8192])
-def test_many_streams(tile):
+@pytest.mark.parametrize("kernel", ["speculative", "exact4096", "exact8192"])
+def test_many_streams(kernel):
+    """300 streams in one call, on the default path and on the exact kernel at both tile sizes
+    (the exact kernel's cross-tile look-back over many short streams: the wait cycle fixed in
+    round 1 commit 3651cbd)."""
     import torch
 
     import drp_amd
     import drp_dist
 
+    tile = 8192 if kernel == "speculative" else int(kernel[5:])
     rng = random.Random(7 + tile)
     streams = _streams(rng, 300)
     # a blob continuation at the front of some streams: decode from `entry`
@@ -71,6 +75,8 @@ def test_many_streams(tile):
     rs = C.sizeof(drp_amd.StreamResult)
     res_t = torch.zeros(len(streams) * rs, dtype=torch.uint8, device=dev)
     with drp_amd.Ctx(0, tile=tile) as ctx:
+        if kernel != "speculative":
+            ctx.set_exact(True)
         ctx.decode_device(wire_t, so_t, en_t, outs, cap, res_t)
         stats = drp_dist.local_stats_device(ctx, res_t, so_t)
         base = drp_dist.global_index_device(ctx, stats)
