@@ -256,10 +256,9 @@ def test_encode_rejects_out_of_range_rows(ctx):
     (drp.h: every call returns a code)."""
     from _gpu import drp_amd
     heap, c = _random_cols(random.Random(4), 50)
-    for col, bad in [("key_off", len(heap) + 1), ("value_len", 1 << 31), ("subset_off", 2**64 - 2)]:
+    for col, bad in [("key_off", len(heap) + 1), ("value_len", len(heap) + 1), ("subset_off", 2**64 - 2)]:
         cc = {k: v.copy() for k, v in c.items()}
-        if col == "subset_off":
-            cc["flags"][17] |= 1
+        cc["flags"][17] |= 3  # subset and value present: their ranges are checked
         cc[col][17] = bad
         with pytest.raises(drp_amd.DrpError) as e:
             ctx.encode_batch(heap, cc)
