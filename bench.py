@@ -227,6 +227,36 @@ def cpu_baseline_c5(min_seconds=10.0, rows_per_core=4000, seed=55):
                       f"(64 KiB writes) by oracle/drp_oracle.c repeatedly for {dt:.1f} s"}
 
 
+def node_path(frames=4_000_000, reps=3):
+    """The product path (north_star: Node host over the N-API addon) on a C2 sample: the
+    package's Decoder fed 64 KiB writes (coalesced per event-loop turn, up to 64 MiB per GPU
+    call) and 256 MiB writes (one GPU call each), with no-op change callbacks. Reported apart
+    from the kernel number: it includes H2D, the D2H of the columns and the per-frame JS replay
+    (building each {subset,key,change,from,to,value} object)."""
+    import shutil
+    import subprocess
+    import tempfile
+    node = shutil.which("node")
+    if node is None:
+        return {"skipped": "node not installed on this host"}
+    _, S = _oracle_modules()
+    wire = S.c2_stream(frames, seed=9).tobytes()
+    out = {"workload": f"C2 sample, {frames} frames x 86 B, change callbacks acknowledged synchronously"}
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(wire)
+        path = f.name
+    try:
+        for name, write, batch in [("writes_64KiB", 65536, 64 << 20), ("writes_256MiB", 256 << 20, 256 << 20)]:
+            env = dict(os.environ, DRP_MAX_BATCH=str(batch))
+            r = subprocess.run([node, os.path.join(ROOT, "scripts", "bench_node.js"), path, str(write), str(reps)],
+                               env=env, capture_output=True, text=True, timeout=600)
+            out[name] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+                {"error": (r.stderr or r.stdout)[-400:]}
+    finally:
+        os.unlink(path)
+    return out
+
+
 def h2d_rate(dev, nbytes=1 << 30):
     """Pinned host -> HBM copy rate for one batch (reported separately, never `value`)."""
     h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
@@ -556,6 +586,8 @@ def main():
             else:
                 out["cpu_baseline"] = cpu_baseline_streams()
             out["h2d"] = h2d_rate(dev)
+            if args.workload == "c2":
+                out["node_path"] = node_path()
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:

@@ -81,8 +81,19 @@ struct drp_ctx {
   int cus = 256;
   uint32_t waves_per_cu = 16;
   DevBuf scratch, in_stage, out_stage, aux;
+  DevBuf dec_cols;  // device columns of the staged host-batch decode (drp_decode_stage)
   drp_timing timing = {};
   std::vector<uint64_t> host_tmp;
+  // the staged host-batch decode: row 0 is a host-built blob continuation when nf0 == 1; GPU
+  // rows follow, their payload_off relative to batch offset `shift` (where staging started)
+  struct Staged {
+    uint64_t rows = 0, nf0 = 0, shift = 0, cap = 0;
+    uint64_t off0 = 0;
+    uint32_t len0 = 0;
+    uint8_t ty0 = 0;
+    drp_frames fr = {};
+    drp_changes co = {};
+  } staged;
 };
 
 #define CHK(x)                                                                     \
@@ -556,13 +567,14 @@ int drp_decode_device(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const u
   return run_decode(c, bytes, nbytes, stream_off, entry, nstreams, frames, cols, cap, results);
 }
 
-int drp_decode_batch(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *carry, const drp_frames *frames,
-                     const drp_changes *cols, uint64_t cap, uint64_t *n_frames, uint64_t *err_frame,
-                     uint32_t *err_code, uint32_t *err_detail) {
-  if (!c || !carry || !frames || !cols || !n_frames || !err_frame || !err_code || !err_detail) return DRP_E_INVAL;
-  if (!bytes && n) return DRP_E_INVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
-  const bool out_dev = is_device_ptr(frames->payload_off);
+// drp_decode_batch into caller-owned DEVICE columns: the whole batch is staged and decoded in place.
+static int decode_batch_device_out(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *carry,
+                                   const drp_frames *frames, const drp_changes *cols, uint64_t cap,
+                                   uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code,
+                                   uint32_t *err_detail) {
+  const bool out_dev = true;
+  carry->frame_bytes = 0;
+  c->staged.rows = 0;
   hipStream_t st = c->st;
   *err_frame = ~0ull;
   *err_code = DRP_ERR_NONE;
@@ -668,7 +680,157 @@ int drp_decode_batch(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *ca
   carry->blob_remaining = r.blob_remaining;
   carry->consumed = r.consumed;
   carry->tail_kind = r.tail_kind;
+  carry->frame_bytes = r.tail_kind == DRP_TAIL_CHANGE ? r.tail_frame_bytes : 0;
   return rc;
+}
+
+
+// Decode a host batch (bytes [a, n), a = the 16-byte-aligned start of the bytes after a leading
+// blob continuation) into the ctx's device columns. The frame capacity starts at a guess and is
+// grown to the exact count when the first launch overflows it (the count is exact either way).
+static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *carry, uint64_t *n_frames,
+                        uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail) {
+  hipStream_t st = c->st;
+  auto &S = c->staged;
+  S.rows = S.nf0 = S.shift = 0;
+  *err_frame = ~0ull;
+  *err_code = DRP_ERR_NONE;
+  *err_detail = 0;
+  carry->frame_bytes = 0;
+  const uint64_t brem = carry->blob_remaining;
+  // A blob continuation (decode.js _id == 2 with _missing > 0 across _write calls) is row 0.
+  if (brem) {
+    S.nf0 = 1;
+    S.off0 = 0;
+    S.len0 = brem > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)brem;
+    S.ty0 = DRP_TYPE_BLOB | DRP_FRAME_CONT | (brem > n ? DRP_FRAME_PARTIAL : 0);
+    if (brem >= n) {
+      carry->blob_remaining = brem - n;
+      carry->consumed = n;
+      carry->tail_kind = carry->blob_remaining ? DRP_TAIL_BLOB : DRP_TAIL_NONE;
+      *n_frames = 1;
+      S.rows = 1;
+      return DRP_OK;
+    }
+  }
+  // the continuation's payload bytes are pass-through: only [a, n) goes to the device
+  const uint64_t a = brem & ~15ull, m = n - a;
+  const uint8_t *dbytes = bytes + a;
+  if (!is_device_ptr(bytes) || ((uintptr_t)bytes & 15)) {
+    if (!c->in_stage.ensure(m + 64)) return DRP_E_NOMEM;
+    if (m) CHK(hipMemcpyAsync(c->in_stage.p, bytes + a, m, hipMemcpyDefault, st));
+    dbytes = (const uint8_t *)c->in_stage.p;
+  }
+  const size_t stage_meta = 256;
+  if (!c->aux.ensure(stage_meta + sizeof(drp_stream_result) + 64)) return DRP_E_NOMEM;
+  uint64_t *soff = c->aux.at<uint64_t>(0);
+  uint64_t *ent = c->aux.at<uint64_t>(16);
+  drp_stream_result *dres = c->aux.at<drp_stream_result>(stage_meta);
+  uint64_t hv[3] = {0, m, brem - a};
+  CHK(hipMemcpyAsync(soff, hv, 16, hipMemcpyHostToDevice, st));
+  CHK(hipMemcpyAsync(ent, hv + 2, 8, hipMemcpyHostToDevice, st));
+  uint64_t cap = m / 32 + 1024;  // frames; grown below when the stream is denser
+  drp_stream_result r;
+  int rc = DRP_OK;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    if (!c->dec_cols.ensure(carve_bytes(cap))) return DRP_E_NOMEM;
+    carve(c->dec_cols, cap, S.fr, S.co);
+    S.cap = cap;
+    rc = run_decode(c, dbytes, m, soff, ent, 1, &S.fr, &S.co, cap, dres);
+    if (rc != DRP_OK && rc != DRP_E_CAPACITY) return rc;
+    CHK(hipMemcpyAsync(&r, dres, sizeof(r), hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+    if (rc == DRP_OK) break;
+    // the chain held more frames than the guess (frames past a malformed Change count too):
+    // retry at the bound, every delivered frame being at least 2 bytes
+    cap = m / 2 + 2;
+  }
+  if (rc != DRP_OK) return rc;
+  const uint64_t bad = (r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0;
+  S.shift = a;
+  S.rows = S.nf0 + r.frames + bad;
+  *n_frames = S.nf0 + r.frames;
+  if (r.err_code) {
+    *err_frame = S.nf0 + r.err_frame;
+    *err_code = r.err_code;
+    *err_detail = r.err_detail;
+  }
+  carry->blob_remaining = r.blob_remaining;
+  carry->consumed = r.consumed + a;
+  carry->tail_kind = r.tail_kind;
+  carry->frame_bytes = r.tail_kind == DRP_TAIL_CHANGE ? r.tail_frame_bytes : 0;
+  return DRP_OK;
+}
+
+// Copy staged rows [first, first + rows) into host columns.
+static int fetch_staged(drp_ctx *c, const drp_frames *frames, const drp_changes *cols, uint64_t first,
+                        uint64_t rows) {
+  auto &S = c->staged;
+  if (first > S.rows || rows > S.rows - first) return DRP_E_INVAL;
+  if (!rows) return DRP_OK;
+  hipStream_t st = c->st;
+  uint64_t dst = 0;  // destination row
+  if (first == 0 && S.nf0) {
+    frames->payload_off[0] = S.off0;
+    frames->payload_len[0] = S.len0;
+    frames->type[0] = S.ty0;
+    dst = 1;
+  }
+  const uint64_t g0 = first + dst - S.nf0;  // first GPU row
+  const uint64_t ng = rows - dst;
+  if (ng) {
+    auto cp = [&](void *d, const void *s_, size_t w) {
+      return hipMemcpyAsync(static_cast<char *>(d) + dst * w, static_cast<const char *>(s_) + g0 * w, ng * w,
+                            hipMemcpyDeviceToHost, st);
+    };
+    CHK(cp(frames->payload_off, S.fr.payload_off, 8));
+    CHK(cp(frames->payload_len, S.fr.payload_len, 4));
+    CHK(cp(frames->type, S.fr.type, 1));
+    CHK(cp(cols->key_off, S.co.key_off, 4));
+    CHK(cp(cols->key_len, S.co.key_len, 4));
+    CHK(cp(cols->subset_off, S.co.subset_off, 4));
+    CHK(cp(cols->subset_len, S.co.subset_len, 4));
+    CHK(cp(cols->value_off, S.co.value_off, 4));
+    CHK(cp(cols->value_len, S.co.value_len, 4));
+    CHK(cp(cols->change, S.co.change, 8));
+    CHK(cp(cols->from, S.co.from, 8));
+    CHK(cp(cols->to, S.co.to, 8));
+    CHK(cp(cols->flags, S.co.flags, 1));
+    CHK(hipStreamSynchronize(st));
+    if (S.shift)
+      for (uint64_t i = 0; i < ng; i++) frames->payload_off[dst + i] += S.shift;
+  }
+  return DRP_OK;
+}
+
+int drp_decode_stage(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *carry, uint64_t *n_frames,
+                     uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail) {
+  if (!c || !carry || !n_frames || !err_frame || !err_code || !err_detail || (!bytes && n)) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  return stage_decode(c, bytes, n, carry, n_frames, err_frame, err_code, err_detail);
+}
+
+int drp_decode_fetch(drp_ctx *c, const drp_frames *frames, const drp_changes *cols, uint64_t first, uint64_t rows) {
+  if (!c || !frames || !cols) return DRP_E_INVAL;
+  if (rows && (is_device_ptr(frames->payload_off) || is_device_ptr(cols->key_off))) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  return fetch_staged(c, frames, cols, first, rows);
+}
+
+int drp_decode_batch(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *carry, const drp_frames *frames,
+                     const drp_changes *cols, uint64_t cap, uint64_t *n_frames, uint64_t *err_frame,
+                     uint32_t *err_code, uint32_t *err_detail) {
+  if (!c || !carry || !frames || !cols || !n_frames || !err_frame || !err_code || !err_detail) return DRP_E_INVAL;
+  if (!bytes && n) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  if (is_device_ptr(frames->payload_off)) return decode_batch_device_out(c, bytes, n, carry, frames, cols, cap,
+                                                                         n_frames, err_frame, err_code, err_detail);
+  int rc = stage_decode(c, bytes, n, carry, n_frames, err_frame, err_code, err_detail);
+  if (rc != DRP_OK) return rc;
+  const uint64_t rows = c->staged.rows;
+  rc = fetch_staged(c, frames, cols, 0, rows < cap ? rows : cap);
+  if (rc != DRP_OK) return rc;
+  return rows > cap ? DRP_E_CAPACITY : DRP_OK;
 }
 
 int drp_encode_device(drp_ctx *c, const drp_change_src *src, const uint8_t *heap, uint64_t heap_bytes,

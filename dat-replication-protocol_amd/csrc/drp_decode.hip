@@ -1525,6 +1525,7 @@ __global__ void finalize_kernel(const uint8_t *bytes, const uint64_t *stream_off
   r.err_detail = 0;
   r.tail_kind = DRP_TAIL_NONE;
   r.reserved = 0;
+  r.tail_frame_bytes = 0;
   if (tf == tl) {
     r.frame_begin = (tf < ntiles) ? tile_base[tf]
                                   : (ntiles ? tile_base[ntiles - 1] + tile_count[ntiles - 1] : 0);
@@ -1541,7 +1542,11 @@ __global__ void finalize_kernel(const uint8_t *bytes, const uint64_t *stream_off
     Hdr h = parse_hdr_global(bytes, q, se);
     switch (h.kind) {
       case H_TAIL_HDR: r.tail_kind = DRP_TAIL_HEADER; r.consumed = q - so; break;
-      case H_TAIL_CHANGE: r.tail_kind = DRP_TAIL_CHANGE; r.consumed = q - so; break;
+      case H_TAIL_CHANGE:
+        r.tail_kind = DRP_TAIL_CHANGE;
+        r.consumed = q - so;
+        r.tail_frame_bytes = h.L > ~0ull - h.vlen ? ~0ull : h.vlen + h.L;  // (saturates)
+        break;
       case H_TAIL_BLOB:
         r.tail_kind = DRP_TAIL_BLOB;
         r.consumed = se - so;
@@ -1562,6 +1567,7 @@ __global__ void finalize_kernel(const uint8_t *bytes, const uint64_t *stream_off
     r.err_detail = 0;
     r.tail_kind = DRP_TAIL_NONE;
     r.blob_remaining = 0;
+    r.tail_frame_bytes = 0;
     r.consumed = se - so;
   }
   if (r.err_frame < frames) frames = r.err_frame;

@@ -2,18 +2,29 @@
  * drp_napi.c — thin N-API addon over libdrp's C ABI (include/drp.h).
  *
  * This is the binding a maintainer adds under the reference's streaming API: the JS
- * Decoder (decode.js in this package) hands each written chunk to decode(), which runs
- * the gfx950 frame split + Change decode and returns the frame table and Change columns;
- * the JS Encoder hands batches of Change rows to encode(). No CPU decode path exists:
- * if libdrp or the GPU is unavailable the calls throw.
+ * Decoder (decode.js in this package) hands coalesced writes to decode(), which runs the
+ * gfx950 frame split + Change decode and returns the frame table and Change columns; the JS
+ * Encoder hands batches of Change rows to encode(). No CPU decode path exists: if libdrp or
+ * the GPU is unavailable the calls fail.
  *
- *   open(device)                       -> ctx (external)
- *   decode(ctx, buf, blobRemaining)    -> {n, errFrame, errCode, errDetail, consumed,
- *                                          tailKind, blobRemaining, off, len, type, ko, kl,
- *                                          so, sl, vo, vl, change, from, to, flags}
- *   encode(ctx, heap, rows, cols...)   -> Buffer of wire bytes
+ * Threading: the GPU work of decode()/encode() runs on a libuv worker thread
+ * (napi_async_work); the result is delivered to the callback on the JS thread, where the JS
+ * layer replays the reference's callbacks. A context may be shared by several streams: its
+ * calls are serialised by a mutex (one HIP stream and one scratch set per device context).
+ *
+ *   open(device)                                 -> ctx (external)
+ *   decode(ctx, buf, blobRemaining, cb)          -> cb(err, {n, errFrame, errCode, errDetail,
+ *                                                   consumed, tailKind, blobRemaining, frameBytes,
+ *                                                   off, len, type, ko, kl, so, sl, vo, vl,
+ *                                                   change, from, to, flags})
+ *   decodeSync(ctx, buf, blobRemaining)          -> the same object (blocks the JS thread)
+ *   encode(ctx, heap, n, 10 column arrays, cb)   -> cb(err, Buffer of wire bytes)
+ *
+ * Host columns are sized from the decoded frame count (drp_decode_stage, then
+ * drp_decode_fetch), and handed to JS as external ArrayBuffers (no second copy).
  */
 #include <node_api.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -29,10 +40,18 @@
     }                                                               \
   } while (0)
 
+typedef struct {
+  drp_ctx *c;
+  pthread_mutex_t mu;
+} ctx_box;
+
 static void ctx_finalize(napi_env env, void *data, void *hint) {
   (void)env;
   (void)hint;
-  drp_close((drp_ctx *)data);
+  ctx_box *b = (ctx_box *)data;
+  drp_close(b->c);
+  pthread_mutex_destroy(&b->mu);
+  free(b);
 }
 
 static napi_value throw_rc(napi_env env, const char *what, int rc) {
@@ -40,6 +59,15 @@ static napi_value throw_rc(napi_env env, const char *what, int rc) {
   snprintf(msg, sizeof msg, "libdrp %s failed (%d)", what, rc);
   napi_throw_error(env, NULL, msg);
   return NULL;
+}
+
+static napi_value make_error(napi_env env, const char *what, int rc) {
+  char msg[128];
+  snprintf(msg, sizeof msg, "libdrp %s failed (%d)", what, rc);
+  napi_value m, e;
+  napi_create_string_utf8(env, msg, NAPI_AUTO_LENGTH, &m);
+  napi_create_error(env, NULL, m, &e);
+  return e;
 }
 
 static napi_value js_open(napi_env env, napi_callback_info info) {
@@ -51,17 +79,86 @@ static napi_value js_open(napi_env env, napi_callback_info info) {
   drp_ctx *c = NULL;
   int rc = drp_open(dev, &c);
   if (rc != DRP_OK) return throw_rc(env, "open", rc);
+  ctx_box *b = (ctx_box *)calloc(1, sizeof *b);
+  if (!b) {
+    drp_close(c);
+    napi_throw_error(env, NULL, "drp addon: out of memory");
+    return NULL;
+  }
+  b->c = c;
+  pthread_mutex_init(&b->mu, NULL);
   napi_value ext;
-  NAPI_CALL(env, napi_create_external(env, c, ctx_finalize, NULL, &ext));
+  NAPI_CALL(env, napi_create_external(env, b, ctx_finalize, NULL, &ext));
   return ext;
 }
 
-/* allocate an ArrayBuffer of n*size bytes and a typed array view over it */
-static napi_value make_ta(napi_env env, napi_typedarray_type ty, size_t n, size_t size, void **data) {
-  napi_value ab, ta;
-  if (napi_create_arraybuffer(env, (n * size) != 0 ? n * size : 8, data, &ab) != napi_ok) return NULL;
-  if (napi_create_typedarray(env, ty, n, ab, 0, &ta) != napi_ok) return NULL;
-  return ta;
+/* ---- decode ---------------------------------------------------------------------------- */
+
+enum { C_OFF, C_LEN, C_TYPE, C_KO, C_KL, C_SO, C_SL, C_VO, C_VL, C_CH, C_FR, C_TO, C_FL, NCOL };
+static const char *const COL_NAME[NCOL] = {"off", "len", "type", "ko", "kl", "so", "sl",
+                                           "vo", "vl", "change", "from", "to", "flags"};
+static const int COL_W[NCOL] = {8, 4, 1, 4, 4, 4, 4, 4, 4, 8, 8, 8, 1};
+static const napi_typedarray_type COL_T[NCOL] = {
+    napi_float64_array, napi_uint32_array, napi_uint8_array,   napi_uint32_array, napi_uint32_array,
+    napi_uint32_array,  napi_uint32_array, napi_uint32_array,  napi_uint32_array, napi_float64_array,
+    napi_float64_array, napi_float64_array, napi_uint8_array};
+
+typedef struct {
+  napi_async_work work;
+  napi_ref buf_ref, cb_ref;
+  ctx_box *box;
+  const uint8_t *bytes;
+  size_t n;
+  int rc;
+  uint64_t nf, ef, rows;
+  uint32_t ec, ed;
+  drp_carry carry;
+  void *col[NCOL];
+} dec_job;
+
+static void free_cols(void **col) {
+  for (int i = 0; i < NCOL; i++) {
+    free(col[i]);
+    col[i] = NULL;
+  }
+}
+
+/* the GPU part: decode, size the host columns from the frame count, fetch (worker thread) */
+static void dec_run(dec_job *j) {
+  pthread_mutex_lock(&j->box->mu);
+  j->rc = drp_decode_stage(j->box->c, j->bytes, j->n, &j->carry, &j->nf, &j->ef, &j->ec, &j->ed);
+  if (j->rc == DRP_OK) {
+    /* rows to expose: delivered frames plus a malformed Change (its flags say why) */
+    j->rows = j->nf + ((j->ec == DRP_ERR_CHANGE || j->ec == DRP_ERR_REQUIRED) ? 1 : 0);
+    for (int i = 0; i < NCOL; i++) {
+      j->col[i] = malloc(j->rows * COL_W[i] + 8);
+      if (!j->col[i]) j->rc = DRP_E_NOMEM;
+    }
+    if (j->rc == DRP_OK) {
+      drp_frames fr = {j->col[C_OFF], j->col[C_LEN], j->col[C_TYPE]};
+      drp_changes co = {j->col[C_KO], j->col[C_KL], j->col[C_SO], j->col[C_SL], j->col[C_VO],
+                        j->col[C_VL], j->col[C_CH], j->col[C_FR], j->col[C_TO], j->col[C_FL]};
+      j->rc = drp_decode_fetch(j->box->c, &fr, &co, 0, j->rows);
+    }
+  }
+  pthread_mutex_unlock(&j->box->mu);
+  if (j->rc != DRP_OK) {
+    free_cols(j->col);
+    return;
+  }
+  /* u64 -> JS Number, in place (varint.decode yields Numbers) */
+  const int conv[] = {C_OFF, C_CH, C_FR, C_TO};
+  for (size_t k = 0; k < sizeof conv / sizeof conv[0]; k++) {
+    uint64_t *u = (uint64_t *)j->col[conv[k]];
+    double *d = (double *)j->col[conv[k]];
+    for (uint64_t r = 0; r < j->rows; r++) d[r] = (double)u[r];
+  }
+}
+
+static void free_finalizer(napi_env env, void *data, void *hint) {
+  (void)env;
+  (void)hint;
+  free(data);
 }
 
 static void set_num(napi_env env, napi_value obj, const char *k, double v) {
@@ -70,165 +167,234 @@ static void set_num(napi_env env, napi_value obj, const char *k, double v) {
   napi_set_named_property(env, obj, k, x);
 }
 
-static napi_value js_decode(napi_env env, napi_callback_info info) {
-  size_t argc = 3;
-  napi_value argv[3];
-  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  if (argc < 2) {
-    napi_throw_type_error(env, NULL, "decode(ctx, buffer[, blobRemaining])");
-    return NULL;
+/* build the JS result object; the columns move into external ArrayBuffers (JS thread) */
+static napi_value dec_result(napi_env env, dec_job *j) {
+  napi_value res;
+  if (napi_create_object(env, &res) != napi_ok) return NULL;
+  set_num(env, res, "n", (double)j->nf);
+  set_num(env, res, "errFrame", j->ec ? (double)j->ef : -1);
+  set_num(env, res, "errCode", j->ec);
+  set_num(env, res, "errDetail", j->ed);
+  set_num(env, res, "consumed", (double)j->carry.consumed);
+  set_num(env, res, "tailKind", j->carry.tail_kind);
+  set_num(env, res, "blobRemaining", (double)j->carry.blob_remaining);
+  set_num(env, res, "frameBytes", (double)j->carry.frame_bytes);
+  for (int i = 0; i < NCOL; i++) {
+    napi_value ab, ta;
+    if (napi_create_external_arraybuffer(env, j->col[i], j->rows * COL_W[i] + 8, free_finalizer, NULL, &ab) !=
+        napi_ok)
+      return NULL;
+    j->col[i] = NULL; /* owned by the ArrayBuffer now */
+    if (napi_create_typedarray(env, COL_T[i], j->rows, ab, 0, &ta) != napi_ok) return NULL;
+    napi_set_named_property(env, res, COL_NAME[i], ta);
   }
-  drp_ctx *c = NULL;
-  NAPI_CALL(env, napi_get_value_external(env, argv[0], (void **)&c));
-  void *bytes = NULL;
-  size_t n = 0;
-  NAPI_CALL(env, napi_get_buffer_info(env, argv[1], &bytes, &n));
-  double brem = 0;
-  if (argc > 2) napi_get_value_double(env, argv[2], &brem);
-
-  const uint64_t cap = n / 2 + 2; /* a delivered frame is at least 2 bytes */
-  uint64_t *off = malloc(cap * 8);
-  uint32_t *len = malloc(cap * 4), *ko = malloc(cap * 4), *kl = malloc(cap * 4), *so = malloc(cap * 4),
-           *sl = malloc(cap * 4), *vo = malloc(cap * 4), *vl = malloc(cap * 4);
-  uint64_t *ch = malloc(cap * 8), *fr = malloc(cap * 8), *to = malloc(cap * 8);
-  uint8_t *ty = malloc(cap), *fl = malloc(cap);
-  if (!off || !len || !ko || !kl || !so || !sl || !vo || !vl || !ch || !fr || !to || !ty || !fl) {
-    napi_throw_error(env, NULL, "drp addon: out of memory");
-    return NULL;
-  }
-  drp_frames frames = {off, len, ty};
-  drp_changes cols = {ko, kl, so, sl, vo, vl, ch, fr, to, fl};
-  drp_carry carry = {(uint64_t)brem, 0, 0, 0};
-  uint64_t nf = 0, ef = 0;
-  uint32_t ec = 0, ed = 0;
-  int rc = drp_decode_batch(c, (const uint8_t *)bytes, n, &carry, &frames, &cols, cap, &nf, &ef, &ec, &ed);
-  napi_value res = NULL;
-  if (rc != DRP_OK) {
-    throw_rc(env, "decode", rc);
-    goto out;
-  }
-  {
-    /* rows to expose: delivered frames plus a malformed Change (its flags say why) */
-    uint64_t rows = nf + ((ec == DRP_ERR_CHANGE || ec == DRP_ERR_REQUIRED) ? 1 : 0);
-    if (rows > cap) rows = cap;
-    if (napi_create_object(env, &res) != napi_ok) goto out;
-    set_num(env, res, "n", (double)nf);
-    set_num(env, res, "errFrame", ec ? (double)ef : -1);
-    set_num(env, res, "errCode", ec);
-    set_num(env, res, "errDetail", ed);
-    set_num(env, res, "consumed", (double)carry.consumed);
-    set_num(env, res, "tailKind", carry.tail_kind);
-    set_num(env, res, "blobRemaining", (double)carry.blob_remaining);
-    struct {
-      const char *k;
-      napi_typedarray_type t;
-      void *src;
-      int w; /* 8: u64 -> f64, 4: u32, 1: u8 */
-    } cs[] = {{"off", napi_float64_array, off, 8}, {"len", napi_uint32_array, len, 4},
-              {"type", napi_uint8_array, ty, 1},   {"ko", napi_uint32_array, ko, 4},
-              {"kl", napi_uint32_array, kl, 4},    {"so", napi_uint32_array, so, 4},
-              {"sl", napi_uint32_array, sl, 4},    {"vo", napi_uint32_array, vo, 4},
-              {"vl", napi_uint32_array, vl, 4},    {"change", napi_float64_array, ch, 8},
-              {"from", napi_float64_array, fr, 8}, {"to", napi_float64_array, to, 8},
-              {"flags", napi_uint8_array, fl, 1}};
-    for (size_t i = 0; i < sizeof cs / sizeof cs[0]; i++) {
-      void *d = NULL;
-      napi_value ta = make_ta(env, cs[i].t, rows, cs[i].w, &d);
-      if (!ta) goto out;
-      if (cs[i].w == 8) {
-        double *dd = d;
-        const uint64_t *s = cs[i].src;
-        for (uint64_t r = 0; r < rows; r++) dd[r] = (double)s[r]; /* JS Numbers, as varint.decode */
-      } else if (rows) {
-        memcpy(d, cs[i].src, rows * cs[i].w);
-      }
-      napi_set_named_property(env, res, cs[i].k, ta);
-    }
-  }
-out:
-  free(off); free(len); free(ko); free(kl); free(so); free(sl); free(vo); free(vl);
-  free(ch); free(fr); free(to); free(ty); free(fl);
   return res;
 }
 
-/* encode(ctx, heap: Buffer, n, keyOff, keyLen, subsetOff, subsetLen, valueOff, valueLen,
- *        change, from, to, flags) — offsets/numbers as Float64Array, lengths Uint32Array,
- *        flags Uint8Array. Returns a Buffer with the wire bytes of n change frames. */
-static napi_value js_encode(napi_env env, napi_callback_info info) {
-  size_t argc = 13;
-  napi_value argv[13];
-  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  if (argc < 13) {
-    napi_throw_type_error(env, NULL, "encode(ctx, heap, n, 10 column arrays)");
+static void dec_execute(napi_env env, void *data) {
+  (void)env;
+  dec_run((dec_job *)data);
+}
+
+static void dec_complete(napi_env env, napi_status status, void *data) {
+  dec_job *j = (dec_job *)data;
+  napi_value cb, argv[2], undef;
+  napi_get_reference_value(env, j->cb_ref, &cb);
+  napi_get_undefined(env, &undef);
+  if (status != napi_ok || j->rc != DRP_OK) {
+    argv[0] = make_error(env, "decode", status != napi_ok ? DRP_E_INVAL : j->rc);
+    argv[1] = undef;
+  } else {
+    napi_get_null(env, &argv[0]);
+    argv[1] = dec_result(env, j);
+    if (!argv[1]) {
+      argv[0] = make_error(env, "decode (result)", DRP_E_NOMEM);
+      argv[1] = undef;
+    }
+  }
+  free_cols(j->col);
+  napi_delete_reference(env, j->buf_ref);
+  napi_delete_reference(env, j->cb_ref);
+  napi_delete_async_work(env, j->work);
+  free(j);
+  napi_call_function(env, undef, cb, 2, argv, NULL);
+}
+
+static dec_job *dec_args(napi_env env, napi_callback_info info, size_t want, napi_value *argv) {
+  size_t argc = want;
+  if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < want) {
+    napi_throw_type_error(env, NULL, want == 4 ? "decode(ctx, buffer, blobRemaining, cb)"
+                                               : "decodeSync(ctx, buffer, blobRemaining)");
     return NULL;
   }
-  drp_ctx *c = NULL;
-  NAPI_CALL(env, napi_get_value_external(env, argv[0], (void **)&c));
-  void *heap = NULL;
-  size_t heap_n = 0;
-  NAPI_CALL(env, napi_get_buffer_info(env, argv[1], &heap, &heap_n));
-  double nd = 0;
-  NAPI_CALL(env, napi_get_value_double(env, argv[2], &nd));
-  const uint64_t n = (uint64_t)nd;
+  dec_job *j = (dec_job *)calloc(1, sizeof *j);
+  if (!j) return NULL;
+  double brem = 0;
+  void *bytes = NULL;
+  if (napi_get_value_external(env, argv[0], (void **)&j->box) != napi_ok ||
+      napi_get_buffer_info(env, argv[1], &bytes, &j->n) != napi_ok ||
+      napi_get_value_double(env, argv[2], &brem) != napi_ok) {
+    free(j);
+    napi_throw_type_error(env, NULL, "decode: bad arguments");
+    return NULL;
+  }
+  j->bytes = (const uint8_t *)bytes;
+  j->carry.blob_remaining = (uint64_t)brem;
+  return j;
+}
+
+static napi_value js_decode(napi_env env, napi_callback_info info) {
+  napi_value argv[4];
+  dec_job *j = dec_args(env, info, 4, argv);
+  if (!j) return NULL;
+  napi_value name;
+  NAPI_CALL(env, napi_create_string_utf8(env, "drp.decode", NAPI_AUTO_LENGTH, &name));
+  NAPI_CALL(env, napi_create_reference(env, argv[1], 1, &j->buf_ref)); /* keep the bytes alive */
+  NAPI_CALL(env, napi_create_reference(env, argv[3], 1, &j->cb_ref));
+  NAPI_CALL(env, napi_create_async_work(env, NULL, name, dec_execute, dec_complete, j, &j->work));
+  NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  return NULL;
+}
+
+static napi_value js_decode_sync(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  dec_job *j = dec_args(env, info, 3, argv);
+  if (!j) return NULL;
+  dec_run(j);
+  napi_value res = NULL;
+  if (j->rc != DRP_OK) throw_rc(env, "decode", j->rc);
+  else if (!(res = dec_result(env, j))) napi_throw_error(env, NULL, "drp addon: result allocation failed");
+  free_cols(j->col);
+  free(j);
+  return res;
+}
+
+/* ---- encode ---------------------------------------------------------------------------- */
+
+typedef struct {
+  napi_async_work work;
+  napi_ref ref[12]; /* heap, 10 columns, cb */
+  ctx_box *box;
+  const uint8_t *heap;
+  size_t heap_n;
+  uint64_t n;
   void *col[10];
+  int rc;
+  uint8_t *out;
+  uint64_t total;
+} enc_job;
+
+static void enc_execute(napi_env env, void *data) {
+  (void)env;
+  enc_job *j = (enc_job *)data;
+  const uint64_t n = j->n;
+  /* JS Numbers (Float64Array) -> u64 for heap offsets and change/from/to */
+  uint64_t *u[6] = {NULL};
+  const int src[6] = {0, 2, 4, 6, 7, 8};
+  for (int k = 0; k < 6; k++) {
+    u[k] = (uint64_t *)malloc(n * 8 + 8);
+    if (!u[k]) {
+      j->rc = DRP_E_NOMEM;
+      goto done;
+    }
+    const double *d = (const double *)j->col[src[k]];
+    for (uint64_t i = 0; i < n; i++) u[k][i] = (uint64_t)d[i];
+  }
+  {
+    drp_change_src s = {u[0], j->col[1], u[1], j->col[3], u[2], j->col[5], u[3], u[4], u[5], j->col[9]};
+    pthread_mutex_lock(&j->box->mu);
+    j->rc = drp_encode_size(j->box->c, &s, n, &j->total);
+    if (j->rc == DRP_OK) {
+      j->out = (uint8_t *)malloc(j->total ? j->total : 1);
+      if (!j->out) j->rc = DRP_E_NOMEM;
+    }
+    uint64_t written = 0;
+    if (j->rc == DRP_OK) j->rc = drp_encode_batch(j->box->c, &s, j->heap, j->heap_n, n, j->out, j->total, &written);
+    pthread_mutex_unlock(&j->box->mu);
+    if (j->rc == DRP_OK && written != j->total) j->rc = DRP_E_INVAL; /* never expected: one kernel sizes both */
+  }
+done:
+  for (int k = 0; k < 6; k++) free(u[k]);
+  if (j->rc != DRP_OK) {
+    free(j->out);
+    j->out = NULL;
+  }
+}
+
+static void enc_complete(napi_env env, napi_status status, void *data) {
+  enc_job *j = (enc_job *)data;
+  napi_value cb, argv[2], undef;
+  napi_get_reference_value(env, j->ref[11], &cb);
+  napi_get_undefined(env, &undef);
+  argv[1] = undef;
+  if (status != napi_ok || j->rc != DRP_OK) {
+    argv[0] = make_error(env, "encode", status != napi_ok ? DRP_E_INVAL : j->rc);
+  } else if (napi_create_external_buffer(env, j->total, j->out ? (void *)j->out : (void *)"", j->out ? free_finalizer : NULL,
+                                         NULL, &argv[1]) != napi_ok) {
+    argv[0] = make_error(env, "encode (result)", DRP_E_NOMEM);
+    argv[1] = undef;
+    free(j->out);
+  } else {
+    napi_get_null(env, &argv[0]);
+  }
+  for (int k = 0; k < 12; k++) napi_delete_reference(env, j->ref[k]);
+  napi_delete_async_work(env, j->work);
+  free(j);
+  napi_call_function(env, undef, cb, 2, argv, NULL);
+}
+
+/* encode(ctx, heap: Buffer, n, keyOff, keyLen, subsetOff, subsetLen, valueOff, valueLen,
+ *        change, from, to, flags, cb) — offsets/numbers as Float64Array, lengths Uint32Array,
+ *        flags Uint8Array; cb(err, Buffer with the wire bytes of n change frames). */
+static napi_value js_encode(napi_env env, napi_callback_info info) {
+  size_t argc = 14;
+  napi_value argv[14];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 14) {
+    napi_throw_type_error(env, NULL, "encode(ctx, heap, n, 10 column arrays, cb)");
+    return NULL;
+  }
+  enc_job *j = (enc_job *)calloc(1, sizeof *j);
+  if (!j) {
+    napi_throw_error(env, NULL, "drp addon: out of memory");
+    return NULL;
+  }
+  void *heap = NULL;
+  double nd = 0;
+  if (napi_get_value_external(env, argv[0], (void **)&j->box) != napi_ok ||
+      napi_get_buffer_info(env, argv[1], &heap, &j->heap_n) != napi_ok ||
+      napi_get_value_double(env, argv[2], &nd) != napi_ok) {
+    free(j);
+    napi_throw_type_error(env, NULL, "encode: bad arguments");
+    return NULL;
+  }
+  j->heap = (const uint8_t *)heap;
+  j->n = (uint64_t)nd;
   for (int i = 0; i < 10; i++) {
     napi_typedarray_type t;
     size_t len, boff;
     napi_value ab;
-    NAPI_CALL(env, napi_get_typedarray_info(env, argv[3 + i], &t, &len, &col[i], &ab, &boff));
-    if (len < n) {
-      napi_throw_range_error(env, NULL, "encode: column shorter than n");
+    if (napi_get_typedarray_info(env, argv[3 + i], &t, &len, &j->col[i], &ab, &boff) != napi_ok || len < j->n) {
+      free(j);
+      napi_throw_range_error(env, NULL, "encode: column missing or shorter than n");
       return NULL;
     }
   }
-  /* JS Numbers (Float64Array) -> u64 for heap offsets and change/from/to */
-  uint64_t *ko = malloc(n * 8 + 8), *so = malloc(n * 8 + 8), *vo = malloc(n * 8 + 8), *ch = malloc(n * 8 + 8),
-           *fr = malloc(n * 8 + 8), *to = malloc(n * 8 + 8);
-  if (!ko || !so || !vo || !ch || !fr || !to) {
-    napi_throw_error(env, NULL, "drp addon: out of memory");
-    free(ko); free(so); free(vo); free(ch); free(fr); free(to);
-    return NULL;
-  }
-  for (uint64_t i = 0; i < n; i++) {
-    ko[i] = (uint64_t)((double *)col[0])[i];
-    so[i] = (uint64_t)((double *)col[2])[i];
-    vo[i] = (uint64_t)((double *)col[4])[i];
-    ch[i] = (uint64_t)((double *)col[6])[i];
-    fr[i] = (uint64_t)((double *)col[7])[i];
-    to[i] = (uint64_t)((double *)col[8])[i];
-  }
-  drp_change_src src = {ko, col[1], so, col[3], vo, col[5], ch, fr, to, col[9]};
-  uint64_t total = 0;
-  napi_value out = NULL;
-  int rc = drp_encode_size(c, &src, n, &total);
-  if (rc != DRP_OK) {
-    throw_rc(env, "encode_size", rc);
-    goto done;
-  }
-  {
-    void *ob = NULL;
-    if (napi_create_buffer(env, total ? total : 1, &ob, &out) != napi_ok) goto done;
-    uint64_t written = 0;
-    rc = drp_encode_batch(c, &src, heap, heap_n, n, ob, total, &written);
-    if (rc != DRP_OK) {
-      out = NULL;
-      throw_rc(env, "encode", rc);
-      goto done;
-    }
-    if (written != total) { /* never expected: both sizes come from the same kernel */
-      napi_throw_error(env, NULL, "libdrp encode size mismatch");
-      out = NULL;
-    }
-  }
-done:
-  free(ko); free(so); free(vo); free(ch); free(fr); free(to);
-  return out;
+  napi_value name;
+  NAPI_CALL(env, napi_create_string_utf8(env, "drp.encode", NAPI_AUTO_LENGTH, &name));
+  NAPI_CALL(env, napi_create_reference(env, argv[1], 1, &j->ref[0]));
+  for (int i = 0; i < 10; i++) NAPI_CALL(env, napi_create_reference(env, argv[3 + i], 1, &j->ref[1 + i]));
+  NAPI_CALL(env, napi_create_reference(env, argv[13], 1, &j->ref[11]));
+  NAPI_CALL(env, napi_create_async_work(env, NULL, name, enc_execute, enc_complete, j, &j->work));
+  NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  return NULL;
 }
 
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"open", NULL, js_open, NULL, NULL, NULL, napi_enumerable, NULL},
       {"decode", NULL, js_decode, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"decodeSync", NULL, js_decode_sync, NULL, NULL, NULL, napi_enumerable, NULL},
       {"encode", NULL, js_encode, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);

@@ -1,12 +1,19 @@
 // Decoder: the reference's streaming decode API (decode.js:63-142 of
 // mafintosh/dat-replication-protocol v4.1.2) over the gfx950 batch codec.
 //
-// Each chunk handed to _write is decoded on the GPU in one call (frame split + Change
-// decode, libdrp via lib/drp.node); the returned frame table is then replayed here with
-// the reference's callback discipline: a change/blob callback increments _pending, and
-// replay stops while _pending > 0 and resumes from _down (decode.js:89-99, 144-169).
-// Bytes of an incomplete trailing frame are carried into the next chunk
-// (decode.js:75-81 state) and an open blob continues across chunks.
+// Writes are coalesced (everything written before the event loop comes round again, up to
+// MAX_BATCH bytes) and decoded on the GPU in one call on a worker thread (frame split +
+// Change decode, libdrp via lib/drp.node). The returned frame table is replayed here with the
+// reference's callback discipline: a change/blob callback increments _pending, and replay stops
+// while _pending > 0 and resumes from _down (decode.js:89-99, 144-169). The event sequence is
+// the reference's; only the timing of write callbacks differs (a write below the batch
+// threshold is acknowledged when queued; one that fills a batch when that batch has been
+// delivered, which is the backpressure).
+//
+// Carry across batches (decode.js:75-81): an incomplete header (<= 10 bytes) is prepended to
+// the next batch; an incomplete Change frame is collected once into a buffer of its declared
+// size (as _onchangedata fills _buffer, decode.js:229-247) and decoded when complete; the
+// bytes of an open blob continue through the next batch as pass-through (never sent to HBM).
 'use strict'
 
 var stream = require('stream')
@@ -14,10 +21,14 @@ var util = require('util')
 var native = require('./native')
 
 var FLUSH = Buffer.from([0]) // identity-compared end sentinel (decode.js:6, :125)
+var MAX_BATCH = Number(process.env.DRP_MAX_BATCH) || 64 * 1024 * 1024
+var MAX_FRAME = require('buffer').constants.MAX_LENGTH
 
 var TYPE_MASK = 0x3f
 var CONT = 0x40
 var PARTIAL = 0x80
+var TAIL_HEADER = 1
+var TAIL_CHANGE = 2
 
 // --- blob payload stream handed to the user's blob handler (decode.js:8-48) ---------
 function BlobStream (parent) {
@@ -76,19 +87,27 @@ function Decoder () {
   this.blobs = 0
 
   this._pending = 0
-  this._onflush = null
+  this._paused = false    // replay stopped at a callback that has not been acknowledged
 
   this._onchange = noopChange
   this._onblob = drainBlob
   this._onfinalize = noopFinalize
 
   this._ctx = native.context()
-  this._carry = null      // bytes of an incomplete frame (header and/or change payload)
+  this._queue = []        // written chunks not yet handed to the GPU
+  this._queued = 0
+  this._scheduled = false
+  this._busy = false      // a batch is being decoded or replayed
+  this._held = null       // write callback held back until its batch is delivered
+  this._final = null      // end(): finalize once everything before it is delivered
+  this._carry = null      // an incomplete frame header (<= 10 bytes)
+  this._partial = null    // an incomplete Change frame of known size: {buf, filled}
   this._blobLeft = 0      // payload bytes of the open blob still to come
   this._blob = null       // the open BlobStream
   this._res = null        // decoded batch being replayed
   this._buf = null        // its bytes
   this._next = 0          // next frame to deliver
+  this._tooBig = 0        // a carried Change frame larger than a Buffer can hold
 
   var self = this
   this._up = function () {
@@ -96,10 +115,13 @@ function Decoder () {
     return self._down
   }
   this._down = function () {
-    if (--self._pending > 0) return
-    var cb = self._onflush
-    self._onflush = null
-    if (cb) self._replay(cb)
+    if (--self._pending > 0 || !self._paused) return
+    self._paused = false
+    self._replay()
+  }
+  this._kickFn = function () {
+    self._scheduled = false
+    self._kick()
   }
 }
 util.inherits(Decoder, stream.Writable)
@@ -117,20 +139,22 @@ Decoder.prototype.blob = function (fn) { this._onblob = fn }
 Decoder.prototype.finalize = function (fn) { this._onfinalize = fn }
 
 Decoder.prototype._write = function (data, enc, cb) {
-  if (data === FLUSH) return this._onfinalize(cb)
+  if (data === FLUSH) {
+    this._final = cb
+    return this._kick()
+  }
   this.bytes += data.length
-
-  var buf = this._carry ? Buffer.concat([this._carry, data]) : data
-  this._carry = null
-  var res = native.decode(this._ctx, buf, this._blobLeft)
-  // tail kinds 1/2: an incomplete header / change payload is carried (copied, as the
-  // reference copies it into _header / _buffer)
-  if (!res.errCode && (res.tailKind === 1 || res.tailKind === 2)) this._carry = Buffer.from(buf.slice(res.consumed))
-  this._blobLeft = res.blobRemaining
-  this._res = res
-  this._buf = buf
-  this._next = 0
-  this._replay(cb)
+  this._queue.push(data)
+  this._queued += data.length
+  if (this._queued >= MAX_BATCH) {
+    this._held = cb // backpressure: acknowledged once this batch has been delivered
+    return this._kick()
+  }
+  cb()
+  if (!this._scheduled) {
+    this._scheduled = true
+    setImmediate(this._kickFn)
+  }
 }
 
 Decoder.prototype.end = function (data, enc, cb) {
@@ -141,19 +165,93 @@ Decoder.prototype.end = function (data, enc, cb) {
   stream.Writable.prototype.end.call(this, cb)
 }
 
+// Hand the queued bytes to the GPU (one batch), or finish when nothing is left.
+Decoder.prototype._kick = function () {
+  if (this._busy || this.destroyed) return
+  if (!this._queued) {
+    var held = this._held
+    this._held = null
+    if (held) held()
+    if (this._final && !this._queued && !this._busy) {
+      var fin = this._final
+      this._final = null
+      this._onfinalize(fin) // decode.js:125-128
+    }
+    return
+  }
+  var chunks = this._queue
+  this._queue = []
+  this._queued = 0
+  var p = this._partial
+  if (p) {
+    // collect the rest of a Change frame of known size: each byte is copied once
+    var k = 0
+    while (k < chunks.length && p.filled < p.buf.length) {
+      var c = chunks[k]
+      var take = Math.min(c.length, p.buf.length - p.filled)
+      c.copy(p.buf, p.filled, 0, take)
+      p.filled += take
+      if (take < c.length) chunks[k] = c.slice(take)
+      else k++
+    }
+    if (p.filled < p.buf.length) return this._kick() // nothing else to decode yet
+    this._partial = null
+    chunks = [p.buf].concat(chunks.slice(k))
+  } else if (this._carry) {
+    chunks.unshift(this._carry)
+    this._carry = null
+  }
+  var batch = chunks.length === 1 ? chunks[0] : Buffer.concat(chunks)
+  this._busy = true
+  var self = this
+  native.decode(this._ctx, batch, this._blobLeft, function (err, res) {
+    self._ondecoded(err, res, batch)
+  })
+}
+
+Decoder.prototype._ondecoded = function (err, res, batch) {
+  if (this.destroyed) return
+  if (err) return this.destroy(err)
+  if (!res.errCode) {
+    var rest = batch.length - res.consumed
+    if (res.tailKind === TAIL_HEADER) {
+      this._carry = Buffer.from(batch.slice(res.consumed)) // copied, as into _header
+    } else if (res.tailKind === TAIL_CHANGE) {
+      if (res.frameBytes > MAX_FRAME) {
+        this._tooBig = res.frameBytes // reported after the frames before it (the reference throws)
+      } else {
+        var buf = Buffer.allocUnsafe(res.frameBytes) // decode.js:227 allocates _buffer the same way
+        batch.copy(buf, 0, res.consumed)
+        this._partial = { buf: buf, filled: rest }
+      }
+    }
+  }
+  this._blobLeft = res.blobRemaining
+  this._res = res
+  this._buf = batch
+  this._next = 0
+  this._replay()
+}
+
 // Deliver decoded frames in order while no callback is outstanding (decode.js:144-169).
-Decoder.prototype._replay = function (cb) {
+Decoder.prototype._replay = function () {
   var res = this._res
   while (this._next < res.n && this._pending <= 0 && !this.destroyed) {
     this._deliver(this._next++)
   }
   if (this.destroyed) return
-  if (this._next >= res.n && res.errCode && this._pending <= 0) {
-    this.destroy(new Error(ERRORS[res.errCode](res.errDetail)))
+  if (this._pending > 0) {
+    this._paused = true // resumed by _down
     return
   }
-  if (this._pending <= 0) cb()
-  else this._onflush = cb
+  if (res.errCode) return this.destroy(new Error(ERRORS[res.errCode](res.errDetail)))
+  if (this._tooBig) {
+    return this.destroy(new RangeError('Change frame of ' + this._tooBig + ' bytes exceeds the maximum Buffer size'))
+  }
+  this._res = null
+  this._buf = null
+  this._busy = false
+  this._kick()
 }
 
 Decoder.prototype._deliver = function (i) {
@@ -176,19 +274,20 @@ Decoder.prototype._deliver = function (i) {
     this._onchange(change, this._up())
     return
   }
-  // blob frame (or the continuation of one opened in an earlier chunk)
+  // blob frame (or the continuation of one opened in an earlier batch)
   if (!(type & CONT)) {
     this.blobs++
     this._blob = new BlobStream(this)
     this._onblob(this._blob, this._down)
   }
   var avail = Math.min(res.len[i], buf.length - off)
-  this._blob._push(buf.slice(off, off + avail), this._up())
+  var blob = this._blob
   if (!(type & PARTIAL)) {
     this._pending++ // released by the handler's cb (decode.js:171-177)
-    this._blob._end()
     this._blob = null
   }
+  blob._push(buf.slice(off, off + avail), this._up())
+  if (!(type & PARTIAL)) blob._end()
 }
 
 module.exports = Decoder

@@ -1,9 +1,11 @@
 // Encoder: the reference's streaming encode API (encode.js:46-151 of
 // mafintosh/dat-replication-protocol v4.1.2) over the gfx950 batch codec.
 //
-// change() calls made in the same tick are encoded together on the GPU
-// (messages.Change.encode + varint(len+1) 0x01 framing, libdrp encode kernels) and pushed
-// as one chunk; the byte stream is identical to the reference's. Blob ordering follows
+// change() calls made in the same tick are encoded together on the GPU, on a worker thread
+// (messages.Change.encode + varint(len+1) 0x01 framing, libdrp encode kernels), and pushed as
+// one chunk; the byte stream is identical to the reference's. Everything the encoder outputs
+// goes through one ordered queue, so a blob header or blob bytes issued after a batch of
+// changes never overtake that batch's (asynchronous) encode. Blob ordering follows
 // encode.js:77-117: blobs serialise in creation order (later blobs are corked) and changes
 // issued while a blob is open wait until every open blob has finished.
 'use strict'
@@ -89,6 +91,7 @@ function Encoder () {
   this._batch = []     // [row, cb] awaiting the GPU encode
   this._scheduled = false
   this._ondrain = null
+  this._out = []       // ordered output: {data, cb} (data null until its encode completes), or EOF
   this._ctx = native.context()
 }
 util.inherits(Encoder, stream.Readable)
@@ -174,19 +177,47 @@ Encoder.prototype._flush = function () {
     if (r.value) { vo[i] = p; vl[i] = r.value.length; p += r.value.copy(heap, p); fl[i] |= 2 }
     ch[i] = r.change; fr[i] = r.from; to[i] = r.to
   }
-  var wire = native.encode(this._ctx, heap, n, ko, kl, so, sl, vo, vl, ch, fr, to, fl)
   var cbs = batch.map(function (b) { return b[1] })
-  this._push(wire, function () { for (var k = 0; k < cbs.length; k++) cbs[k]() })
+  var slot = { data: null, cb: function () { for (var k = 0; k < cbs.length; k++) cbs[k]() } }
+  this._out.push(slot)
+  var self = this
+  native.encode(this._ctx, heap, n, ko, kl, so, sl, vo, vl, ch, fr, to, fl, function (err, wire) {
+    if (self.destroyed) return
+    if (err) return self.destroy(err)
+    slot.data = wire
+    self._drainOut()
+  })
 }
 
 Encoder.prototype.finalize = function (cb) {
   this._flush()
-  if (!this._readableState.ended) this.push(null)
-  if (cb) cb()
+  this._out.push({ eof: true, cb: cb || noop })
+  this._drainOut()
 }
 
+// Queue output behind anything still being encoded (encode.js:139-145 pushes in call order).
 Encoder.prototype._push = function (data, cb) {
   if (this.destroyed) return
+  this._out.push({ data: data, cb: cb })
+  this._drainOut()
+}
+
+Encoder.prototype._drainOut = function () {
+  while (this._out.length && !this.destroyed) {
+    var o = this._out[0]
+    if (o.eof) {
+      this._out.shift()
+      if (!this._readableState.ended) this.push(null)
+      o.cb()
+      continue
+    }
+    if (!o.data) return // its encode is still running
+    this._out.shift()
+    this._emit(o.data, o.cb)
+  }
+}
+
+Encoder.prototype._emit = function (data, cb) {
   this.bytes += data.length
   if (this.push(data)) return cb()
   var prev = this._ondrain

@@ -12,5 +12,6 @@ exports.context = function () {
   return ctx
 }
 exports.decode = addon.decode
+exports.decodeSync = addon.decodeSync
 exports.encode = addon.encode
 exports.abiVersion = addon.abiVersion

@@ -22,7 +22,8 @@ TAIL_NONE, TAIL_HEADER, TAIL_CHANGE, TAIL_BLOB = 0, 1, 2, 3
 EXPORTS = [
     "drp_abi_version", "drp_open", "drp_close", "drp_stream", "drp_synchronize",
     "drp_last_timing", "drp_set_tile", "drp_set_strict", "drp_set_exact", "drp_decode_scratch_bytes",
-    "drp_decode_device", "drp_decode_batch", "drp_encode_size", "drp_encode_device",
+    "drp_decode_device", "drp_decode_batch", "drp_decode_stage", "drp_decode_fetch",
+    "drp_encode_size", "drp_encode_device",
     "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results",
 ]
 
@@ -45,13 +46,14 @@ class ChangeSrc(C.Structure):
 
 
 class Carry(C.Structure):
-    _fields_ = [("blob_remaining", U64), ("consumed", U64), ("tail_kind", U32), ("reserved", U32)]
+    _fields_ = [("blob_remaining", U64), ("consumed", U64), ("tail_kind", U32), ("reserved", U32),
+                ("frame_bytes", U64)]
 
 
 class StreamResult(C.Structure):
     _fields_ = [("frame_begin", U64), ("frames", U64), ("changes", U64), ("blobs", U64),
                 ("consumed", U64), ("blob_remaining", U64), ("err_frame", U64), ("err_code", U32),
-                ("err_detail", U32), ("tail_kind", U32), ("reserved", U32)]
+                ("err_detail", U32), ("tail_kind", U32), ("reserved", U32), ("tail_frame_bytes", U64)]
 
 
 class StreamStats(C.Structure):
@@ -91,6 +93,9 @@ def lib():
         L.drp_decode_batch.argtypes = [P, P, U64, C.POINTER(Carry), C.POINTER(Frames),
                                        C.POINTER(Changes), U64, C.POINTER(U64), C.POINTER(U64),
                                        C.POINTER(U32), C.POINTER(U32)]
+        L.drp_decode_stage.argtypes = [P, P, U64, C.POINTER(Carry), C.POINTER(U64), C.POINTER(U64),
+                                       C.POINTER(U32), C.POINTER(U32)]
+        L.drp_decode_fetch.argtypes = [P, C.POINTER(Frames), C.POINTER(Changes), U64, U64]
         L.drp_encode_size.argtypes = [P, C.POINTER(ChangeSrc), U64, C.POINTER(U64)]
         L.drp_encode_device.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, P, U64]
         L.drp_encode_batch.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, U64,
@@ -98,7 +103,8 @@ def lib():
         L.drp_index_scan.argtypes = [P, P, U64, P]
         L.drp_stream_stats_from_results.argtypes = [P, P, P, U64, P]
         for f in ["drp_open", "drp_synchronize", "drp_last_timing", "drp_set_tile",
-                  "drp_set_strict", "drp_set_exact", "drp_decode_device", "drp_decode_batch", "drp_encode_size",
+                  "drp_set_strict", "drp_set_exact", "drp_decode_device", "drp_decode_batch",
+                  "drp_decode_stage", "drp_decode_fetch", "drp_encode_size",
                   "drp_encode_device", "drp_encode_batch", "drp_index_scan",
                   "drp_stream_stats_from_results"]:
             getattr(L, f).restype = C.c_int
@@ -212,7 +218,7 @@ class Ctx:
             cap = n // 2 + 2
         o = alloc_host_outputs(cap)
         fr, co = _structs(o, _p)
-        carry = Carry(blob_remaining, 0, 0, 0)
+        carry = Carry(blob_remaining, 0, 0, 0, 0)
         nf, ef, ec, ed = U64(), U64(), U32(), U32()
         buf = w if n else np.zeros(16, np.uint8)
         rc = self.L.drp_decode_batch(self.h, _p(buf), n, C.byref(carry), C.byref(fr), C.byref(co),
@@ -223,8 +229,31 @@ class Ctx:
         res = {k: v[:keep] for k, v in o.items()}
         res.update(nframes=nframes, err_frame=int(ef.value), err_code=int(ec.value),
                    err_detail=int(ed.value), consumed=int(carry.consumed),
-                   tail=int(carry.tail_kind), blob_remaining=int(carry.blob_remaining))
+                   tail=int(carry.tail_kind), blob_remaining=int(carry.blob_remaining),
+                   frame_bytes=int(carry.frame_bytes))
         return res
+
+    def decode_staged(self, wire, blob_remaining=0, pieces=1):
+        """drp_decode_stage, then drp_decode_fetch of the rows in `pieces` consecutive
+        fetches into host columns sized from the frame count (the N-API addon's path)."""
+        w = np.frombuffer(bytes(wire), np.uint8) if not isinstance(wire, np.ndarray) else wire
+        n = int(w.size)
+        carry = Carry(blob_remaining, 0, 0, 0, 0)
+        nf, ef, ec, ed = U64(), U64(), U32(), U32()
+        buf = w if n else np.zeros(16, np.uint8)
+        _chk("drp_decode_stage", self.L.drp_decode_stage(self.h, _p(buf), n, C.byref(carry), C.byref(nf),
+                                                         C.byref(ef), C.byref(ec), C.byref(ed)))
+        rows = int(nf.value) + (1 if ec.value in (ERR_CHANGE, ERR_REQUIRED) else 0)
+        o = alloc_host_outputs(rows)
+        bounds = np.linspace(0, rows, pieces + 1).astype(np.int64)
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            part = {k: v[a:] for k, v in o.items()}
+            fr, co = _structs(part, _p)
+            _chk("drp_decode_fetch", self.L.drp_decode_fetch(self.h, C.byref(fr), C.byref(co), int(a), int(b - a)))
+        o.update(nframes=int(nf.value), err_frame=int(ef.value), err_code=int(ec.value), err_detail=int(ed.value),
+                 consumed=int(carry.consumed), tail=int(carry.tail_kind), blob_remaining=int(carry.blob_remaining),
+                 frame_bytes=int(carry.frame_bytes))
+        return o
 
     # ---- device decode over torch tensors (bench path) --------------------------------
     def decode_device(self, wire_t, stream_off_t, entry_t, outs, cap, results_t):

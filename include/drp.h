@@ -112,6 +112,9 @@ typedef struct drp_carry {
   uint64_t consumed;       /* out */
   uint32_t tail_kind;      /* out: DRP_TAIL_* */
   uint32_t reserved;
+  uint64_t frame_bytes;    /* out, tail CHANGE: size of the carried frame (header + id + payload), so
+                              the caller can collect exactly that many bytes once (decode.js:229-247
+                              fills _buffer the same way) instead of re-sending a growing carry */
 } drp_carry;
 
 /* Per-stream result of a (multi-)stream decode. */
@@ -127,6 +130,7 @@ typedef struct drp_stream_result {
   uint32_t err_detail;     /* DRP_ERR_TYPE: the id byte */
   uint32_t tail_kind;      /* DRP_TAIL_* */
   uint32_t reserved;
+  uint64_t tail_frame_bytes; /* tail CHANGE: header + id + payload bytes of the carried frame */
 } drp_stream_result;
 
 /* The 32-byte per-stream record exchanged by the multi-GPU all-gather. */
@@ -188,6 +192,19 @@ int drp_decode_batch(drp_ctx *ctx, const uint8_t *bytes, uint64_t n, drp_carry *
                      const drp_frames *frames, const drp_changes *cols, uint64_t cap,
                      uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code,
                      uint32_t *err_detail);
+
+/* Two-step form of drp_decode_batch for callers that size their host columns from the
+ * result (the N-API addon, which runs it on a worker thread): drp_decode_stage decodes one
+ * host batch into device columns owned by the ctx (capacity grows as needed) and reports the
+ * same counts, error and carry as drp_decode_batch; drp_decode_fetch then copies rows
+ * [first, first + rows) into caller-owned HOST columns. Rows = *n_frames, plus one for a
+ * malformed Change (DRP_ERR_CHANGE / DRP_ERR_REQUIRED: its flags say why). The staged result
+ * stays valid until the next decode call on the ctx. A leading blob continuation's bytes
+ * (carry->blob_remaining) are never copied to the device. */
+int drp_decode_stage(drp_ctx *ctx, const uint8_t *bytes, uint64_t n, drp_carry *carry,
+                     uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail);
+int drp_decode_fetch(drp_ctx *ctx, const drp_frames *frames, const drp_changes *cols, uint64_t first,
+                     uint64_t rows);
 
 /* ---- encode -------------------------------------------------------------- */
 /* Wire size of encoding rows [0,n) as change frames (varint(len+1) 0x01 payload). */

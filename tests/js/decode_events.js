@@ -1,27 +1,48 @@
 // Feed a wire file through the package's Decoder in the given chunk sizes and print the
-// delivered events as JSON lines (used by tests/test_js_api.py to compare with the oracle).
-// usage: node decode_events.js <wire file> <chunk sizes comma separated, cycled> [asyncAck]
+// delivered events as JSON (used by tests/test_js_api.py to compare with the oracle).
+// usage: node decode_events.js <wire file> <chunk sizes comma separated, cycled> [mode] [n]
+//   mode "async": change/blob callbacks acknowledged on setImmediate
+//   mode "destroy": async acks, and decoder.destroy() inside the n-th change callback
+//   mode "digest": events carry sha256 of keys/values/blob data instead of hex
 'use strict'
 var fs = require('fs')
 var path = require('path')
+var crypto = require('crypto')
 var protocol = require(path.join(__dirname, '..', '..', 'dat-replication-protocol_amd'))
 
 var wire = fs.readFileSync(process.argv[2])
 var sizes = (process.argv[3] || '65536').split(',').map(Number)
-var asyncAck = process.argv[4] === 'async'
+var mode = process.argv[4] || ''
+var nth = Number(process.argv[5] || 0)
+var asyncAck = mode === 'async' || mode === 'destroy'
+var digest = mode === 'digest'
+function enc (b) {
+  return digest ? crypto.createHash('sha256').update(b).digest('hex').slice(0, 16) : b.toString('hex')
+}
 var out = []
 var d = protocol.decode()
+var seen = 0
 d.change(function (c, cb) {
-  out.push({ t: 'change', subset: Buffer.from(c.subset, 'utf8').toString('hex'), key: Buffer.from(c.key, 'utf8').toString('hex'),
-    change: c.change, from: c.from, to: c.to, value: c.value === null ? null : c.value.toString('hex') })
+  out.push({ t: 'change', subset: enc(Buffer.from(c.subset, 'utf8')), key: enc(Buffer.from(c.key, 'utf8')),
+    change: c.change, from: c.from, to: c.to, value: c.value === null ? null : enc(c.value) })
+  if (mode === 'destroy' && ++seen === nth) {
+    d.destroy()
+    setTimeout(done, 200) // anything delivered after destroy() would land before this
+    return
+  }
   if (asyncAck) setImmediate(cb); else cb()
 })
 d.blob(function (b, cb) {
   var parts = []
   b.on('data', function (x) { parts.push(x) })
-  b.on('end', function () { out.push({ t: 'blob', data: Buffer.concat(parts).toString('hex') }); cb() })
+  b.on('end', function () {
+    var data = Buffer.concat(parts)
+    out.push({ t: 'blob', data: enc(data), len: data.length })
+    if (asyncAck) setImmediate(cb); else cb()
+  })
 })
 d.on('error', function (e) { out.push({ t: 'error', message: e.message }); done() })
+d.on('close', function () { out.push({ t: 'close' }) })
 d.on('finish', function () { out.push({ t: 'finish', changes: d.changes, blobs: d.blobs, bytes: d.bytes }); done() })
 var printed = false
 function done () {
@@ -37,3 +58,4 @@ while (pos < wire.length) {
   pos += n
 }
 d.end()
+setTimeout(function () { process.stderr.write('decode_events: timeout\n'); done(); process.exit(3) }, 100000).unref()

@@ -274,3 +274,28 @@ def test_encode_max_width_varints(ctx):
         c[k][:] = np.uint64(2**64 - 1)
     c["flags"][:] |= 2
     assert ctx.encode_batch(heap, c) == O.encode_changes(heap, c)
+
+
+def test_stage_fetch_pieces_and_continuations(ctx):
+    """drp_decode_stage + drp_decode_fetch (the N-API path): rows fetched in pieces equal the
+    one-call decode; a leading blob continuation of every length mod 16 (its bytes are not
+    staged to HBM: the device stream starts at the aligned offset after it) gives the oracle's
+    frames at the right absolute offsets; a change frame cut by the batch end reports its full
+    size (drp_carry.frame_bytes) for the O(n) carry."""
+    from _gpu import assert_same
+    rng = random.Random(31)
+    wire = S.random_stream(rng, 1500, blob_p=0.1, blob_max=3000)
+    full = ctx.decode_batch(wire)
+    for pieces in (1, 3, 7):
+        st = ctx.decode_staged(wire, pieces=pieces)
+        assert_same({k: (v[:len(full["type"])] if hasattr(v, "shape") else v) for k, v in st.items()}, full,
+                    f"pieces{pieces}")
+    for brem in list(range(1, 40)) + [4095, 4096, 4097, 65537]:
+        w = rng.randbytes(brem) + wire
+        g = ctx.decode_staged(w, blob_remaining=brem)
+        r = O.decode_batch(w, blob_remaining=brem)
+        assert_same({k: (v[:len(r["type"])] if hasattr(v, "shape") else v) for k, v in g.items()}, r, f"brem{brem}")
+    f = S.frame(S.change_payload(b"k" * 40, 1, 2, 3, value=rng.randbytes(5000)))
+    for cut in (3, 100, len(f) - 1):  # (1 or 2 bytes: the header itself is incomplete)
+        g = ctx.decode_staged(wire + f[:cut])
+        assert g["tail"] == 2 and g["frame_bytes"] == len(f) and g["consumed"] == len(wire), cut

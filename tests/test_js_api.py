@@ -1,6 +1,7 @@
 """The Node host layer (dat-replication-protocol_amd/{index,decode,encode}.js over the
 N-API addon): reference-API round trips (test/basic.js restated) and event-level parity
 with the oracle across chunkings and asynchronous callback acks."""
+import hashlib
 import json
 import os
 import random
@@ -29,10 +30,14 @@ def test_package_loads_without_gpu_use():
             % (os.path.join(ROOT, "dat-replication-protocol_amd"),
                os.path.join(ROOT, "dat-replication-protocol_amd", "lib", "drp.node")))
     out = json.loads(subprocess.check_output([NODE, "-e", code], text=True, timeout=60))
-    assert out == ["function", "function", ["abiVersion", "decode", "encode", "open"], 2]
+    assert out == ["function", "function", ["abiVersion", "decode", "decodeSync", "encode", "open"], 2]
 
 
-def oracle_events(wire):
+def _enc(b, digest):
+    return hashlib.sha256(b).hexdigest()[:16] if digest else b.hex()
+
+
+def oracle_events(wire, digest=False):
     r = O.decode_batch(wire)
     ev = []
     for k in range(r["nframes"]):
@@ -46,24 +51,49 @@ def oracle_events(wire):
             # the JS object carries strings; compare their UTF-8 re-encoding
             sub = p[so:so + sl].decode("utf-8", "replace").encode() if f & 1 else b""
             key = p[ko:ko + kl].decode("utf-8", "replace").encode()
-            ev.append({"t": "change", "subset": sub.hex(), "key": key.hex(), "change": int(r["change"][k]),
-                       "from": int(r["from"][k]), "to": int(r["to"][k]),
-                       "value": p[vo:vo + vl].hex() if f & 2 else None})
+            ev.append({"t": "change", "subset": _enc(sub, digest), "key": _enc(key, digest),
+                       "change": int(r["change"][k]), "from": int(r["from"][k]), "to": int(r["to"][k]),
+                       "value": _enc(p[vo:vo + vl], digest) if f & 2 else None})
         else:
-            ev.append({"t": "blob", "data": wire[off:off + ln].hex()})
+            ev.append({"t": "blob", "data": _enc(wire[off:off + ln], digest), "len": ln})
     return r, ev
 
 
-def run_js(wire, sizes, mode=""):
+def run_js(wire, sizes, mode="", nth=0):
     with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
         f.write(wire)
         path = f.name
     try:
-        out = subprocess.check_output([NODE, os.path.join(JS, "decode_events.js"), path, sizes, mode],
+        out = subprocess.check_output([NODE, os.path.join(JS, "decode_events.js"), path, sizes, mode, str(nth)],
+                                      text=True, timeout=150)
+    finally:
+        os.unlink(path)
+    return json.loads(out)
+
+
+def run_encode(ops, slow=False):
+    from test_ref_fixtures import _val  # noqa: F401  (ops carry hex values already)
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(ops, f)
+        path = f.name
+    try:
+        out = subprocess.check_output([NODE, os.path.join(JS, "encode_ops.js"), path] + (["slow"] if slow else []),
                                       text=True, timeout=120)
     finally:
         os.unlink(path)
     return json.loads(out)
+
+
+def ops_json(ops):
+    out = []
+    for o in ops:
+        o = dict(o)
+        if o.get("value") is not None and not isinstance(o["value"], str):
+            o["value"] = o["value"].hex()
+        if "writes" in o:
+            o["writes"] = [w if isinstance(w, str) else w.hex() for w in o["writes"]]
+        out.append(o)
+    return out
 
 
 @pytest.mark.gpu
@@ -85,6 +115,7 @@ def test_decoder_events_match_oracle(sizes, mode):
                            subset_p=0.3)
     r, exp = oracle_events(wire)
     got = run_js(wire, sizes, mode)
+    got = [e for e in got if e["t"] != "close"]
     assert got[-1]["t"] == "finish", got[-3:]
     assert got[:-1] == exp
     assert got[-1]["changes"] == r["changes"] and got[-1]["blobs"] == r["blobs"]
@@ -99,3 +130,71 @@ def test_decoder_protocol_error():
     got = run_js(wire, "5")
     assert [e["t"] for e in got] == ["change", "error"]
     assert got[1]["message"] == "Protocol error, unknown type: 7"
+
+
+@pytest.mark.gpu
+@needs_node
+def test_c1_round_trip_through_the_package():
+    """BASELINE configs[0] (C1): 10,000 Changes (32-char [a-z0-9] keys, change=i+1, from=i,
+    to=i+1, 64 random value bytes) with e.blob(12) "hello world\n" issued after change 5000 while
+    the later changes queue behind it, through encode() with a slow consumer (push() returns
+    false: the drain path of encode.js:139-151), then decode(). The encoder's bytes equal the
+    reference encode.js's (fixture recorded in place) and the oracle's; the decoder's events
+    equal the oracle's (reference test/basic.js:86-126 at scale)."""
+    from test_ref_fixtures import FIX, reference_order_encode
+    ops = S.c1_ops()
+    got = run_encode(ops_json(ops), slow=True)
+    ref = FIX["encode"]["c1"]
+    wire = reference_order_encode(ops)
+    assert hashlib.sha256(wire).hexdigest() == ref["wire_sha256"]
+    assert got["sha256"] == ref["wire_sha256"] and got["len"] == ref["wire_len"]
+    assert (got["changes"], got["blobs"], got["bytes"]) == (10000, 1, ref["bytes"])
+    assert got["acked"] == 10001  # every change cb and the blob's finish cb ran
+    assert got["pushFalse"] >= 1, "the slow consumer never made push() return false"
+    r, exp = oracle_events(wire, digest=True)
+    assert r["changes"] == 10000 and r["blobs"] == 1
+    for sizes in ["65536", "1000,7"]:
+        ev = [e for e in run_js(wire, sizes, "digest") if e["t"] != "close"]
+        assert ev[:-1] == exp and ev[-1] == {"t": "finish", "changes": 10000, "blobs": 1, "bytes": len(wire)}
+
+
+@pytest.mark.gpu
+@needs_node
+@pytest.mark.parametrize("name", ["basic_change", "basic_blob", "basic_blob_then_change", "interleave", "widths"])
+def test_encoder_matches_reference_fixtures(name):
+    """The package's encoder reproduces the bytes the reference encode.js wrote for the same
+    call sequence (blob/change interleavings, field widths, absent/empty values, subsets)."""
+    from test_ref_fixtures import FIX
+    c = FIX["encode"][name]
+    for slow in (False, True):
+        got = run_encode(c["ops"], slow=slow)
+        assert got["hex"] == c["wire"], (name, slow)
+        assert (got["changes"], got["blobs"], got["bytes"]) == (c["changes"], c["blobs"], c["bytes"])
+
+
+@pytest.mark.gpu
+@needs_node
+def test_decoder_destroy_mid_batch():
+    """destroy() inside a change callback (decode.js:104-110) stops delivery at once: the events
+    before it equal the oracle's, 'close' follows, nothing else is delivered and there is no
+    'finish'; the GPU batch still in flight is dropped."""
+    wire = S.c2_stream(5000, seed=3).tobytes() + S.random_stream(random.Random(3), 200)
+    _, exp = oracle_events(wire)
+    for sizes, nth in [("65536", 37), ("1000", 1), ("300000", 4999)]:
+        got = run_js(wire, sizes, "destroy", nth)
+        assert got[:nth] == exp[:nth], sizes
+        assert got[nth:] == [{"t": "close"}], (sizes, got[nth:nth + 3])
+
+
+@pytest.mark.gpu
+@needs_node
+def test_c3_blobs_through_the_package():
+    """BASELINE configs[2] shape through the Node path: 1 MiB blobs between C2 runs in 64 KiB
+    writes (blob headers and frames straddle the write edges; blob continuations pass through
+    without going to HBM), asynchronous acks; every event equals the oracle's."""
+    wire = S.c3_stream(random.Random(8), 3, frames_per_unit=1000)
+    r, exp = oracle_events(wire, digest=True)
+    for sizes, mode in [("65536", "digest"), ("65536,1,4093", "digest")]:
+        got = [e for e in run_js(wire, sizes, mode) if e["t"] != "close"]
+        assert got[:-1] == exp
+        assert got[-1] == {"t": "finish", "changes": r["changes"], "blobs": r["blobs"], "bytes": len(wire)}
