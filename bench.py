@@ -490,10 +490,13 @@ def main():
 
     def step():
         ctx.decode_device(wire, stream_off, None, outs, cap, res)
-        if dist:  # the only collective: all-gather of 32-byte per-stream stats (RCCL over xGMI)
+        if dist:  # the only collective: all-gather of 32-byte per-stream stats
             stats = drp_dist.local_stats_device(ctx, res, stream_off)
-            table = drp_dist.gather_stats(stats, nstreams_total)
-            state["base"] = drp_dist.global_index_device(ctx, table)
+            if args.backend == "nccl":  # libdrp's RCCL communicator over xGMI (drp_index_allgather)
+                _, state["base"] = drp_dist.global_index_rccl(ctx, stats, nstreams_total)
+            else:  # gloo rehearsal of several ranks on one GPU
+                table = drp_dist.gather_stats(stats, nstreams_total)
+                state["base"] = drp_dist.global_index_device(ctx, table)
 
     for _ in range(max(1, args.warmup)):
         step()
@@ -542,7 +545,8 @@ def main():
     exact = os.environ.get("DRP_DECODE") == "exact"
     kname = (f"decode_tiles<{tile // 64}>" if exact else
              "speculative decode: spec_claims + verify_counts + tile scans + emit_tiles")
-    gather = "; RCCL all-gather of 32 B stream stats + index scan" if dist else "; no collective (1 GPU)"
+    gather = ("; drp_index_allgather (RCCL) of 32 B stream stats + index scan" if args.backend == "nccl" else
+              "; gloo all-gather of 32 B stream stats + index scan") if dist else "; no collective (1 GPU)"
     if args.workload == "c2":
         workload = {"workload": f"C2: {nframes / 1e6:g}M Change frames x 86 B (64 B values), one "
                                 f"{nframes * FRAME / 1e9:.2f} GB stream per GPU",
@@ -589,6 +593,7 @@ def main():
             if args.workload == "c2":
                 out["node_path"] = node_path()
         print(json.dumps(out), flush=True)
+    drp_dist.close_comms()
     ctx.close()
     if dist:
         torch.distributed.destroy_process_group()

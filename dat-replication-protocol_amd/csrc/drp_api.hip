@@ -78,6 +78,7 @@ struct drp_ctx {
   uint32_t B = 128;
   int strict = 0;
   int exact = 0;  // 1: always the exact kernel (decode_tiles), never the speculative one
+  int key_post = 0;  // drp_decode_stage computes key hashes / key flags
   int cus = 256;
   uint32_t waves_per_cu = 16;
   DevBuf scratch, in_stage, out_stage, aux;
@@ -153,6 +154,8 @@ void drp_close(drp_ctx *c) {
 
 void *drp_stream(drp_ctx *c) { return c ? (void *)c->st : nullptr; }
 
+int drp_device(drp_ctx *c) { return c ? c->device : DRP_E_INVAL; }
+
 int drp_synchronize(drp_ctx *c) {
   if (!c) return DRP_E_INVAL;
   CHK(hipStreamSynchronize(c->st));
@@ -176,6 +179,12 @@ int drp_set_tile(drp_ctx *c, uint32_t tile_bytes) {
 int drp_set_exact(drp_ctx *c, int exact) {
   if (!c) return DRP_E_INVAL;
   c->exact = exact ? 1 : 0;
+  return DRP_OK;
+}
+
+int drp_set_key_post(drp_ctx *c, int on) {
+  if (!c) return DRP_E_INVAL;
+  c->key_post = on ? 1 : 0;
   return DRP_OK;
 }
 
@@ -320,6 +329,7 @@ int run_decode_exact_once(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, con
   CHK(hipEventRecord(c->ev[2], st));
   CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
                           scount, fr->type, co->flags, cap, res, st));
+  CHK(drp_launch_key_post(bytes, tile_prefix, ns, P.tile_base, P.tile_count, cap, fr, co, st));
   CHK(hipEventRecord(c->ev[3], st));
   uint32_t h[2];
   CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
@@ -478,6 +488,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     CHK(hipEventRecord(c->ev[2], st));
     CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
                             scount, fr->type, co->flags, cap, res, st));
+    CHK(drp_launch_key_post(bytes, tile_prefix, ns, P.tile_base, P.tile_count, cap, fr, co, st));
   } else {
     CHK(hipEventRecord(c->ev[2], st));
   }
@@ -552,8 +563,9 @@ void carve(DevBuf &b, uint64_t cap, drp_frames &fr, drp_changes &co) {
   co.from = (uint64_t *)take(cap * 8);
   co.to = (uint64_t *)take(cap * 8);
   co.flags = (uint8_t *)take(cap);
+  co.key_hash = (uint64_t *)take(cap * 8);
 }
-size_t carve_bytes(uint64_t cap) { return 13 * 256 + cap * 62; }
+size_t carve_bytes(uint64_t cap) { return 14 * 256 + cap * 70; }
 
 }  // namespace
 
@@ -639,6 +651,7 @@ static int decode_batch_device_out(drp_ctx *c, const uint8_t *bytes, uint64_t n,
     dco.from = cols->from + nf0;
     dco.to = cols->to + nf0;
     dco.flags = cols->flags + nf0;
+    dco.key_hash = cols->key_hash ? cols->key_hash + nf0 : nullptr;
   } else {
     if (!c->out_stage.ensure(carve_bytes(cap_rest))) return DRP_E_NOMEM;
     carve(c->out_stage, cap_rest, dfr, dco);
@@ -735,6 +748,7 @@ static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry 
   for (int attempt = 0; attempt < 2; attempt++) {
     if (!c->dec_cols.ensure(carve_bytes(cap))) return DRP_E_NOMEM;
     carve(c->dec_cols, cap, S.fr, S.co);
+    if (!c->key_post) S.co.key_hash = nullptr;
     S.cap = cap;
     rc = run_decode(c, dbytes, m, soff, ent, 1, &S.fr, &S.co, cap, dres);
     if (rc != DRP_OK && rc != DRP_E_CAPACITY) return rc;
@@ -796,6 +810,10 @@ static int fetch_staged(drp_ctx *c, const drp_frames *frames, const drp_changes 
     CHK(cp(cols->from, S.co.from, 8));
     CHK(cp(cols->to, S.co.to, 8));
     CHK(cp(cols->flags, S.co.flags, 1));
+    if (cols->key_hash) {
+      if (!S.co.key_hash) return DRP_E_INVAL;  // not computed: drp_set_key_post(ctx, 1) first
+      CHK(cp(cols->key_hash, S.co.key_hash, 8));
+    }
     CHK(hipStreamSynchronize(st));
     if (S.shift)
       for (uint64_t i = 0; i < ng; i++) frames->payload_off[dst + i] += S.shift;
@@ -825,7 +843,10 @@ int drp_decode_batch(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *ca
   if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
   if (is_device_ptr(frames->payload_off)) return decode_batch_device_out(c, bytes, n, carry, frames, cols, cap,
                                                                          n_frames, err_frame, err_code, err_detail);
+  const int key_post = c->key_post;
+  c->key_post = cols->key_hash != nullptr;  // key hashes when the caller asks for them
   int rc = stage_decode(c, bytes, n, carry, n_frames, err_frame, err_code, err_detail);
+  c->key_post = key_post;
   if (rc != DRP_OK) return rc;
   const uint64_t rows = c->staged.rows;
   rc = fetch_staged(c, frames, cols, 0, rows < cap ? rows : cap);

@@ -96,6 +96,10 @@ hipError_t drp_launch_finalize(const uint8_t *bytes, const uint64_t *stream_off,
                                const uint8_t *type, const uint8_t *flags, uint64_t cap,
                                drp_stream_result *res, hipStream_t st);
 hipError_t drp_launch_encode(const drp::EncodeParams *P, hipStream_t st);
+// key hash + key flags for every change frame written (no-op when co->key_hash is NULL)
+hipError_t drp_launch_key_post(const uint8_t *bytes, const uint64_t *tile_prefix, uint64_t nstreams,
+                               const uint64_t *tile_base, const uint64_t *tile_count, uint64_t cap,
+                               const drp_frames *fr, const drp_changes *co, hipStream_t st);
 hipError_t drp_launch_index_scan(const drp_stream_stats *stats, uint64_t count, uint64_t *base,
                                  hipStream_t st);
 hipError_t drp_launch_stats_from_results(const drp_stream_result *res, const uint64_t *stream_off,

@@ -13,11 +13,14 @@
  * calls are serialised by a mutex (one HIP stream and one scratch set per device context).
  *
  *   open(device)                                 -> ctx (external)
- *   decode(ctx, buf, blobRemaining, cb)          -> cb(err, {n, errFrame, errCode, errDetail,
+ *   decode(ctx, buf, blobRemaining, cb[, keyPost])
+ *                                                -> cb(err, {n, errFrame, errCode, errDetail,
  *                                                   consumed, tailKind, blobRemaining, frameBytes,
  *                                                   off, len, type, ko, kl, so, sl, vo, vl,
- *                                                   change, from, to, flags})
- *   decodeSync(ctx, buf, blobRemaining)          -> the same object (blocks the JS thread)
+ *                                                   change, from, to, flags[, keyHash]})
+ *                                                   keyPost: also keyHash (BigUint64Array, XXH64
+ *                                                   of each key) and the key flags 0x10 / 0x20
+ *   decodeSync(ctx, buf, blobRemaining[, keyPost]) -> the same object (blocks the JS thread)
  *   encode(ctx, heap, n, 10 column arrays, cb)   -> cb(err, Buffer of wire bytes)
  *
  * Host columns are sized from the decoded frame count (drp_decode_stage, then
@@ -114,18 +117,23 @@ typedef struct {
   uint32_t ec, ed;
   drp_carry carry;
   void *col[NCOL];
+  int key_post;   /* also the key hash column + key flags (drp_set_key_post) */
+  void *khash;
 } dec_job;
 
-static void free_cols(void **col) {
+static void free_cols(dec_job *j) {
   for (int i = 0; i < NCOL; i++) {
-    free(col[i]);
-    col[i] = NULL;
+    free(j->col[i]);
+    j->col[i] = NULL;
   }
+  free(j->khash);
+  j->khash = NULL;
 }
 
 /* the GPU part: decode, size the host columns from the frame count, fetch (worker thread) */
 static void dec_run(dec_job *j) {
   pthread_mutex_lock(&j->box->mu);
+  drp_set_key_post(j->box->c, j->key_post);
   j->rc = drp_decode_stage(j->box->c, j->bytes, j->n, &j->carry, &j->nf, &j->ef, &j->ec, &j->ed);
   if (j->rc == DRP_OK) {
     /* rows to expose: delivered frames plus a malformed Change (its flags say why) */
@@ -134,16 +142,17 @@ static void dec_run(dec_job *j) {
       j->col[i] = malloc(j->rows * COL_W[i] + 8);
       if (!j->col[i]) j->rc = DRP_E_NOMEM;
     }
+    if (j->key_post && !(j->khash = malloc(j->rows * 8 + 8))) j->rc = DRP_E_NOMEM;
     if (j->rc == DRP_OK) {
       drp_frames fr = {j->col[C_OFF], j->col[C_LEN], j->col[C_TYPE]};
       drp_changes co = {j->col[C_KO], j->col[C_KL], j->col[C_SO], j->col[C_SL], j->col[C_VO],
-                        j->col[C_VL], j->col[C_CH], j->col[C_FR], j->col[C_TO], j->col[C_FL]};
+                        j->col[C_VL], j->col[C_CH], j->col[C_FR], j->col[C_TO], j->col[C_FL], j->khash};
       j->rc = drp_decode_fetch(j->box->c, &fr, &co, 0, j->rows);
     }
   }
   pthread_mutex_unlock(&j->box->mu);
   if (j->rc != DRP_OK) {
-    free_cols(j->col);
+    free_cols(j);
     return;
   }
   /* u64 -> JS Number, in place (varint.decode yields Numbers) */
@@ -188,6 +197,14 @@ static napi_value dec_result(napi_env env, dec_job *j) {
     if (napi_create_typedarray(env, COL_T[i], j->rows, ab, 0, &ta) != napi_ok) return NULL;
     napi_set_named_property(env, res, COL_NAME[i], ta);
   }
+  if (j->khash) {
+    napi_value ab, ta;
+    if (napi_create_external_arraybuffer(env, j->khash, j->rows * 8 + 8, free_finalizer, NULL, &ab) != napi_ok)
+      return NULL;
+    j->khash = NULL;
+    if (napi_create_typedarray(env, napi_biguint64_array, j->rows, ab, 0, &ta) != napi_ok) return NULL;
+    napi_set_named_property(env, res, "keyHash", ta);
+  }
   return res;
 }
 
@@ -212,7 +229,7 @@ static void dec_complete(napi_env env, napi_status status, void *data) {
       argv[1] = undef;
     }
   }
-  free_cols(j->col);
+  free_cols(j);
   napi_delete_reference(env, j->buf_ref);
   napi_delete_reference(env, j->cb_ref);
   napi_delete_async_work(env, j->work);
@@ -221,7 +238,7 @@ static void dec_complete(napi_env env, napi_status status, void *data) {
 }
 
 static dec_job *dec_args(napi_env env, napi_callback_info info, size_t want, napi_value *argv) {
-  size_t argc = want;
+  size_t argc = want + 1; /* + optional keyPost */
   if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < want) {
     napi_throw_type_error(env, NULL, want == 4 ? "decode(ctx, buffer, blobRemaining, cb)"
                                                : "decodeSync(ctx, buffer, blobRemaining)");
@@ -240,11 +257,16 @@ static dec_job *dec_args(napi_env env, napi_callback_info info, size_t want, nap
   }
   j->bytes = (const uint8_t *)bytes;
   j->carry.blob_remaining = (uint64_t)brem;
+  if (argc > want) {
+    bool kp = false;
+    napi_get_value_bool(env, argv[want], &kp);
+    j->key_post = kp;
+  }
   return j;
 }
 
 static napi_value js_decode(napi_env env, napi_callback_info info) {
-  napi_value argv[4];
+  napi_value argv[5];
   dec_job *j = dec_args(env, info, 4, argv);
   if (!j) return NULL;
   napi_value name;
@@ -257,14 +279,14 @@ static napi_value js_decode(napi_env env, napi_callback_info info) {
 }
 
 static napi_value js_decode_sync(napi_env env, napi_callback_info info) {
-  napi_value argv[3];
+  napi_value argv[4];
   dec_job *j = dec_args(env, info, 3, argv);
   if (!j) return NULL;
   dec_run(j);
   napi_value res = NULL;
   if (j->rc != DRP_OK) throw_rc(env, "decode", j->rc);
   else if (!(res = dec_result(env, j))) napi_throw_error(env, NULL, "drp addon: result allocation failed");
-  free_cols(j->col);
+  free_cols(j);
   free(j);
   return res;
 }

@@ -27,6 +27,7 @@ var MAX_FRAME = require('buffer').constants.MAX_LENGTH
 var TYPE_MASK = 0x3f
 var CONT = 0x40
 var PARTIAL = 0x80
+var KEY_ASCII = 0x10 // key flags, only set when key post-processing is on
 var TAIL_HEADER = 1
 var TAIL_CHANGE = 2
 
@@ -77,9 +78,14 @@ var ERRORS = {
   5: function () { return 'Decoded message is not valid' }
 }
 
-function Decoder () {
-  if (!(this instanceof Decoder)) return new Decoder()
+// opts (not in the reference, whose constructor takes none):
+//   keyHash: true  - every change object also carries keyHash, the XXH64 of its key bytes as
+//                    a BigInt, computed on the GPU (drp_keys.hip); ASCII keys then become
+//                    strings through the latin1 decoder (the same string, without UTF-8 work)
+function Decoder (opts) {
+  if (!(this instanceof Decoder)) return new Decoder(opts)
   stream.Writable.call(this)
+  this._keyPost = !!(opts && opts.keyHash)
 
   this.destroyed = false
   this.bytes = 0
@@ -206,7 +212,7 @@ Decoder.prototype._kick = function () {
   var self = this
   native.decode(this._ctx, batch, this._blobLeft, function (err, res) {
     self._ondecoded(err, res, batch)
-  })
+  }, this._keyPost)
 }
 
 Decoder.prototype._ondecoded = function (err, res, batch) {
@@ -262,14 +268,16 @@ Decoder.prototype._deliver = function (i) {
   if ((type & TYPE_MASK) === 1) {
     // messages.Change.decode result shape: {subset, key, change, from, to, value}
     var flags = res.flags[i]
+    var ko = off + res.ko[i]
     var change = {
       subset: (flags & 1) ? buf.toString('utf8', off + res.so[i], off + res.so[i] + res.sl[i]) : '',
-      key: buf.toString('utf8', off + res.ko[i], off + res.ko[i] + res.kl[i]),
+      key: buf.toString((flags & KEY_ASCII) ? 'latin1' : 'utf8', ko, ko + res.kl[i]),
       change: res.change[i],
       from: res.from[i],
       to: res.to[i],
       value: (flags & 2) ? buf.slice(off + res.vo[i], off + res.vo[i] + res.vl[i]) : null
     }
+    if (res.keyHash) change.keyHash = res.keyHash[i]
     this.changes++
     this._onchange(change, this._up())
     return

@@ -15,17 +15,22 @@ LIB_PATH = os.environ.get("DRP_LIB") or os.path.join(PKG, "lib", "libdrp.so")
 
 DRP_OK, DRP_E_INVAL, DRP_E_HIP, DRP_E_NOMEM, DRP_E_CAPACITY, DRP_E_NODEV = 0, -1, -2, -3, -4, -5
 TYPE_CHANGE, TYPE_BLOB, FRAME_CONT, FRAME_PARTIAL = 1, 2, 0x40, 0x80
-F_SUBSET, F_VALUE, F_BAD, F_MISSING = 1, 2, 4, 8
+F_SUBSET, F_VALUE, F_BAD, F_MISSING, F_KEY_ASCII, F_KEY_UTF8 = 1, 2, 4, 8, 0x10, 0x20
 ERR_NONE, ERR_TYPE, ERR_LEN, ERR_VARINT, ERR_CHANGE, ERR_REQUIRED = 0, 1, 2, 3, 4, 5
 TAIL_NONE, TAIL_HEADER, TAIL_CHANGE, TAIL_BLOB = 0, 1, 2, 3
 
 EXPORTS = [
     "drp_abi_version", "drp_open", "drp_close", "drp_stream", "drp_synchronize",
-    "drp_last_timing", "drp_set_tile", "drp_set_strict", "drp_set_exact", "drp_decode_scratch_bytes",
+    "drp_last_timing", "drp_set_tile", "drp_set_strict", "drp_set_exact", "drp_set_key_post",
+    "drp_decode_scratch_bytes",
     "drp_decode_device", "drp_decode_batch", "drp_decode_stage", "drp_decode_fetch",
     "drp_encode_size", "drp_encode_device",
-    "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results",
+    "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results", "drp_device",
+    "drp_comm_id", "drp_comm_init_rank", "drp_comm_init_all", "drp_comm_destroy",
+    "drp_index_allgather", "drp_index_allgather_multi",
 ]
+DRP_E_COMM = -7
+COMM_ID_BYTES = 128
 
 P = C.c_void_p
 U64, U32 = C.c_uint64, C.c_uint32
@@ -37,7 +42,7 @@ class Frames(C.Structure):
 
 class Changes(C.Structure):
     _fields_ = [(k, P) for k in ["key_off", "key_len", "subset_off", "subset_len", "value_off",
-                                 "value_len", "change", "from_", "to", "flags"]]
+                                 "value_len", "change", "from_", "to", "flags", "key_hash"]]
 
 
 class ChangeSrc(C.Structure):
@@ -86,6 +91,7 @@ def lib():
         L.drp_set_tile.argtypes = [P, U32]
         L.drp_set_strict.argtypes = [P, C.c_int]
         L.drp_set_exact.argtypes = [P, C.c_int]
+        L.drp_set_key_post.argtypes = [P, C.c_int]
         L.drp_decode_scratch_bytes.argtypes = [P, U64, U64]
         L.drp_decode_scratch_bytes.restype = U64
         L.drp_decode_device.argtypes = [P, P, U64, P, P, U64, C.POINTER(Frames),
@@ -102,11 +108,21 @@ def lib():
                                        C.POINTER(U64)]
         L.drp_index_scan.argtypes = [P, P, U64, P]
         L.drp_stream_stats_from_results.argtypes = [P, P, P, U64, P]
+        L.drp_device.argtypes = [P]
+        L.drp_comm_id.argtypes = [P]
+        L.drp_comm_init_rank.argtypes = [P, P, C.c_int, C.c_int, C.POINTER(P)]
+        L.drp_comm_init_all.argtypes = [C.POINTER(P), C.c_int, C.POINTER(P)]
+        L.drp_comm_destroy.argtypes = [P]
+        L.drp_comm_destroy.restype = None
+        L.drp_index_allgather.argtypes = [P, P, P, U64, P, P]
+        L.drp_index_allgather_multi.argtypes = [C.POINTER(P), C.POINTER(P), C.c_int, C.POINTER(P), U64,
+                                                C.POINTER(P), C.POINTER(P)]
         for f in ["drp_open", "drp_synchronize", "drp_last_timing", "drp_set_tile",
-                  "drp_set_strict", "drp_set_exact", "drp_decode_device", "drp_decode_batch",
+                  "drp_set_strict", "drp_set_exact", "drp_set_key_post", "drp_decode_device", "drp_decode_batch",
                   "drp_decode_stage", "drp_decode_fetch", "drp_encode_size",
                   "drp_encode_device", "drp_encode_batch", "drp_index_scan",
-                  "drp_stream_stats_from_results"]:
+                  "drp_stream_stats_from_results", "drp_device", "drp_comm_id", "drp_comm_init_rank",
+                  "drp_comm_init_all", "drp_index_allgather", "drp_index_allgather_multi"]:
             getattr(L, f).restype = C.c_int
         _lib = L
     return _lib
@@ -131,9 +147,11 @@ COLS32 = ["key_off", "key_len", "subset_off", "subset_len", "value_off", "value_
 COLS64 = ["change", "from", "to"]
 
 
-def alloc_host_outputs(cap):
+def alloc_host_outputs(cap, key_hash=False):
     o = {"payload_off": np.zeros(cap, np.uint64), "payload_len": np.zeros(cap, np.uint32),
          "type": np.zeros(cap, np.uint8), "flags": np.zeros(cap, np.uint8)}
+    if key_hash:
+        o["key_hash"] = np.zeros(cap, np.uint64)
     for k in COLS32:
         o[k] = np.zeros(cap, np.uint32)
     for k in COLS64:
@@ -144,7 +162,7 @@ def alloc_host_outputs(cap):
 def _structs(o, ptr):
     fr = Frames(ptr(o["payload_off"]), ptr(o["payload_len"]), ptr(o["type"]))
     co = Changes(*[ptr(o[k]) for k in COLS32], ptr(o["change"]), ptr(o["from"]), ptr(o["to"]),
-                 ptr(o["flags"]))
+                 ptr(o["flags"]), ptr(o["key_hash"]) if o.get("key_hash") is not None else None)
     return fr, co
 
 
@@ -211,12 +229,14 @@ class Ctx:
         return t
 
     # ---- host-buffer batch decode (the N-API addon's path) -----------------------------
-    def decode_batch(self, wire, blob_remaining=0, cap=None):
+    def decode_batch(self, wire, blob_remaining=0, cap=None, key_hash=False):
+        """drp_decode_batch into host columns; key_hash=True also asks for the key hash
+        column and the DRP_F_KEY_ASCII / DRP_F_KEY_UTF8 flags."""
         w = np.frombuffer(bytes(wire), np.uint8) if not isinstance(wire, np.ndarray) else wire
         n = int(w.size)
         if cap is None:
             cap = n // 2 + 2
-        o = alloc_host_outputs(cap)
+        o = alloc_host_outputs(cap, key_hash)
         fr, co = _structs(o, _p)
         carry = Carry(blob_remaining, 0, 0, 0, 0)
         nf, ef, ec, ed = U64(), U64(), U32(), U32()
@@ -299,3 +319,31 @@ class Ctx:
         _chk("drp_encode_batch", self.L.drp_encode_batch(self.h, C.byref(src), _p(hb), int(h.size), n,
                                                          _p(out), int(total.value), C.byref(written)))
         return out[:int(written.value)].tobytes()
+
+
+class Comm:
+    """An RCCL communicator owned by libdrp (drp_comm_*): one rank per process."""
+
+    def __init__(self, ctx, comm_id, nranks, rank):
+        self.L = lib()
+        h = P()
+        _chk("drp_comm_init_rank", self.L.drp_comm_init_rank(ctx.h, comm_id, nranks, rank, C.byref(h)))
+        self.h, self.nranks, self.rank = h, nranks, rank
+
+    @staticmethod
+    def new_id():
+        buf = C.create_string_buffer(COMM_ID_BYTES)
+        _chk("drp_comm_id", lib().drp_comm_id(buf))
+        return buf.raw
+
+    def allgather_index(self, ctx, local_t, global_t, base_t):
+        """drp_index_allgather over torch CUDA tensors (int64 (per_rank, 4) local stats)."""
+        ctx.order_after_torch(local_t)
+        tp = lambda t: C.c_void_p(t.data_ptr())
+        _chk("drp_index_allgather", self.L.drp_index_allgather(ctx.h, self.h, tp(local_t), local_t.shape[0],
+                                                               tp(global_t), tp(base_t)))
+
+    def close(self):
+        if self.h:
+            self.L.drp_comm_destroy(self.h)
+            self.h = None

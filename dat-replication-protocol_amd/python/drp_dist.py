@@ -1,11 +1,16 @@
 """Multi-GPU sharding of independent replication streams.
 
-One process per GPU (torch.distributed; backend "nccl" is RCCL over xGMI on ROCm, "gloo"
-in the CPU tests). Streams are sharded in contiguous blocks, so the all-gathered per-stream
-stats table is already in global stream order and its exclusive prefix over `frames` is
-the global index of every stream's first frame. The gather of the 32-byte
-`drp_stream_stats` records is the only collective: the data path itself never crosses
-ranks (weak scaling).
+One process per GPU, launched by torch.distributed. Streams are sharded in contiguous blocks,
+so the all-gathered per-stream stats table is already in global stream order and its
+exclusive prefix over `frames` is the global index of every stream's first frame. The gather
+of the 32-byte `drp_stream_stats` records is the only collective: the data path itself never
+crosses ranks (weak scaling).
+
+Two transports for that one gather:
+- `global_index_rccl`: libdrp's own RCCL communicator (drp_index_allgather, the C ABI a Node
+  or C host uses too); torch.distributed only hands the RCCL unique id to every rank.
+- `gather_stats` + `global_index_device`: torch.distributed's all_gather ("gloo" in the CPU
+  tests and for rehearsing several ranks on one GPU, where RCCL refuses duplicate devices).
 """
 import ctypes as C
 
@@ -78,3 +83,41 @@ def local_stats_device(ctx, results_t, stream_off_t):
                                                  C.c_void_p(stats.data_ptr())))
         _chk("drp_synchronize", ctx.L.drp_synchronize(ctx.h))
     return stats
+
+
+_comms = {}
+
+
+def comm_for(ctx, group=None):
+    """libdrp's RCCL communicator for this process group (created once): rank 0 makes the
+    unique id, torch.distributed broadcasts its bytes, every rank joins with its ctx."""
+    from drp_amd import Comm
+    key = (id(group), ctx.h.value)
+    if key not in _comms:
+        obj = [Comm.new_id() if dist.get_rank(group) == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        _comms[key] = Comm(ctx, obj[0], dist.get_world_size(group), dist.get_rank(group))
+    return _comms[key]
+
+
+def close_comms():
+    for c in _comms.values():
+        c.close()
+    _comms.clear()
+
+
+def global_index_rccl(ctx, local_stats, nstreams, group=None):
+    """All-gather of the (n_local, 4) int64 CUDA stats through drp_index_allgather (RCCL) and
+    the global index scan on this GPU; returns (table, base) in global stream order."""
+    world = dist.get_world_size(group)
+    slots = per_rank_slots(nstreams, world)
+    dev = local_stats.device
+    send = torch.zeros((slots, STATS_WORDS), dtype=torch.int64, device=dev)
+    send[: local_stats.shape[0]] = local_stats
+    table = torch.empty((world * slots, STATS_WORDS), dtype=torch.int64, device=dev)
+    base = torch.empty(world * slots, dtype=torch.int64, device=dev)
+    comm_for(ctx, group).allgather_index(ctx, send, table, base)
+    keep = [torch.arange(r * slots, r * slots + (hi - lo), device=dev)
+            for r, (lo, hi) in ((r, shard_range(nstreams, world, r)) for r in range(world))]
+    idx = torch.cat(keep) if keep else torch.zeros(0, dtype=torch.int64, device=dev)
+    return table[idx], base[idx]

@@ -45,6 +45,7 @@ extern "C" {
 #define DRP_E_CAPACITY (-4) /* output capacity too small */
 #define DRP_E_NODEV (-5)    /* no gfx950 device */
 #define DRP_E_RETRY (-6)    /* internal: speculation failed and strict re-run also failed */
+#define DRP_E_COMM (-7)     /* RCCL error (multi-GPU index) */
 
 /* ---- frame types (the id byte, decode.js:146-161) ------------------------ */
 #define DRP_TYPE_CHANGE 1
@@ -57,6 +58,9 @@ extern "C" {
 #define DRP_F_VALUE 0x02  /* optional bytes value = 6 present (value may be empty) */
 #define DRP_F_BAD 0x04    /* payload is not a well-formed Change (see err codes) */
 #define DRP_F_MISSING 0x08 /* with DRP_F_BAD: a required field (key/change/from/to) is missing */
+/* key post-processing (only when drp_changes.key_hash is non-NULL / drp_set_key_post is on): */
+#define DRP_F_KEY_ASCII 0x10 /* every key byte < 0x80 */
+#define DRP_F_KEY_UTF8 0x20  /* the key bytes are well-formed UTF-8 (so toString('utf-8') is lossless) */
 
 /* ---- stream error codes (first failing frame, see DESIGN.md "policy") ---- */
 #define DRP_ERR_NONE 0
@@ -89,6 +93,9 @@ typedef struct drp_changes {
   uint32_t *value_off, *value_len;
   uint64_t *change, *from, *to;
   uint8_t *flags;
+  /* optional (NULL = not computed): XXH64 (seed 0) of the key bytes; when set, flags also get
+   * DRP_F_KEY_ASCII / DRP_F_KEY_UTF8 (decode.js:210-213 builds a string of every key) */
+  uint64_t *key_hash;
 } drp_changes;
 
 /* Encoder input: one Change per row; offsets are absolute into `heap`. */
@@ -155,6 +162,8 @@ int drp_open(int device, drp_ctx **out);
 void drp_close(drp_ctx *ctx);
 /* The hipStream_t (as void*) all kernels of this ctx are launched on. */
 void *drp_stream(drp_ctx *ctx);
+/* The HIP device of this ctx. */
+int drp_device(drp_ctx *ctx);
 int drp_synchronize(drp_ctx *ctx);
 int drp_last_timing(drp_ctx *ctx, drp_timing *out);
 /* Tunables (0 = default 8192). tile_bytes is 4096 or 8192 (64 lanes x 64 or 128 bytes). */
@@ -163,6 +172,9 @@ int drp_set_tile(drp_ctx *ctx, uint32_t tile_bytes);
  * speculate-and-verify kernel and fall back to the exact one when a prediction fails.
  * Results are identical either way; drp_timing.strict_reruns reports a fallback. */
 int drp_set_exact(drp_ctx *ctx, int exact);
+/* 1: drp_decode_stage also computes the key hash / key flags (fetched when the caller's
+ * drp_changes.key_hash is non-NULL); 0 (default): it does not. */
+int drp_set_key_post(drp_ctx *ctx, int on);
 /* Look-back composes exact inclusive exits only, never the per-tile maps agg_t. Test hook. */
 int drp_set_strict(drp_ctx *ctx, int strict);
 /* Device scratch bytes needed to decode `n` bytes split into `nstreams` streams. */
@@ -228,6 +240,30 @@ int drp_index_scan(drp_ctx *ctx, const drp_stream_stats *stats, uint64_t count, 
 int drp_stream_stats_from_results(drp_ctx *ctx, const drp_stream_result *results,
                                   const uint64_t *stream_off, uint64_t nstreams,
                                   drp_stream_stats *stats);
+
+/* ---- multi-GPU all-gather over RCCL ----------------------- */
+/* The only collective of the codec: independent streams are sharded across GPUs (contiguous
+ * blocks of stream ids), each GPU decodes its block (drp_decode_device) and builds its stats
+ * (drp_stream_stats_from_results); the records are all-gathered (ncclAllGather over xGMI)
+ * and scanned on every GPU into the global index of each stream's first frame.
+ * No reference counterpart (the reference is one stream on one thread). */
+#define DRP_COMM_ID_BYTES 128
+typedef struct drp_comm drp_comm;
+/* One process per GPU: rank 0 creates the id (ncclGetUniqueId), the launcher hands the bytes
+ * to every rank, each rank joins with its ctx. */
+int drp_comm_id(uint8_t *id /* [DRP_COMM_ID_BYTES] */);
+int drp_comm_init_rank(drp_ctx *ctx, const uint8_t *id, int nranks, int rank, drp_comm **out);
+/* One process driving ngpu devices: one comm per ctx (ncclCommInitAll). */
+int drp_comm_init_all(drp_ctx **ctxs, int ngpu, drp_comm **comms);
+void drp_comm_destroy(drp_comm *comm);
+/* local[per_rank] -> global[nranks * per_rank] (rank order) and base[nranks * per_rank]: the
+ * exclusive prefix of frames = the global index of every stream's first frame (a short block
+ * is padded with zero records). Device pointers; returns after completion. */
+int drp_index_allgather(drp_ctx *ctx, drp_comm *comm, const drp_stream_stats *local, uint64_t per_rank,
+                        drp_stream_stats *global, uint64_t *base);
+/* The same for ngpu contexts in one process (one grouped all-gather). */
+int drp_index_allgather_multi(drp_ctx **ctxs, drp_comm **comms, int ngpu, const drp_stream_stats *const *local,
+                              uint64_t per_gpu, drp_stream_stats *const *global, uint64_t *const *base);
 
 #ifdef __cplusplus
 }

@@ -4,6 +4,7 @@
 //   mode "async": change/blob callbacks acknowledged on setImmediate
 //   mode "destroy": async acks, and decoder.destroy() inside the n-th change callback
 //   mode "digest": events carry sha256 of keys/values/blob data instead of hex
+//   mode "keyhash": decode({keyHash: true}); change events also carry keyHash (decimal)
 'use strict'
 var fs = require('fs')
 var path = require('path')
@@ -20,11 +21,13 @@ function enc (b) {
   return digest ? crypto.createHash('sha256').update(b).digest('hex').slice(0, 16) : b.toString('hex')
 }
 var out = []
-var d = protocol.decode()
+var d = protocol.decode(mode === 'keyhash' ? { keyHash: true } : undefined)
 var seen = 0
 d.change(function (c, cb) {
-  out.push({ t: 'change', subset: enc(Buffer.from(c.subset, 'utf8')), key: enc(Buffer.from(c.key, 'utf8')),
-    change: c.change, from: c.from, to: c.to, value: c.value === null ? null : enc(c.value) })
+  var ev = { t: 'change', subset: enc(Buffer.from(c.subset, 'utf8')), key: enc(Buffer.from(c.key, 'utf8')),
+    change: c.change, from: c.from, to: c.to, value: c.value === null ? null : enc(c.value) }
+  if (mode === 'keyhash') ev.keyHash = c.keyHash.toString()
+  out.push(ev)
   if (mode === 'destroy' && ++seen === nth) {
     d.destroy()
     setTimeout(done, 200) // anything delivered after destroy() would land before this

@@ -198,3 +198,32 @@ def test_c3_blobs_through_the_package():
         got = [e for e in run_js(wire, sizes, mode) if e["t"] != "close"]
         assert got[:-1] == exp
         assert got[-1] == {"t": "finish", "changes": r["changes"], "blobs": r["blobs"], "bytes": len(wire)}
+
+
+@pytest.mark.gpu
+@needs_node
+def test_decoder_key_hash_option():
+    """decode({keyHash: true}) (f4): every change also carries the GPU's XXH64 of its key bytes,
+    equal to python-xxhash; the events are otherwise the reference's (ASCII keys go through the
+    latin1 path, invalid UTF-8 keys still become U+FFFD strings like toString('utf-8'))."""
+    import xxhash
+    rng = random.Random(12)
+    keys = [b"plain", "été".encode(), b"\xff\xfebad", b"x" * 40, b""]
+    wire = b"".join(S.frame(S.change_payload(keys[i % len(keys)] + str(i).encode(), i, 0, 1, value=b"v"))
+                    for i in range(500)) + S.random_stream(rng, 300)
+    r, exp = oracle_events(wire)
+    got = [e for e in run_js(wire, "65536", "keyhash") if e["t"] != "close"]
+    assert got[-1]["t"] == "finish"
+    for g, e in zip(got[:-1], exp):
+        h = g.pop("keyHash", None)
+        assert g == e
+        if e["t"] == "change":
+            assert h is not None
+    # hashes of the raw key bytes (not of the decoded strings)
+    hashes = [int(e["keyHash"]) for e in run_js(wire, "65536", "keyhash") if e["t"] == "change"]
+    raw = []
+    for k in range(r["nframes"]):
+        if r["type"][k] & 0x3F == 1:
+            po, ko, kl = int(r["payload_off"][k]), int(r["key_off"][k]), int(r["key_len"][k])
+            raw.append(xxhash.xxh64_intdigest(wire[po + ko:po + ko + kl]))
+    assert hashes == raw
