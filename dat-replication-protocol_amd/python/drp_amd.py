@@ -253,7 +253,7 @@ class Ctx:
                    frame_bytes=int(carry.frame_bytes))
         return res
 
-    def decode_staged(self, wire, blob_remaining=0, pieces=1):
+    def decode_staged(self, wire, blob_remaining=0, pieces=1, key_hash=False):
         """drp_decode_stage, then drp_decode_fetch of the rows in `pieces` consecutive
         fetches into host columns sized from the frame count (the N-API addon's path)."""
         w = np.frombuffer(bytes(wire), np.uint8) if not isinstance(wire, np.ndarray) else wire
@@ -261,10 +261,11 @@ class Ctx:
         carry = Carry(blob_remaining, 0, 0, 0, 0)
         nf, ef, ec, ed = U64(), U64(), U32(), U32()
         buf = w if n else np.zeros(16, np.uint8)
+        _chk("drp_set_key_post", self.L.drp_set_key_post(self.h, 1 if key_hash else 0))
         _chk("drp_decode_stage", self.L.drp_decode_stage(self.h, _p(buf), n, C.byref(carry), C.byref(nf),
                                                          C.byref(ef), C.byref(ec), C.byref(ed)))
         rows = int(nf.value) + (1 if ec.value in (ERR_CHANGE, ERR_REQUIRED) else 0)
-        o = alloc_host_outputs(rows)
+        o = alloc_host_outputs(rows, key_hash)
         bounds = np.linspace(0, rows, pieces + 1).astype(np.int64)
         for a, b in zip(bounds[:-1], bounds[1:]):
             part = {k: v[a:] for k, v in o.items()}

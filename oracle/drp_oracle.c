@@ -245,7 +245,8 @@ typedef struct {
   int id;
   int64_t missing;
   uint8_t *buffer; /* _buffer: partial change payload (non-fast-track) */
-  uint64_t buffer_len;
+  uint64_t buffer_len, buffer_cap;
+  int in_change_buffer; /* _buffer != null */
   int in_blob; /* _blob != null */
   /* bookkeeping for the SoA view */
   uint64_t abs;         /* absolute offset of the next byte to be written */
@@ -310,8 +311,7 @@ static void onchangeend(oracle_dec *d, const uint8_t *payload) {
     d->to[f] = c.to;
     d->flags[f] = c.flags;
   }
-  free(d->buffer);
-  d->buffer = NULL;
+  d->in_change_buffer = 0;
   d->buffer_len = 0;
   if (c.err) {
     /* policy: the reference throws out of _write; we stop after the earlier frames */
@@ -384,24 +384,40 @@ static uint64_t onblobdata(oracle_dec *d, uint64_t len) {
 }
 
 /* _onchangedata (decode.js:216-249). Returns bytes consumed. */
+/* The reference allocates Buffer(_missing) up front (decode.js:227); the restatement grows its
+ * buffer with the bytes that actually arrive, so a frame that declares a huge length and is
+ * cut by EOF costs only what was received. Returns 0 when the buffer cannot grow. */
+static int grow(oracle_dec *d, uint64_t need) {
+  if (need <= d->buffer_cap) return 1;
+  uint64_t cap = d->buffer_cap ? d->buffer_cap : 64;
+  while (cap < need) cap *= 2;
+  if (cap > (uint64_t)d->missing + d->buffer_len) cap = (uint64_t)d->missing + d->buffer_len;
+  uint8_t *b = (uint8_t *)realloc(d->buffer, (size_t)cap);
+  if (!b) return 0;
+  d->buffer = b;
+  d->buffer_cap = cap;
+  return 1;
+}
+
 static uint64_t onchangedata(oracle_dec *d, const uint8_t *data, uint64_t len) {
-  if (!d->buffer) { /* fast track: the whole payload is in this slice */
+  if (!d->in_change_buffer) { /* fast track: the whole payload is in this slice */
     if ((int64_t)len >= d->missing) {
       uint64_t used = (uint64_t)d->missing;
       onchangeend(d, data);
       return used;
     }
-    d->buffer = (uint8_t *)malloc(d->missing > 0 ? (size_t)d->missing : 1);
+    d->in_change_buffer = 1;
     d->buffer_len = 0;
   }
-  if ((int64_t)len < d->missing) {
-    memcpy(d->buffer + d->buffer_len, data, len);
-    d->buffer_len += len;
-    d->missing -= (int64_t)len;
+  uint64_t used = (int64_t)len < d->missing ? len : (uint64_t)d->missing;
+  if (!grow(d, d->buffer_len + used)) {
+    destroy(d, DRP_ERR_CHANGE, 0); /* out of memory: treated as a malformed frame */
     return len;
   }
-  uint64_t used = (uint64_t)d->missing;
-  memcpy(d->buffer + d->buffer_len, data, used);
+  if (used) memcpy(d->buffer + d->buffer_len, data, used);
+  d->buffer_len += used;
+  d->missing -= (int64_t)used;
+  if (d->missing > 0) return used;
   onchangeend(d, d->buffer);
   return used;
 }

@@ -63,9 +63,7 @@ def test_key_hash_and_flags(ctx, kernel):
         ctx.set_exact(True)
     try:
         if kernel == "staged":
-            ctx.L.drp_set_key_post(ctx.h, 1)
-            g = ctx.decode_staged(wire, pieces=3)
-            ctx.L.drp_set_key_post(ctx.h, 0)
+            g = ctx.decode_staged(wire, pieces=3, key_hash=True)
         else:
             g = ctx.decode_batch(wire, key_hash=True)
     finally:
