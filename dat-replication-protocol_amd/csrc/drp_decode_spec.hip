@@ -38,9 +38,20 @@
 namespace drp {
 namespace spec {
 
-constexpr int NT = 128;                       // threads per workgroup
+#ifndef DRP_SPEC_NT
+#define DRP_SPEC_NT 128
+#endif
+constexpr int NT = DRP_SPEC_NT;               // threads per workgroup (64: one wave, no s_barrier)
 constexpr uint32_t SEGB = 64;                 // bytes per thread
-constexpr uint32_t TILE = NT * SEGB;          // 8 KiB: the B = 128 tile geometry of tile_prefix
+constexpr uint32_t TILE = NT * SEGB;          // 8 KiB (4 KiB at NT 64): the B = NT tile geometry of tile_prefix
+static_assert(NT == 64 || NT == 128, "one or two waves per tile");
+
+// Workgroup barrier. A one-wave workgroup needs none: its LDS accesses complete in issue order,
+// so only the compiler must not move LDS accesses across this point (and earlier ones retire).
+__device__ __forceinline__ void bsync() {
+  if constexpr (NT == 64) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  else __syncthreads();
+}
 constexpr uint32_t HALO = 512;
 constexpr uint32_t IMG = TILE + HALO;         // LDS image bytes (+32 slack)
 #ifndef DRP_VALIDATE_ALL
@@ -57,6 +68,9 @@ constexpr uint32_t IMG = TILE + HALO;         // LDS image bytes (+32 slack)
 #endif
 #ifndef DRP_KSTRONG
 #define DRP_KSTRONG 4
+#endif
+#ifndef DRP_ABLATE
+#define DRP_ABLATE 0  // measurement builds only: spec_claims stops after phase N (output invalid)
 #endif
 constexpr int KSTRONG = DRP_KSTRONG;                    // frames a candidate chain must survive
 constexpr uint64_t RDY = 1ull << 63;          // published word: value | RDY
@@ -271,7 +285,7 @@ void link(const Img &m, uint64_t s1, uint64_t g, uint64_t e_first, uint64_t &E,
       if (lane >= d && x == NONE) x = y;
     }
     if (lane == 63) wl[wid] = x;
-    __syncthreads();  // (A) wl of this round visible; fl reads of the last round are done
+    bsync();  // (A) wl of this round visible; fl reads of the last round are done
     uint64_t prev = VERIFY ? e_first : NONE;  // latest carrier exit before this wave
 #pragma unroll
     for (uint32_t w = 0; w < NWV; w++)
@@ -282,13 +296,23 @@ void link(const Img &m, uint64_t s1, uint64_t g, uint64_t e_first, uint64_t &E,
     const uint64_t En = VERIFY ? ex : (rs ? g : ex);
     if (restart) *restart = rs;
     const bool ch = En != E;
-    const uint64_t any = __ballot(ch);
+    // only carriers feed the scan: a thread that neither is nor becomes one (its bytes lie
+    // inside a frame that jumps over it) takes the passing exit without another round
+    const bool relevant = ch && (carrier || (is_pos(En) && En < s1));
+    const uint64_t any = __ballot(relevant);
     if (lane == 0) fl[wid] = any != 0;
-    __syncthreads();  // (B) fl visible; wl reads of this round are done
+    bsync();  // (B) fl visible; wl reads of this round are done
     uint32_t more = 0;
 #pragma unroll
     for (uint32_t w = 0; w < NWV; w++) more |= fl[w];
-    if (!more) break;
+    if (!more) {
+      if (ch) {  // a non-carrier passes the exit on (walk returns it unchanged, no frames)
+        E = En;
+        R = En;
+        n = 0;
+      }
+      break;
+    }
     if (round > NT + 2) {  // cannot happen: entries settle thread by thread
       if (tid == 0) atomicOr(overflow, F_WAIT);
       break;
@@ -306,11 +330,11 @@ __device__ __forceinline__ uint32_t block_max_u32(uint32_t v, uint32_t *xf) {
 #pragma unroll
   for (uint32_t k = 1; k < WAVE; k <<= 1) v = max(v, shfl_xor32(v, k));
   if (lane == 0) xf[wid] = v;
-  __syncthreads();
+  bsync();
   uint32_t r = 0;
 #pragma unroll
   for (uint32_t w = 0; w < NT / WAVE; w++) r = max(r, xf[w]);
-  __syncthreads();
+  bsync();
   return r;
 }
 // two maxima with one exchange (scratch: 2 * NT / WAVE words)
@@ -325,13 +349,13 @@ __device__ __forceinline__ void block_max2_u32(uint32_t &a, uint32_t &b, uint32_
     xf[wid] = a;
     xf[NT / WAVE + wid] = b;
   }
-  __syncthreads();
+  bsync();
 #pragma unroll
   for (uint32_t w = 0; w < NT / WAVE; w++) {
     a = max(a, xf[w]);
     b = max(b, xf[NT / WAVE + w]);
   }
-  __syncthreads();
+  bsync();
 }
 // bits strictly above bit j of the 128-bit mask (m0 low, m1 high) exist
 __device__ __forceinline__ bool any_above(uint64_t m0, uint64_t m1, uint32_t j) {
@@ -349,11 +373,11 @@ __device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t *xf) {
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   v = wave_sum32(v);
   if (lane == 0) xf[wid] = v;
-  __syncthreads();
+  bsync();
   uint32_t r = 0;
 #pragma unroll
   for (uint32_t w = 0; w < NT / WAVE; w++) r += xf[w];
-  __syncthreads();
+  bsync();
   return r;
 }
 
@@ -420,7 +444,7 @@ __device__ __forceinline__ void stage(const DecodeParams &P, const TileGeo &G, u
   for (int k = 0; k < (int)(SEGB / 16); k++) *reinterpret_cast<uint4 *>(buf + tid * SEGB + 16 * k) = v[k];
   if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = h;
   if (tid < 2) *reinterpret_cast<uint4 *>(buf + IMG + tid * 16) = make_uint4(0, 0, 0, 0);
-  __syncthreads();
+  bsync();
 }
 
 // Stage the tile (64 B per thread, coalesced dwordx4) and its halo into LDS; returns the
@@ -435,7 +459,7 @@ __device__ __forceinline__ uint64_t stage_live(const DecodeParams &P, const Tile
   for (int k = 0; k < (int)(SEGB / 16); k++) *reinterpret_cast<uint4 *>(buf + tid * SEGB + 16 * k) = v[k];
   if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = hv;
   if (tid < 2) *reinterpret_cast<uint4 *>(buf + IMG + tid * 16) = make_uint4(0, 0, 0, 0);
-  __syncthreads();
+  bsync();
   uint32_t m16[5], s16[5];
 #pragma unroll
   for (int k = 0; k < 4; k++) gather16(v[k], m16[k], s16[k]);
@@ -471,7 +495,7 @@ __device__ __forceinline__ uint64_t stage_live(const DecodeParams &P, const Tile
 
 // ==== kernel 1: every tile's claim (entry-independent, no waiting) ===========================
 #ifndef DRP_LLCAP
-#define DRP_LLCAP 1024
+#define DRP_LLCAP (8 * DRP_SPEC_NT)  // 1024 live positions per 8 KiB tile (C2 has ~220)
 #endif
 constexpr uint32_t LLCAP = DRP_LLCAP;  // live positions per tile checked through the LDS list
 constexpr uint16_t NX_NEAR = 0xFFFD, NX_FAR = 0xFFFE, NX_DEAD = 0xFFFF;
@@ -483,7 +507,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   __shared__ uint64_t lmw[NT];
   __shared__ uint16_t loff[NT];
   __shared__ uint32_t xf2[2 * NT / WAVE];
-  __shared__ uint64_t xm[2 * NT / WAVE];  // candidate masks: [w] strong, [NWV + w] strong and far
+  __shared__ uint64_t xm[4];  // candidate masks (two waves): [w] strong, [2 + w] strong and far
   __shared__ uint16_t lpos[LLCAP], lnx[LLCAP];
   __shared__ uint8_t lal[LLCAP];
   const uint32_t tid = threadIdx.x;
@@ -497,6 +521,10 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   const Img m{buf, P.bytes, G.A, G.se};
   const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
   PHASE(0);
+#if DRP_ABLATE == 1
+  if (tid == 0) P.claim[t] = __builtin_popcountll(live);  // (measurement build: stage + live mask only)
+  return;
+#endif
 
   // ---- strong candidate: the first live position whose chain survives, preferring chains
   // that can be checked inside the LDS image (shadow headers whose varint swallows a real
@@ -513,7 +541,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   const uint32_t cpre = wave_incl_scan32(cnt);
   if (lane == 63) xf[wid] = cpre;
   lmw[tid] = live;
-  __syncthreads();
+  bsync();
   uint32_t off = cpre - cnt, total = 0;
 #pragma unroll
   for (uint32_t w = 0; w < NT / WAVE; w++) {
@@ -521,7 +549,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
     total += xf[w];
   }
   loff[tid] = (uint16_t)off;
-  __syncthreads();  // (xf is reused below)
+  bsync();  // (xf is reused below)
   if (total <= LLCAP) {
     {
       uint64_t bits = live;
@@ -531,22 +559,39 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
         bits &= bits - 1;
       }
     }
-    __syncthreads();
+    bsync();
+    // tile-relative 32-bit arithmetic: the stream end as an offset from A (clamped), and the
+    // one-byte-length header (every C2 frame) parsed inline; longer varints take parse_win
+    const uint32_t se_rel = (uint32_t)umin64(G.se - G.A, 0x7FFFFFFFull);
     for (uint32_t i = tid; i < total; i += NT) {
-      const uint64_t p = G.A + (lpos[i] & 0x7FFFu);
-      const Hdr h = m.at(p);
+      const uint32_t o = lpos[i] & 0x7FFFu;
+      uint64_t w0, w1;
+      lds_win16(buf, o, w0, w1);  // o < TILE: the 16-byte window is inside the image
+      bool valid, near;  // near: the frame ends at or past the stream end
+      uint32_t sr;       // successor offset from A (saturated)
+      const uint32_t b0 = (uint32_t)(w0 & 0xFFu), id = (uint32_t)((w0 >> 8) & 0xFFu);
+      if (b0 < 0x80u && se_rel - o >= 2u) {  // same grammar as parse_win's one-byte branch
+        sr = id == 0 ? o + 2u : o + 1u + b0;
+        valid = id < 3u && (id == 0 || (b0 != 0 && b0 <= se_rel - o - 1u));
+        near = sr >= se_rel;  // (se_rel is exact whenever it can be reached from here)
+      } else {
+        const Hdr h = parse_win(w0, w1, G.A + o, G.se);
+        valid = h.kind == H_VALID;
+        sr = (uint32_t)umin64(h.succ - G.A, 0xFFFFFFFFull);
+        near = h.succ >= G.se;
+      }
       uint16_t code = NX_DEAD;
       uint8_t a = 0;
-      if (h.kind == H_VALID && h.succ >= G.A + TILE) lpos[i] |= 0x8000u;  // first frame leaves the tile
-      if (h.kind == H_VALID && (DRP_LIST_PLAUSIBLE == 0 || plausible(m, p, h, false))) {
-        if (h.succ >= G.se) {
+      if (valid && sr >= TILE) lpos[i] |= 0x8000u;  // first frame leaves the tile
+      if (valid && (DRP_LIST_PLAUSIBLE == 0 || plausible(m, G.A + o, m.at(G.A + o), false))) {
+        if (near) {
           code = NX_NEAR;  // the stream end: survived
           a = 1;
-        } else if (h.succ >= G.A + TILE) {
+        } else if (sr >= TILE) {
           code = NX_FAR;   // past the tile: undecided (a restart that needs it checks in HBM)
           a = 2;
         } else {
-          const uint32_t q = (uint32_t)(h.succ - G.A), th = q / SEGB, b = q % SEGB;
+          const uint32_t q = sr, th = q / SEGB, b = q % SEGB;
           const uint64_t lw = lmw[th];
           if ((lw >> b) & 1ull) {
             code = (uint16_t)(loff[th] + __builtin_popcountll(lw & ((1ull << b) - 1)));
@@ -557,7 +602,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
       lnx[i] = code;
       lal[i] = a;
     }
-    __syncthreads();
+    bsync();
     for (int r = 1; r < KSTRONG; r++) {
       for (uint32_t i = tid; i < total; i += NT) {
         const uint16_t v = lnx[i];
@@ -566,7 +611,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
           if (b != 1) lal[i] = b;  // dead or undecided downstream
         }
       }
-      __syncthreads();
+      bsync();
     }
     // this thread's first strong position; undecided ones are deferred
     for (uint32_t i = off; i < off + cnt; i++) {
@@ -578,6 +623,10 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
       }
       if (a == 2) defer |= 1ull << ((lpos[i] & 0x7FFFu) - tid * SEGB);
     }
+#if DRP_ABLATE == 2
+    if (tid == 0) P.claim[t] = g;  // (measurement build: + list survival)
+    return;
+#endif
     if (g != NONE) R = walk<true>(m, g, s1, n);
   } else {  // very dense tile: per-thread checks
     uint64_t bits = live;
@@ -603,16 +652,21 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   // survives any number of frames, but it jumps over the tile's real (dense) chain. The
   // tile-wide candidate masks (128 bits) are exchanged once; the survivors' mask S is then
   // known to every thread without further barriers.
-  static_assert(NT == 2 * WAVE, "candidate masks are two words");
   uint64_t S0, S1;
   {
     const uint64_t hm = __ballot(g != NONE), fm = __ballot(g != NONE && far);
-    if (lane == 0) {
-      xm[wid] = hm;
-      xm[2 + wid] = fm;
+    uint64_t H0 = hm, H1 = 0, F0 = fm, F1 = 0;  // one wave: its own ballots are the tile's masks
+    if constexpr (NT == 2 * WAVE) {
+      if (lane == 0) {
+        xm[wid] = hm;
+        xm[2 + wid] = fm;
+      }
+      bsync();
+      H0 = xm[0];
+      H1 = xm[1];
+      F0 = xm[2];
+      F1 = xm[3];
     }
-    __syncthreads();
-    const uint64_t H0 = xm[0], H1 = xm[1], F0 = xm[2], F1 = xm[3];
     const uint64_t L1 = H1 ? ((1ull << (63 - __builtin_clzll(H1))) - 1) : 0ull;  // below the top bit
     const uint64_t L0 = H1 ? ~0ull : (H0 ? ((1ull << (63 - __builtin_clzll(H0))) - 1) : 0ull);
     S0 = H0 & ~(F0 & L0);
@@ -626,6 +680,10 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   uint64_t E = g;
   bool rs = false;  // this thread restarts the chain (no chain enters it, or the entering one died)
   PHASE(1);
+#if DRP_ABLATE == 3
+  if (tid == 0) P.claim[t] = R + E;  // (measurement build: + own walk and masks)
+  return;
+#endif
   // ---- link the threads' chains ------------------------------------------------------------
   link<false>(m, s1, g, NONE, E, R, n, xr, xf, P.overflow, &rs);
   // A thread no chain reaches and without an LDS-decided candidate, with none later in the
@@ -660,6 +718,10 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
     block_max2_u32(need, js, xf2);
   }
   PHASE(2);
+#if DRP_ABLATE == 4
+  if (tid == 0) P.claim[t] = R + E;  // (measurement build: + link and HBM restarts)
+  return;
+#endif
   // The chain's last frame may jump over threads that hold strong candidates: a shadow that
   // joined the chain can jump far and land on a real frame start past the tile. Build the
   // chain those candidates start as well and keep it when it is the denser one (>= 2
@@ -718,8 +780,18 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
   if (t >= ntiles) return;  // (whole workgroup)
   const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
+  // every load this tile needs goes out first (their latencies overlap)
+  const uint64_t ix = t * NT + tid;
+  const uint8_t eb = P.ent[ix];
+  const uint8_t en = P.ent_n[ix], ecn = P.ent_c[ix];
+  const uint64_t claim = P.claim[t];
+  const uint64_t cprev = t != G.tf ? P.claim[t - 1] : C_ID;
   PHASE(8);
-  if (wid == 0) {
+  if (t != G.tf && cprev != C_ID) {
+    // the common case: the previous tile's claim is its exit (a published incl_e of a
+    // non-identity tile always equals its claim), so e_t needs no look-back
+    if (tid == 0) sh_e = cprev;
+  } else if (wid == 0) {
     uint64_t e = G.e0;
     if (t != G.tf) {
       int64_t j0 = (int64_t)t - 1;
@@ -743,17 +815,14 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     }
     if (lane == 0) sh_e = e;
   }
-  __syncthreads();
+  bsync();
   const uint64_t et = sh_e;
-  const uint64_t claim = P.claim[t];
   if (tid == NT - 1) st_agent(&P.incl_e[t], (claim == C_ID ? et : claim) | RDY);
   PHASE(9);
   // Fast check from kernel 1's per-thread records (no tile bytes): when the thread holding e_t
   // has e_t as its predicted entry and no later thread restarted the predicted chain, the
   // walks from there on are the exact walks (same entries, and no prediction-only deaths), so
   // the predicted entries, counts and exit are exact.
-  const uint64_t ix = t * NT + tid;
-  const uint8_t eb = P.ent[ix];
   const bool inside = is_pos(et) && et < G.A + TILE;
   const uint32_t k = inside ? (uint32_t)((et - G.A) / SEGB) : NT;
   uint32_t bad = 0;
@@ -764,7 +833,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   }
   // one exchange: any thread disagrees (max), and the fast path's frame and change counts
   const bool mine = tid >= k && eb != 0xFF;
-  uint32_t cnt_f = mine ? P.ent_n[ix] : 0u, cnt_c = mine ? P.ent_c[ix] : 0u;
+  uint32_t cnt_f = mine ? en : 0u, cnt_c = mine ? ecn : 0u;
   {
     cnt_f = wave_sum32(cnt_f);
     cnt_c = wave_sum32(cnt_c);
@@ -774,7 +843,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
       xr[wid] = ((uint64_t)cnt_c << 32) | cnt_f;
       xf[wid] = bad;
     }
-    __syncthreads();
+    bsync();
     uint64_t acc = 0;
     uint32_t b = 0;
 #pragma unroll
@@ -782,7 +851,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
       acc += xr[w];
       b = max(b, xf[w]);
     }
-    __syncthreads();
+    bsync();
     cnt_f = (uint32_t)acc;
     cnt_c = (uint32_t)(acc >> 32);
     bad = b;
@@ -817,9 +886,9 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     // the last thread's R is the tile's exact exit; it must be what the claim predicted (an
     // error on the exact chain never is: predictions restart after errors)
     xr[0] = 0;
-    __syncthreads();
+    bsync();
     if (tid == NT - 1) xr[0] = R;
-    __syncthreads();
+    bsync();
     const uint64_t Rl = xr[0];
     exit_t = (Rl & MARK_TERM) ? (Rl & ~M_ERR) : Rl;
     const uint64_t want = claim == C_ID ? et : claim;
@@ -924,7 +993,10 @@ __global__ __launch_bounds__(SCAN_BLK) void scan_down(const uint64_t *cnt, const
 // ==== kernel 3: emission ========================================================================
 // Frame-major: the tile's frame starts go to an LDS list (thread order = stream order), then
 // thread i decodes frames i, i + NT, ... so every column store is a contiguous run.
-constexpr uint32_t LCAP = 1024;  // frames per tile listed in LDS (denser tiles emit per thread)
+#ifndef DRP_LCAP
+#define DRP_LCAP 1024
+#endif
+constexpr uint32_t LCAP = DRP_LCAP;  // frames per tile listed in LDS (denser tiles emit per thread)
 
 __device__ __noinline__ ChangeCols decode_change_hbm(const uint8_t *g, uint64_t se, uint64_t po, uint64_t pl) {
   const GlobalReader gr{g, se};
@@ -972,17 +1044,19 @@ __global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P)
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
   if (t >= ntiles) return;  // (whole workgroup)
   const uint64_t se = G.se, A = G.A;
+  // the records load with the tile bytes, not after them
+  const uint64_t base = P.tile_base[t];
+  const uint8_t eb = P.ent[t * NT + tid];     // exact entry of this thread's bytes (kernel 2)
+  const uint8_t en = P.ent_n[t * NT + tid];   // exact frames from it (kernel 2)
   stage(P, G, buf);
   const Img m{buf, P.bytes, A, se};
   const uint64_t lb = A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
-  const uint64_t base = P.tile_base[t];
-  const uint8_t eb = P.ent[t * NT + tid];  // exact entry of this thread's bytes (kernel 2)
   const uint64_t E = !(eb & 0x80) ? lb + (eb & 63) : NONE;
   PHASE(11);
-  const uint32_t n = (eb & 0x80) ? 0u : P.ent_n[t * NT + tid];  // exact frames from E (kernel 2)
+  const uint32_t n = (eb & 0x80) ? 0u : en;
   const uint32_t ni = wave_incl_scan32(n);
   if (lane == 63) wsum[wid] = ni;
-  __syncthreads();
+  bsync();
   uint32_t woff = 0, count_t = 0;
 #pragma unroll
   for (int w = 0; w < NT / WAVE; w++) {
@@ -1010,7 +1084,7 @@ __global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P)
     }
   }
   if (listed) {
-    __syncthreads();
+    bsync();
     for (uint32_t i = tid; i < count_t; i += NT) emit_frame(P, m, A + lst[i], base + i, nch, nbl, badf);
   }
   PHASE(13);
