@@ -440,8 +440,8 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.cap = cap;
   P.claim = rec;
   P.incl_e = rec + NT;
-  P.agg_n = rec + 2 * NT;
-  P.incl_n = rec + 3 * NT;
+  P.work = reinterpret_cast<uint32_t *>(rec + 2 * NT);
+  P.work_n = ctrl + 2;
   P.tile_exit = tiles;
   P.tile_base = tiles + NT;
   P.tile_count = tiles + 2 * NT;

@@ -69,6 +69,9 @@ constexpr uint32_t IMG = TILE + HALO;         // LDS image bytes (+32 slack)
 #ifndef DRP_KSTRONG
 #define DRP_KSTRONG 4
 #endif
+#ifndef DRP_CLAIMS_FAST
+#define DRP_CLAIMS_FAST 1  // 0: the general claims kernel for every tile (A/B)
+#endif
 #ifndef DRP_ABLATE
 #define DRP_ABLATE 0  // measurement builds only: spec_claims stops after phase N (output invalid)
 #endif
@@ -512,18 +515,23 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   __shared__ uint8_t lal[LLCAP];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wid = tid >> 6;
-  const uint64_t t = blockIdx.x;
   uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  // With a work list (the fast kernel ran first): the edge and dense tiles it listed, a few per
+  // workgroup; without one: every tile, one per workgroup.
+  const uint32_t nwork = P.work ? *P.work_n : 0u;
+  for (uint32_t wi = blockIdx.x; P.work ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
+  const uint64_t t = P.work ? P.work[wi] : wi;
+  bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
-  if (t >= ntiles) return;  // (whole workgroup)
+  if (t >= ntiles) continue;  // (whole workgroup)
   const uint64_t live = stage_live(P, G, buf);
   const Img m{buf, P.bytes, G.A, G.se};
   const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
   PHASE(0);
 #if DRP_ABLATE == 1
   if (tid == 0) P.claim[t] = __builtin_popcountll(live);  // (measurement build: stage + live mask only)
-  return;
+  continue;
 #endif
 
   // ---- strong candidate: the first live position whose chain survives, preferring chains
@@ -625,7 +633,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
     }
 #if DRP_ABLATE == 2
     if (tid == 0) P.claim[t] = g;  // (measurement build: + list survival)
-    return;
+    continue;
 #endif
     if (g != NONE) R = walk<true>(m, g, s1, n);
   } else {  // very dense tile: per-thread checks
@@ -682,7 +690,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   PHASE(1);
 #if DRP_ABLATE == 3
   if (tid == 0) P.claim[t] = R + E;  // (measurement build: + own walk and masks)
-  return;
+  continue;
 #endif
   // ---- link the threads' chains ------------------------------------------------------------
   link<false>(m, s1, g, NONE, E, R, n, xr, xf, P.overflow, &rs);
@@ -720,7 +728,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
   PHASE(2);
 #if DRP_ABLATE == 4
   if (tid == 0) P.claim[t] = R + E;  // (measurement build: + link and HBM restarts)
-  return;
+  continue;
 #endif
   // The chain's last frame may jump over threads that hold strong candidates: a shadow that
   // joined the chain can jump far and land on a real frame start past the tile. Build the
@@ -762,6 +770,414 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
     P.ent_c[ix] = carrier ? (uint8_t)(n >> 16) : (uint8_t)0;
   }
   if (tid == NT - 1) P.claim[t] = (R == NONE || ((R & MARK_TERM) && (R & M_ERR))) ? C_ID : R;
+  }
+}
+
+// ==== kernel 1, fast form: claims of interior tiles ============================================
+// Same outputs as spec_claims (claim, per-thread entry records), for the tiles whose LDS image
+// [A, A + IMG) lies inside their stream: no stream-start masking, every in-tile header window is
+// inside the image and the stream, and all arithmetic is 32-bit and tile-relative. Differences in
+// what is *predicted* (never in what is output: verification is exact):
+//  * live positions are those of 1..3-byte length varints (frames < 2 MiB); a longer frame's
+//    header is no candidate, so a tile whose chain holds one mispredicts and is repaired;
+//  * a change frame behind a multi-byte varint that ends inside the image must start with a
+//    Change field tag (subset, key, change, from, to, value), not hold a well-formed Change;
+//  * every live position is parsed once into an LDS node (successor node and offset, type);
+//    chain walks and the threads' link rounds follow nodes and never re-parse a header;
+//  * the link's "latest carrier" lookup is a ballot + one lane permute, not a shuffle scan.
+// Edge tiles and tiles with more than FCAP live positions are appended to a work list for the
+// general kernel, which runs after this one.
+#ifndef DRP_FCAP
+#define DRP_FCAP 512
+#endif
+constexpr uint32_t FCAP = DRP_FCAP;
+constexpr uint16_t NX_TAILB = 0xFFFB, NX_TAILC = 0xFFFC;  // the node's frame runs past the stream end
+// Chain exits (32-bit): a node index | its offset << 16 (offset < TILE), or one of
+constexpr uint32_t RX_NONE = 0xFFFFFFFFu;  // no chain
+constexpr uint32_t RX_DEAD = 0xFFFFFFFEu;  // the chain died (invalid header)
+constexpr uint32_t RX_FAR = 0x40000000u;   // | node: that node's frame ends past the tile (or at the stream end)
+constexpr uint32_t RX_TERM = 0x20000000u;  // | node: that node's frame is cut by the stream end (tail)
+__device__ __forceinline__ bool rx_node(uint32_t x) { return x < RX_TERM; }
+__device__ __forceinline__ uint32_t rx_off(uint32_t x) { return x >> 16; }  // (nodes only)
+
+// 16-byte block -> bit k = MSB of byte k (m), bit k = byte k <= 2 (s); v_dot4 gathers the bits
+__device__ __forceinline__ uint32_t le2_bytes(uint32_t x) { return ~(((x | 0x80808080u) - 0x03030303u) | x) & 0x80808080u; }
+__device__ __forceinline__ uint32_t gather_msb(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint32_t lo = __builtin_amdgcn_udot4(a, 0x08040201u, __builtin_amdgcn_udot4(b, 0x80402010u, 0u, false), false);
+  const uint32_t hi = __builtin_amdgcn_udot4(c, 0x08040201u, __builtin_amdgcn_udot4(d, 0x80402010u, 0u, false), false);
+  return (lo >> 7) | (hi << 1);  // (both are 128 x an 8-bit mask)
+}
+__device__ __forceinline__ uint32_t masks16(const uint4 v) {  // m | s << 16
+  constexpr uint32_t H = 0x80808080u;
+  const uint32_t m = gather_msb(v.x & H, v.y & H, v.z & H, v.w & H);
+  const uint32_t s = gather_msb(le2_bytes(v.x), le2_bytes(v.y), le2_bytes(v.z), le2_bytes(v.w));
+  return m | (s << 16);
+}
+
+// inclusive prefix sum over the wave (DPP: row shifts, then row broadcasts)
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return v;
+}
+
+// Node word: successor code (node index or NX_*) | min(successor offset, 0x3FFF) << 16 | id << 30
+// (id 3: the node's own header is invalid).
+// Walk from node exit x (offset < s1r) through the thread's bytes: returns the exit (a node whose
+// offset is >= s1r, or RX_*); n = frames delivered | change frames << 16.
+__device__ __forceinline__ uint32_t fwalk(const uint32_t *lnd, uint32_t x, uint32_t s1r, uint32_t &n) {
+  n = 0;
+  uint32_t i = x & 0xFFFFu;
+#pragma unroll 1
+  for (;;) {
+    const uint32_t nd = lnd[i], id = nd >> 30, c = nd & 0xFFFFu, q = (nd >> 16) & 0x3FFFu;
+    if (id == 3) return RX_DEAD;
+    if (c == NX_TAILC) return RX_TERM | i;  // a change frame cut by the stream end is not delivered
+    n += 1u + ((id == 1) << 16) - (id == 0);
+    if (c == NX_TAILB) return RX_TERM | i;  // a partial blob is delivered and ends the chain
+    if (c == NX_FAR || c == NX_NEAR) return RX_FAR | i;
+    if (q >= s1r) return c == NX_DEAD ? RX_DEAD : (c | (q << 16));
+    if (c == NX_DEAD) return RX_DEAD;
+    i = c;
+  }
+}
+
+// Link rounds (spec mode of link()): a thread's entry is the exit of the latest carrier before it;
+// no carrier, or a dead one, restarts the chain at the thread's own strong node g.
+__device__ __forceinline__ void flink(const uint32_t *lnd, uint32_t s1r, uint32_t g, uint32_t &E, uint32_t &R,
+                                      uint32_t &n, bool &rs, uint32_t *wl, uint32_t *fl, uint32_t *overflow) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll 1
+  for (uint32_t round = 0;; round++) {
+    const bool carrier = rx_node(E) && rx_off(E) < s1r;
+    const uint64_t cm = __ballot(carrier);
+    const uint64_t bm = cm & below;
+    const uint32_t j = bm ? 63u - (uint32_t)__builtin_clzll(bm) : 0u;
+    const uint32_t xj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)R);
+    if constexpr (NT == 2 * WAVE) {
+      if (lane == 0) wl[wid] = cm ? (uint32_t)__builtin_amdgcn_readlane((int)R, 63 - __builtin_clzll(cm)) : RX_NONE;
+      bsync();  // (A) wl visible; fl reads of the last round are done
+    }
+    const uint32_t prev = (NT == 2 * WAVE && wid == 1) ? wl[0] : RX_NONE;
+    const uint32_t ex = bm ? xj : prev;
+    const bool r = ex >= RX_DEAD;  // none or dead
+    const uint32_t En = r ? g : ex;
+    const bool ch = En != E;
+    const bool relevant = ch && (carrier || (rx_node(En) && rx_off(En) < s1r));
+    const uint64_t any = __ballot(relevant);
+    bool more = any != 0;
+    if constexpr (NT == 2 * WAVE) {
+      if (lane == 0) fl[wid] = any != 0;
+      bsync();  // (B) fl visible; wl reads of this round are done
+      more = (fl[0] | fl[1]) != 0;
+    }
+    rs = r;
+    if (!more) {
+      if (ch) {  // a non-carrier passes the exit on
+        E = En;
+        R = En;
+        n = 0;
+      }
+      break;
+    }
+    if (round > NT + 2) {  // cannot happen: entries settle thread by thread
+      if (tid == 0) atomicOr(overflow, F_WAIT);
+      break;
+    }
+    if (ch) {
+      E = En;
+      if (rx_node(E) && rx_off(E) < s1r) R = fwalk(lnd, E, s1r, n);
+      else {
+        R = E;
+        n = 0;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void push_work(const DecodeParams &P, uint64_t t) {
+  if (threadIdx.x == 0) P.work[atomicAdd(P.work_n, 1u)] = (uint32_t)t;
+}
+
+__global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+  __shared__ uint64_t lmw[NT];   // live masks; then strong masks
+  __shared__ uint64_t dmw[NT];   // undecided masks
+  __shared__ uint16_t loff[NT];  // first list index of each thread
+  __shared__ uint16_t lpos[FCAP];
+  __shared__ uint32_t lnd[FCAP > NT + 1 ? FCAP : NT + 1];  // nodes (first: the next-16-byte masks)
+  __shared__ uint8_t lal[FCAP];  // 0 dead, 1 strong, 2 undecided (leaves the image)
+  __shared__ uint32_t xw[8];
+  __shared__ uint32_t xf[2 * NT / WAVE], wl[NT / WAVE], fl[NT / WAVE];
+  __shared__ uint64_t xm[4];  // candidate masks (two waves): [w] strong, [2 + w] strong and far
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  const uint64_t t = blockIdx.x;
+  const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  const TileGeo G = tile_geo(P, t);
+  if (t >= ntiles) return;  // (whole workgroup)
+  if (G.A < G.so || G.A + IMG > G.se) {  // edge tile: the general kernel
+    push_work(P, t);
+    return;
+  }
+  // ---- stage, masks, live positions (varints of 1..3 bytes) --------------------------------
+  uint4 v[SEGB / 16], hv;
+  {
+    const uint4 *q = reinterpret_cast<const uint4 *>(P.bytes + G.A + (uint64_t)tid * SEGB);
+#pragma unroll
+    for (int k = 0; k < (int)(SEGB / 16); k++) v[k] = q[k];
+    hv = tid < HALO / 16 ? *reinterpret_cast<const uint4 *>(P.bytes + G.A + TILE + tid * 16) : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int k = 0; k < (int)(SEGB / 16); k++) *reinterpret_cast<uint4 *>(buf + tid * SEGB + 16 * k) = v[k];
+  if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = hv;
+  if (tid < 2) *reinterpret_cast<uint4 *>(buf + IMG + tid * 16) = make_uint4(0, 0, 0, 0);
+  uint32_t mk[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) mk[k] = masks16(v[k]);
+  uint32_t *mx = lnd;  // next-16-byte masks of every thread (thread NT-1: the halo's first bytes)
+  mx[tid] = mk[0];
+  if (tid == 0) mx[NT] = masks16(hv);
+  bsync();
+  const uint32_t nx = mx[tid + 1];
+  const uint64_t M0 = (uint64_t)(mk[0] & 0xFFFFu) | ((uint64_t)(mk[1] & 0xFFFFu) << 16) |
+                      ((uint64_t)(mk[2] & 0xFFFFu) << 32) | ((uint64_t)(mk[3] & 0xFFFFu) << 48);
+  const uint64_t S0 = (uint64_t)(mk[0] >> 16) | ((uint64_t)(mk[1] >> 16) << 16) | ((uint64_t)(mk[2] >> 16) << 32) |
+                      ((uint64_t)(mk[3] >> 16) << 48);
+  const uint64_t M1 = nx & 0xFFFFu, S1 = nx >> 16;
+  const uint64_t X0 = ~M0 & ((S0 >> 1) | (S1 << 63));  // varint terminator followed by an id <= 2
+  const uint64_t X1 = ~M1 & (S1 >> 1);
+  const uint64_t Xs1 = (X0 >> 1) | (X1 << 63), Xs2 = (X0 >> 2) | (X1 << 62), Ms1 = (M0 >> 1) | (M1 << 63);
+  const uint64_t live = X0 | (M0 & (Xs1 | (Ms1 & Xs2)));
+  // ---- the tile's live positions as an LDS list ------------------------------------------------
+  const uint32_t cnt = (uint32_t)__builtin_popcountll(live);
+  const uint32_t cpre = wave_scan_dpp(cnt);
+  if (lane == 63) xw[wid] = cpre;
+  lmw[tid] = live;
+  bsync();  // (also: mx reads done)
+  const uint32_t off = cpre - cnt + (wid ? xw[0] : 0u);
+  const uint32_t total = NT == 2 * WAVE ? xw[0] + xw[1] : xw[0];
+  if (total > FCAP) {  // very dense tile: the general kernel's per-thread checks
+    push_work(P, t);
+    return;
+  }
+  loff[tid] = (uint16_t)off;
+  {
+    uint64_t bits = live;
+    uint32_t i = off;
+    while (bits) {
+      lpos[i++] = (uint16_t)(tid * SEGB + (uint32_t)__builtin_ctzll(bits));
+      bits &= bits - 1;
+    }
+  }
+  bsync();
+  // ---- parse every node once --------------------------------------------------------------------
+  const uint32_t se_rel = (uint32_t)umin64(G.se - G.A, 0x7FFFFFFFull);  // >= IMG
+  constexpr uint32_t KPT = FCAP / NT;  // nodes per thread (at most)
+  uint32_t ncode[KPT], npos[KPT];
+  uint32_t na[KPT];
+  const uint32_t *w32 = reinterpret_cast<const uint32_t *>(buf);
+#pragma unroll
+  for (uint32_t j = 0; j < KPT; j++) {
+    const uint32_t i = tid + j * NT;
+    ncode[j] = NX_DEAD;
+    na[j] = 0;
+    npos[j] = 0;
+    if (i < total) {
+      const uint32_t o = lpos[i], d = o >> 2, sh = (o & 3u) * 8u;
+      const uint32_t a0 = w32[d], a1 = w32[d + 1], a2 = w32[d + 2];
+      const uint32_t w = __builtin_amdgcn_alignbit(a1, a0, sh), wn = __builtin_amdgcn_alignbit(a2, a1, sh);
+      const uint32_t tm = ~w & 0x808080u;  // live => a terminator in bytes 0..2
+      const uint32_t k = ((uint32_t)__builtin_ctz(tm | 0x80000000u) >> 3) + 1u;
+      const uint32_t L3 = (w & 0x7Fu) | ((w >> 1) & 0x3F80u) | ((w >> 2) & 0x1FC000u);
+      const uint32_t L = L3 & ((1u << (7u * k)) - 1u);
+      const uint32_t id = (w >> (8u * k)) & 0xFFu;
+      const uint32_t succ = o + k + (id ? L : 1u);
+      const uint32_t avail = se_rel - o;  // >= IMG - o
+      bool valid = id <= 2u && (id == 0u || L != 0u);
+      const bool tail = valid && id != 0u && L > avail - k;
+      uint32_t c = NX_DEAD, a = 0;
+      if (valid && !tail && id == 1u && k >= 2u && succ <= IMG) {  // Change field tag first
+        const uint32_t pb = k == 3u ? (wn & 0xFFu) : (w >> (8u * (k + 1u))) & 0xFFu;
+        constexpr uint64_t TAGS = (1ull << 0x0a) | (1ull << 0x12) | (1ull << 0x18) | (1ull << 0x20) | (1ull << 0x28) |
+                                  (1ull << 0x32);
+        valid = pb < 64u && ((TAGS >> pb) & 1ull);
+      }
+      if (!valid) {
+        c = NX_DEAD;
+      } else if (tail) {
+        c = id == 2u ? NX_TAILB : NX_TAILC;
+      } else if (succ >= se_rel) {
+        c = NX_NEAR;  // ends at the stream end: survived
+        a = 1;
+      } else if (succ >= TILE) {
+        c = NX_FAR;   // past the tile: undecided (a restart that needs it checks in HBM)
+        a = 2;
+      } else {
+        const uint32_t th = succ / SEGB, b = succ % SEGB;
+        const uint64_t lw = lmw[th];
+        if ((lw >> b) & 1ull) {
+          c = loff[th] + (uint32_t)__builtin_popcountll(lw & ((1ull << b) - 1ull));
+          a = 1;
+        }
+      }
+      lnd[i] = c | (min(succ, 0x3FFFu) << 16) | ((valid ? id : 3u) << 30);
+      lal[i] = (uint8_t)a;
+      ncode[j] = c;
+      na[j] = a;
+      npos[j] = o;
+    }
+  }
+  bsync();
+  lmw[tid] = 0;  // (now the strong masks)
+  dmw[tid] = 0;
+  // ---- survival: KSTRONG - 1 rounds propagate death / undecided back along the chains ------------
+#pragma unroll 1
+  for (int r = 1; r < KSTRONG; r++) {
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++) {
+      if (na[j] == 1u && ncode[j] < NX_NEAR) {
+        const uint32_t b = lal[ncode[j]];
+        if (b != 1u) {
+          na[j] = b;
+          lal[tid + j * NT] = (uint8_t)b;
+        }
+      }
+    }
+    bsync();
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < KPT; j++) {
+    if (na[j]) {
+      const uint32_t o = npos[j];
+      atomicOr((unsigned long long *)(na[j] == 1u ? &lmw[o / SEGB] : &dmw[o / SEGB]), 1ull << (o % SEGB));
+    }
+  }
+  bsync();
+  // ---- this thread's strong candidate g (the first strong node of its bytes) -------------------
+  const uint64_t sm = lmw[tid];
+  const uint32_t lb = tid * SEGB, s1r = lb + SEGB;
+  uint32_t g = RX_NONE;
+  uint64_t defer = dmw[tid];
+  bool far = false;
+  if (sm) {
+    const uint32_t b = (uint32_t)__builtin_ctzll(sm);
+    defer &= (1ull << b) - 1ull;
+    const uint32_t gi = off + (uint32_t)__builtin_popcountll(live & ((1ull << b) - 1ull));
+    g = gi | ((lb + b) << 16);
+    const uint32_t gc = lnd[gi] & 0xFFFFu;
+    far = gc == NX_FAR || gc == NX_NEAR;
+  }
+  uint32_t n = 0, R = RX_NONE;
+  if (g != RX_NONE) R = fwalk(lnd, g, s1r, n);
+  // rule 2: a chain that starts by jumping past the tile only where nothing later can start one
+  uint64_t S0m, S1m;
+  {
+    const uint64_t hm = __ballot(g != RX_NONE), fm = __ballot(g != RX_NONE && far);
+    uint64_t H0 = hm, H1 = 0, F0 = fm, F1 = 0;  // one wave: its own ballots are the tile's masks
+    if constexpr (NT == 2 * WAVE) {
+      if (lane == 0) {
+        xm[wid] = hm;
+        xm[2 + wid] = fm;
+      }
+      bsync();
+      H0 = xm[0];
+      H1 = xm[1];
+      F0 = xm[2];
+      F1 = xm[3];
+    }
+    const uint64_t L1 = H1 ? ((1ull << (63 - __builtin_clzll(H1))) - 1) : 0ull;  // below the top bit
+    const uint64_t L0 = H1 ? ~0ull : (H0 ? ((1ull << (63 - __builtin_clzll(H0))) - 1) : 0ull);
+    S0m = H0 & ~(F0 & L0);
+    S1m = H1 & ~(F1 & L1);
+    if (far && any_above(H0, H1, tid)) {
+      g = RX_NONE;
+      R = RX_NONE;
+      n = 0;
+    }
+  }
+  uint32_t E = g;
+  bool rs = false;
+  flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow);
+  // restarts from deferred candidates, decided in HBM (big frames), as in spec_claims
+  const Img m{buf, P.bytes, G.A, G.se};
+  uint32_t need = (E == RX_NONE && defer && !any_above(S0m, S1m, tid)) ? 1u : 0u;
+  uint32_t js = (rx_node(E) && rx_off(E) < s1r) ? tid + 1 : 0u;  // last carrier + 1
+  block_max2_u32(need, js, xf);
+  bool moved = false;
+#pragma unroll 1
+  for (uint32_t it = 0; need && it < 3; it++) {
+    moved = true;
+    if (E == RX_NONE && defer && !any_above(S0m, S1m, tid)) {
+      while (defer) {
+        const uint32_t o = (uint32_t)__builtin_ctzll(defer);
+        defer &= defer - 1;
+        uint64_t r;
+        uint32_t k;
+        bool f;
+        if (strong<false>(m, G.A + lb + o, G.A + s1r, r, k, f) == S_OK) {
+          g = (off + (uint32_t)__builtin_popcountll(live & ((1ull << o) - 1ull))) | ((lb + o) << 16);
+          E = g;
+          R = fwalk(lnd, g, s1r, n);
+          break;
+        }
+      }
+    }
+    flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow);
+    need = (E == RX_NONE && defer && !any_above(S0m, S1m, tid)) ? 1u : 0u;
+    js = (rx_node(E) && rx_off(E) < s1r) ? tid + 1 : 0u;
+    block_max2_u32(need, js, xf);
+  }
+  // rule 3: the chain's last frame may jump over threads holding strong candidates; keep the
+  // chain they start when it is the denser one (>= 2 frames)
+  {
+    bool after;
+    if (!moved) after = any_from(S0m, S1m, js);
+    else after = block_max_u32(g != RX_NONE && tid + 1 > js ? 1u : 0u, xf) != 0;
+    if (js && after) {
+      const uint32_t Ea = E, Ra = R, na0 = n;
+      const bool rsa = rs;
+      const bool mine = tid + 1 > js;
+      E = RX_NONE;
+      R = RX_NONE;
+      n = 0;
+      flink(lnd, s1r, mine ? g : RX_NONE, E, R, n, rs, wl, fl, P.overflow);
+      const uint32_t nb = block_sum_u32(mine ? (n & 0xFFFFu) : 0u, xf);
+      if (nb < 2 || !mine) {
+        E = Ea;
+        R = Ra;
+        n = na0;
+        rs = rsa;
+      }
+    }
+  }
+  // per-thread records for kernel 2 (as spec_claims) and the claim
+  {
+    const bool carrier = rx_node(E) && rx_off(E) < s1r;
+    const uint64_t ix = t * NT + tid;
+    P.ent[ix] = carrier ? (uint8_t)(((rx_off(E) - lb) & 63u) | (rs ? 0x40u : 0u)) : (uint8_t)0xFF;
+    P.ent_n[ix] = carrier ? (uint8_t)(n & 0xFFFFu) : (uint8_t)0;
+    P.ent_c[ix] = carrier ? (uint8_t)(n >> 16) : (uint8_t)0;
+  }
+  if (tid == NT - 1) {
+    uint64_t cl = C_ID;
+    if (R < RX_DEAD && !rx_node(R)) {
+      const uint64_t p = G.A + lpos[R & 0xFFFFu];
+      if (R & RX_FAR) {
+        const Hdr h = m.at(p);
+        if (h.kind == H_VALID) cl = h.succ;
+      } else {
+        cl = MARK_TERM | p;  // a tail ends the chain
+      }
+    } else if (rx_node(R)) {
+      cl = G.A + rx_off(R);
+    }
+    P.claim[t] = cl;
+  }
 }
 
 // ==== kernel 2: exact entries, verification, frame counts =====================================
@@ -1169,7 +1585,15 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
                        P->tile_prefix, nstreams, nt_max, tile_stream);
     Q.tile_stream = tile_stream;
   }
+#if DRP_CLAIMS_FAST
+  // interior tiles in the fast form; the edge and dense tiles it lists in the general one
+  hipLaunchKernelGGL(spec::claims_fast, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  const uint32_t gw = (uint32_t)(nt_max < 16384 ? nt_max : 16384);
+  hipLaunchKernelGGL(spec::spec_claims, dim3(gw), dim3(spec::NT), 0, st, Q);
+#else
+  Q.work = nullptr;
   hipLaunchKernelGGL(spec::spec_claims, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+#endif
   hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
   return hipGetLastError();
 }

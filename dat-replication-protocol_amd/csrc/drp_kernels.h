@@ -48,6 +48,8 @@ struct DecodeParams {
   const uint32_t *tile_stream;  // tile -> stream (null: one stream)
   uint8_t *ent;                 // [tile][thread]: entry offset in the thread's 64 B, 0xFF none
   uint8_t *ent_n, *ent_c;       // [tile][thread]: frames / change frames from that entry
+  uint32_t *work;               // tiles for the general claims kernel (edge / dense tiles)
+  uint32_t *work_n;             //  and their count (the fast claims kernel appends)
   uint64_t *tile_nch;           // change frames of tile t (per-stream counts come from a scan:
   uint64_t *tile_nch_base;      //  same-address atomics per tile serialise across the XCDs)
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
