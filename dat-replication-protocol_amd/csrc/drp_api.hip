@@ -507,7 +507,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   c->timing.spec_repairs = (uint32_t)pass;
   TRACE("decode_spec done: tiles=%u flags=%#x", h[0], h[1]);
   if (dstats) {
-    unsigned long long hs[56];
+    unsigned long long hs[64];
     CHK(hipMemcpy(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost));
     fprintf(stderr, "[drp-spec] misses=%llu", hs[0]);
     for (unsigned k = 0; k < 5 && k < hs[0]; k++)
@@ -517,7 +517,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
                                "k2_stage", "k2_entry", "k2_link", "k3_stage", "k3_link", "k3_emit"};
     for (int k = 0; k < 14; k++)
       if (ph[k][0]) fprintf(stderr, " %s=%.0f", ph[k], (double)hs[40 + k] / (double)(h[0] ? h[0] : 1));
-    fprintf(stderr, " repairs=%d (avg cycles per tile)\n", pass);
+    fprintf(stderr, " repairs=%d (avg cycles per tile) link_rounds=%llu\n", pass, hs[56]);
     (void)hipFree(dstats);
   }
   if (h[1] & drp_spec_retry_mask()) return DRP_E_RETRY;

@@ -69,8 +69,14 @@ constexpr uint32_t IMG = TILE + HALO;         // LDS image bytes (+32 slack)
 #ifndef DRP_KSTRONG
 #define DRP_KSTRONG 4
 #endif
+#ifndef DRP_HALO_NODES
+#define DRP_HALO_NODES 1  // 0: the fast claims kernel lists the tile's positions only (A/B)
+#endif
 #ifndef DRP_CLAIMS_FAST
 #define DRP_CLAIMS_FAST 1  // 0: the general claims kernel for every tile (A/B)
+#endif
+#ifndef DRP_ABLATE_F
+#define DRP_ABLATE_F 0  // measurement builds only: claims_fast stops after phase N (output invalid)
 #endif
 #ifndef DRP_ABLATE
 #define DRP_ABLATE 0  // measurement builds only: spec_claims stops after phase N (output invalid)
@@ -792,11 +798,12 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) 
 #endif
 constexpr uint32_t FCAP = DRP_FCAP;
 constexpr uint16_t NX_TAILB = 0xFFFB, NX_TAILC = 0xFFFC;  // the node's frame runs past the stream end
-// Chain exits (32-bit): a node index | its offset << 16 (offset < TILE), or one of
+// Chain exits (32-bit): a node index | its offset << 16 (offset < 0x4000: the tile and its halo), or
 constexpr uint32_t RX_NONE = 0xFFFFFFFFu;  // no chain
 constexpr uint32_t RX_DEAD = 0xFFFFFFFEu;  // the chain died (invalid header)
-constexpr uint32_t RX_FAR = 0x40000000u;   // | node: that node's frame ends past the tile (or at the stream end)
-constexpr uint32_t RX_TERM = 0x20000000u;  // | node: that node's frame is cut by the stream end (tail)
+constexpr uint32_t RX_FAR = 0x80000000u;   // | node: that node's frame ends past the listed positions
+constexpr uint32_t RX_TERM = 0x40000000u;  // | node: that node's frame is cut by the stream end (tail)
+static_assert(IMG < 0x4000, "node offsets are 14-bit");
 __device__ __forceinline__ bool rx_node(uint32_t x) { return x < RX_TERM; }
 __device__ __forceinline__ uint32_t rx_off(uint32_t x) { return x >> 16; }  // (nodes only)
 
@@ -849,7 +856,8 @@ __device__ __forceinline__ uint32_t fwalk(const uint32_t *lnd, uint32_t x, uint3
 // Link rounds (spec mode of link()): a thread's entry is the exit of the latest carrier before it;
 // no carrier, or a dead one, restarts the chain at the thread's own strong node g.
 __device__ __forceinline__ void flink(const uint32_t *lnd, uint32_t s1r, uint32_t g, uint32_t &E, uint32_t &R,
-                                      uint32_t &n, bool &rs, uint32_t *wl, uint32_t *fl, uint32_t *overflow) {
+                                      uint32_t &n, bool &rs, uint32_t *wl, uint32_t *fl, uint32_t *overflow,
+                                      unsigned long long *stats = nullptr) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll 1
@@ -878,6 +886,7 @@ __device__ __forceinline__ void flink(const uint32_t *lnd, uint32_t s1r, uint32_
     }
     rs = r;
     if (!more) {
+      if (stats && tid == 0) atomicAdd(&stats[56], (unsigned long long)(round + 1));  // (DRP_STATS)
       if (ch) {  // a non-carrier passes the exit on
         E = En;
         R = En;
@@ -900,15 +909,26 @@ __device__ __forceinline__ void flink(const uint32_t *lnd, uint32_t s1r, uint32_
   }
 }
 
+// measurement builds (DRP_ABLATE_F): valid "no prediction" records that keep x live
+__device__ __forceinline__ void abl_out(const DecodeParams &P, uint64_t t, uint64_t x) {
+  const uint64_t ix = t * NT + threadIdx.x;
+  P.ent[ix] = x == 0x123456789ull ? 0 : 0xFF;
+  P.ent_n[ix] = 0;
+  P.ent_c[ix] = 0;
+  if (threadIdx.x == 0) P.claim[t] = C_ID;
+}
+
 __device__ __forceinline__ void push_work(const DecodeParams &P, uint64_t t) {
   if (threadIdx.x == 0) P.work[atomicAdd(P.work_n, 1u)] = (uint32_t)t;
 }
 
 __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
-  __shared__ uint64_t lmw[NT];   // live masks; then strong masks
-  __shared__ uint64_t dmw[NT];   // undecided masks
-  __shared__ uint16_t loff[NT];  // first list index of each thread
+  constexpr uint32_t HV = DRP_HALO_NODES ? HALO / SEGB : 0;  // halo "threads" with nodes
+  __shared__ uint64_t lmw[NT + HV];   // live masks; then strong masks
+  __shared__ uint64_t dmw[NT];        // undecided masks
+  __shared__ uint16_t loff[NT + HV];  // first list index of each thread
+  __shared__ uint32_t hmx[HALO / 16 + 1];  // halo masks per 16 bytes
   __shared__ uint16_t lpos[FCAP];
   __shared__ uint32_t lnd[FCAP > NT + 1 ? FCAP : NT + 1];  // nodes (first: the next-16-byte masks)
   __shared__ uint8_t lal[FCAP];  // 0 dead, 1 strong, 2 undecided (leaves the image)
@@ -941,7 +961,12 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   for (int k = 0; k < 4; k++) mk[k] = masks16(v[k]);
   uint32_t *mx = lnd;  // next-16-byte masks of every thread (thread NT-1: the halo's first bytes)
   mx[tid] = mk[0];
-  if (tid == 0) mx[NT] = masks16(hv);
+  if (tid < HALO / 16) {
+    const uint32_t hmk = masks16(hv);
+    if (DRP_HALO_NODES) hmx[tid] = hmk;
+    if (tid == 0) mx[NT] = hmk;
+  }
+  if (DRP_HALO_NODES && tid == HALO / 16) hmx[HALO / 16] = 0xFFFFu;  // (past the image: no terminators)
   bsync();
   const uint32_t nx = mx[tid + 1];
   const uint64_t M0 = (uint64_t)(mk[0] & 0xFFFFu) | ((uint64_t)(mk[1] & 0xFFFFu) << 16) |
@@ -953,14 +978,42 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   const uint64_t X1 = ~M1 & (S1 >> 1);
   const uint64_t Xs1 = (X0 >> 1) | (X1 << 63), Xs2 = (X0 >> 2) | (X1 << 62), Ms1 = (M0 >> 1) | (M1 << 63);
   const uint64_t live = X0 | (M0 & (Xs1 | (Ms1 & Xs2)));
-  // ---- the tile's live positions as an LDS list ------------------------------------------------
+#if DRP_ABLATE_F == 1
+  abl_out(P, t, (uint64_t)(live));
+  return;
+#endif
+  // Halo nodes (DRP_HALO_NODES): the halo's live positions join the list as HV more "threads", so
+  // the survival check of the tile's last frames does not stop at the tile end (their chains
+  // would otherwise leave the list within KSTRONG frames and stay undecided, and the link would
+  // reach their threads one round at a time). Lanes 0..HV-1 of wave 0 build their masks.
+  uint64_t hlive = 0;
+  if (DRP_HALO_NODES && tid < HV) {
+    uint32_t hk[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) hk[k] = hmx[tid * 4 + k];
+    const uint64_t hM0 = (uint64_t)(hk[0] & 0xFFFFu) | ((uint64_t)(hk[1] & 0xFFFFu) << 16) |
+                         ((uint64_t)(hk[2] & 0xFFFFu) << 32) | ((uint64_t)(hk[3] & 0xFFFFu) << 48);
+    const uint64_t hS0 = (uint64_t)(hk[0] >> 16) | ((uint64_t)(hk[1] >> 16) << 16) | ((uint64_t)(hk[2] >> 16) << 32) |
+                         ((uint64_t)(hk[3] >> 16) << 48);
+    const uint64_t hM1 = hk[4] & 0xFFFFu, hS1 = hk[4] >> 16;
+    const uint64_t hX0 = ~hM0 & ((hS0 >> 1) | (hS1 << 63)), hX1 = ~hM1 & (hS1 >> 1);
+    const uint64_t hXs1 = (hX0 >> 1) | (hX1 << 63), hXs2 = (hX0 >> 2) | (hX1 << 62), hMs1 = (hM0 >> 1) | (hM1 << 63);
+    hlive = hX0 | (hM0 & (hXs1 | (hMs1 & hXs2)));
+    if (tid == HV - 1) hlive &= (1ull << (SEGB - 16)) - 1ull;  // (the image's last 16 bytes: no lookahead)
+  }
+  // ---- the tile's (and halo's) live positions as an LDS list -----------------------------------
   const uint32_t cnt = (uint32_t)__builtin_popcountll(live);
   const uint32_t cpre = wave_scan_dpp(cnt);
+  const uint32_t hcnt = (uint32_t)__builtin_popcountll(hlive);
+  const uint32_t hpre = DRP_HALO_NODES ? wave_scan_dpp(hcnt) : 0u;
   if (lane == 63) xw[wid] = cpre;
+  if (DRP_HALO_NODES && tid == 63) xw[2] = hpre;
   lmw[tid] = live;
+  if (DRP_HALO_NODES && tid < HV) lmw[NT + tid] = hlive;
   bsync();  // (also: mx reads done)
   const uint32_t off = cpre - cnt + (wid ? xw[0] : 0u);
-  const uint32_t total = NT == 2 * WAVE ? xw[0] + xw[1] : xw[0];
+  const uint32_t ttotal = NT == 2 * WAVE ? xw[0] + xw[1] : xw[0];  // the tile's nodes
+  const uint32_t total = ttotal + (DRP_HALO_NODES ? xw[2] : 0u);
   if (total > FCAP) {  // very dense tile: the general kernel's per-thread checks
     push_work(P, t);
     return;
@@ -971,6 +1024,15 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
     uint32_t i = off;
     while (bits) {
       lpos[i++] = (uint16_t)(tid * SEGB + (uint32_t)__builtin_ctzll(bits));
+      bits &= bits - 1;
+    }
+  }
+  if (DRP_HALO_NODES && tid < HV) {
+    uint64_t bits = hlive;
+    uint32_t i = ttotal + hpre - hcnt;
+    loff[NT + tid] = (uint16_t)i;
+    while (bits) {
+      lpos[i++] = (uint16_t)(TILE + tid * SEGB + (uint32_t)__builtin_ctzll(bits));
       bits &= bits - 1;
     }
   }
@@ -1014,8 +1076,8 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
       } else if (succ >= se_rel) {
         c = NX_NEAR;  // ends at the stream end: survived
         a = 1;
-      } else if (succ >= TILE) {
-        c = NX_FAR;   // past the tile: undecided (a restart that needs it checks in HBM)
+      } else if (succ >= (DRP_HALO_NODES ? IMG - 16 : TILE)) {
+        c = NX_FAR;   // past the listed positions: undecided (a restart that needs it checks in HBM)
         a = 2;
       } else {
         const uint32_t th = succ / SEGB, b = succ % SEGB;
@@ -1033,6 +1095,10 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
     }
   }
   bsync();
+#if DRP_ABLATE_F == 2
+  abl_out(P, t, (uint64_t)(ncode[0] + na[1]));
+  return;
+#endif
   lmw[tid] = 0;  // (now the strong masks)
   dmw[tid] = 0;
   // ---- survival: KSTRONG - 1 rounds propagate death / undecided back along the chains ------------
@@ -1052,7 +1118,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   }
 #pragma unroll
   for (uint32_t j = 0; j < KPT; j++) {
-    if (na[j]) {
+    if (na[j] && npos[j] < TILE) {
       const uint32_t o = npos[j];
       atomicOr((unsigned long long *)(na[j] == 1u ? &lmw[o / SEGB] : &dmw[o / SEGB]), 1ull << (o % SEGB));
     }
@@ -1072,8 +1138,16 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
     const uint32_t gc = lnd[gi] & 0xFFFFu;
     far = gc == NX_FAR || gc == NX_NEAR;
   }
+#if DRP_ABLATE_F == 3
+  abl_out(P, t, (uint64_t)(g + defer));
+  return;
+#endif
   uint32_t n = 0, R = RX_NONE;
   if (g != RX_NONE) R = fwalk(lnd, g, s1r, n);
+#if DRP_ABLATE_F == 4
+  abl_out(P, t, (uint64_t)(R + n));
+  return;
+#endif
   // rule 2: a chain that starts by jumping past the tile only where nothing later can start one
   uint64_t S0m, S1m;
   {
@@ -1102,7 +1176,11 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   }
   uint32_t E = g;
   bool rs = false;
-  flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow);
+  flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow, P.stats);
+#if DRP_ABLATE_F == 5
+  abl_out(P, t, (uint64_t)(R + E));
+  return;
+#endif
   // restarts from deferred candidates, decided in HBM (big frames), as in spec_claims
   const Img m{buf, P.bytes, G.A, G.se};
   uint32_t need = (E == RX_NONE && defer && !any_above(S0m, S1m, tid)) ? 1u : 0u;
@@ -1132,6 +1210,10 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
     js = (rx_node(E) && rx_off(E) < s1r) ? tid + 1 : 0u;
     block_max2_u32(need, js, xf);
   }
+#if DRP_ABLATE_F == 6
+  abl_out(P, t, (uint64_t)(R + E + need));
+  return;
+#endif
   // rule 3: the chain's last frame may jump over threads holding strong candidates; keep the
   // chain they start when it is the denser one (>= 2 frames)
   {
@@ -1239,7 +1321,11 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   // has e_t as its predicted entry and no later thread restarted the predicted chain, the
   // walks from there on are the exact walks (same entries, and no prediction-only deaths), so
   // the predicted entries, counts and exit are exact.
-  const bool inside = is_pos(et) && et < G.A + TILE;
+  // e_t < A: an identity-claimed tile before this one passed on an entry that lies inside it. That
+  // tile misses (an identity claim never verifies on its own entry) and is repaired, so this pass
+  // proves nothing here: no miss, no repair of this tile's claim (it is re-verified next pass).
+  const bool bogus = is_pos(et) && et < G.A;
+  const bool inside = is_pos(et) && !bogus && et < G.A + TILE;
   const uint32_t k = inside ? (uint32_t)((et - G.A) / SEGB) : NT;
   uint32_t bad = 0;
   if (inside) {
@@ -1284,7 +1370,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
       P.ent_n[ix] = 0;
     }
     exit_t = inside ? claim : et;  // pass-through tiles keep the entry
-    miss = !inside && claim != C_ID && claim != et;  // (a chain that rejoined the stream's one)
+    miss = !inside && !bogus && claim != C_ID && claim != et;  // (a chain that rejoined the stream's one)
   } else {
     const uint64_t live = stage_live(P, G, buf);
     const Img m{buf, P.bytes, G.A, G.se};
@@ -1419,9 +1505,42 @@ __device__ __noinline__ ChangeCols decode_change_hbm(const uint8_t *g, uint64_t 
   return decode_change(gr, po, pl);
 }
 
+// The header at absolute p, 32-bit fast form for 1..3-byte length varints whose 16-byte window is
+// inside the image and the stream (same results as Img::at); anything else takes Img::at.
+__device__ __forceinline__ Hdr hdr_fast(const Img &m, uint64_t p) {
+  const uint32_t o = (uint32_t)(p - m.A);
+  if (p + 16 <= m.A + IMG && p + 16 <= m.se) {
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(m.lds) + (o >> 2);
+    const uint32_t w = __builtin_amdgcn_alignbit(q[1], q[0], (o & 3u) * 8u);
+    const uint32_t tm = ~w & 0x808080u;
+    if (tm) {
+      const uint32_t k = ((uint32_t)__builtin_ctz(tm) >> 3) + 1u;
+      const uint32_t L = ((w & 0x7Fu) | ((w >> 1) & 0x3F80u) | ((w >> 2) & 0x1FC000u)) & ((1u << (7u * k)) - 1u);
+      const uint32_t id = (w >> (8u * k)) & 0xFFu;
+      Hdr h;
+      h.succ = 0;
+      h.L = L;
+      h.vlen = k;
+      h.id = id;
+      if (id >= 3u) h.kind = H_ERR_TYPE;
+      else if (id == 0u) {
+        h.kind = H_VALID;
+        h.succ = p + k + 1u;
+      } else if (L == 0u) h.kind = H_ERR_LEN;
+      else if ((uint64_t)L > m.se - p - k) h.kind = id == 1u ? H_TAIL_CHANGE : H_TAIL_BLOB;
+      else {
+        h.kind = H_VALID;
+        h.succ = p + k + L;
+      }
+      return h;
+    }
+  }
+  return m.at(p);
+}
+
 __device__ __forceinline__ void emit_frame(const DecodeParams &P, const Img &m, uint64_t p, uint64_t f,
                                            uint32_t &nch, uint32_t &nbl, uint64_t &badf) {
-  const Hdr h = m.at(p);
+  const Hdr h = hdr_fast(m, p);
   const uint64_t po = p + h.vlen + 1;
   const uint64_t pl = h.L - 1;
   if (h.id == 1) nch++; else nbl++;
@@ -1488,7 +1607,7 @@ __global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P)
     uint32_t i = woff + ni - n;
     uint64_t p = E;
     while (p < s1 && p < se) {
-      const Hdr h = m.at(p);
+      const Hdr h = hdr_fast(m, p);
       if (h.kind != H_VALID && h.kind != H_TAIL_BLOB) break;
       if (h.id != 0) {
         if (listed) lst[i] = (uint16_t)(p - A);

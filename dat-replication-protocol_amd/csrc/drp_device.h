@@ -143,10 +143,14 @@ struct LdsReader {
   __device__ __forceinline__ void win(uint64_t p, uint64_t &w0, uint64_t &w1) const {
     lds_win16(lds, (uint32_t)(p - base), w0, w1);
   }
-  __device__ __forceinline__ void peek2(uint64_t p, uint32_t &b0, uint32_t &b1) const {
-    const uint32_t o = (uint32_t)(p - base);
-    b0 = lds[o];
-    b1 = lds[o + 1];
+  // bytes p..p+3 and p+4..p+7 (three aligned dword reads; the buffer is 4-byte aligned and has
+  // >= 12 bytes of slack after lim)
+  __device__ __forceinline__ void win8(uint64_t p, uint32_t &w, uint32_t &wn) const {
+    const uint32_t o = (uint32_t)(p - base), sh = (o & 3u) * 8u;
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(lds) + (o >> 2);
+    const uint32_t a0 = q[0], a1 = q[1], a2 = q[2];
+    w = __builtin_amdgcn_alignbit(a1, a0, sh);
+    wn = __builtin_amdgcn_alignbit(a2, a1, sh);
   }
 };
 
@@ -196,42 +200,48 @@ __device__ __forceinline__ ChangeCols decode_change(const R &rd, uint64_t pstart
   uint64_t off = 0;
   while (off < len) {
     uint64_t avail = len - off;
-    if constexpr (R::kFast) if (avail >= 2 && rd.ok(pstart + off, 2)) {
-      // fast path: one-byte field prefix of a known tag and a one-byte varint after it (the
-      // shape the reference's encoder writes for short fields); same results as below
-      uint32_t b0, b1;
-      rd.peek2(pstart + off, b0, b1);
-      const uint32_t tag = b0 >> 3;
-      if (b0 < 0x80u && b1 < 0x80u && tag >= 1u && tag <= 6u) {
+    if constexpr (R::kFast) if (avail >= 2 && rd.ok(pstart + off, 5)) {
+      // fast path: a one-byte field prefix of a known tag and a 1..4-byte varint after it (the
+      // shapes the reference's encoder writes for values < 2^28); same results as below
+      uint32_t w, wn;
+      rd.win8(pstart + off, w, wn);
+      const uint32_t b0 = w & 0xFFu, tag = b0 >> 3;
+      const uint32_t x = __builtin_amdgcn_alignbit(wn, w, 8);  // bytes 1..4
+      const uint32_t tm = ~x & 0x80808080u;
+      if (b0 < 0x80u && tag >= 1u && tag <= 6u && tm) {
+        const uint32_t k2 = ((uint32_t)__builtin_ctz(tm) >> 3) + 1u;
+        if ((uint64_t)k2 > avail - 1) goto bad;  // the varint runs past the field
+        const uint32_t v = ((x & 0x7Fu) | ((x >> 1) & 0x3F80u) | ((x >> 2) & 0x1FC000u) | ((x >> 3) & 0xFE00000u)) &
+                           ((1u << (7u * k2)) - 1u);
         if (tag == 3u || tag == 4u || tag == 5u) {
           if (tag == 3u) {
-            c.change = b1;
+            c.change = v;
             found |= 2;
           } else if (tag == 4u) {
-            c.from = b1;
+            c.from = v;
             found |= 4;
           } else {
-            c.to = b1;
+            c.to = v;
             found |= 8;
           }
-          off += 2;
+          off += 1u + k2;
         } else {
-          const uint64_t o2 = off + 2;
-          if ((uint64_t)b1 > len - o2) goto bad;
+          const uint64_t o2 = off + 1u + k2;
+          if ((uint64_t)v > len - o2) goto bad;
           if (tag == 1u) {
             c.subset_off = (uint32_t)o2;
-            c.subset_len = b1;
+            c.subset_len = v;
             c.flags |= DRP_F_SUBSET;
           } else if (tag == 2u) {
             c.key_off = (uint32_t)o2;
-            c.key_len = b1;
+            c.key_len = v;
             found |= 1;
           } else {
             c.value_off = (uint32_t)o2;
-            c.value_len = b1;
+            c.value_len = v;
             c.flags |= DRP_F_VALUE;
           }
-          off = o2 + b1;
+          off = o2 + v;
         }
         continue;
       }

@@ -12,7 +12,7 @@ for v in $1; do
   DRP_LIB=$GRAFT_REPO_ROOT/exp/$v/libdrp.so timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU \
     SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU --output-format csv \
     -d $GRAFT_REPO_ROOT/gpurun_out/pmcab/$v -o run -- python3 -u $GRAFT_REPO_ROOT/bench.py --frames $F --steps 1 \
-    --warmup 1 --no-cpu > $GRAFT_REPO_ROOT/gpurun_out/pmcab/$v.log 2>&1 || { rc=$?; case $v in abl*) [ $rc = 1 ] || exit $rc;; *) exit $rc;; esac; }
+    --warmup 1 --no-cpu > $GRAFT_REPO_ROOT/gpurun_out/pmcab/$v.log 2>&1 || { rc=$?; case $v in abl*|fa*) [ $rc = 1 ] || exit $rc;; *) exit $rc;; esac; }
   cd $GRAFT_REPO_ROOT
   echo "$v done"
 done
