@@ -922,28 +922,34 @@ __device__ __forceinline__ void push_work(const DecodeParams &P, uint64_t t) {
   if (threadIdx.x == 0) P.work[atomicAdd(P.work_n, 1u)] = (uint32_t)t;
 }
 
-__global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
-  constexpr uint32_t HV = DRP_HALO_NODES ? HALO / SEGB : 0;  // halo "threads" with nodes
-  __shared__ uint64_t lmw[NT + HV];   // live masks; then strong masks
-  __shared__ uint64_t dmw[NT];        // undecided masks
-  __shared__ uint16_t loff[NT + HV];  // first list index of each thread
-  __shared__ uint32_t hmx[HALO / 16 + 1];  // halo masks per 16 bytes
-  __shared__ uint16_t lpos[FCAP];
-  __shared__ uint32_t lnd[FCAP > NT + 1 ? FCAP : NT + 1];  // nodes (first: the next-16-byte masks)
-  __shared__ uint8_t lal[FCAP];  // 0 dead, 1 strong, 2 undecided (leaves the image)
-  __shared__ uint32_t xw[8];
-  __shared__ uint32_t xf[2 * NT / WAVE], wl[NT / WAVE], fl[NT / WAVE];
-  __shared__ uint64_t xm[4];  // candidate masks (two waves): [w] strong, [2 + w] strong and far
+constexpr uint32_t HV = DRP_HALO_NODES ? HALO / SEGB : 0;  // halo "threads" with nodes
+// LDS of the fast claims form (one struct so the fused kernel can share it)
+struct FastLds {
+  __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+  uint64_t lmw[NT + HV];   // live masks; then strong masks
+  uint64_t dmw[NT];        // undecided masks
+  uint16_t loff[NT + HV];  // first list index of each thread
+  uint32_t hmx[HALO / 16 + 1];  // halo masks per 16 bytes
+  uint16_t lpos[FCAP];
+  uint32_t lnd[FCAP > NT + 1 ? FCAP : NT + 1];  // nodes (first: the next-16-byte masks; last: the emit list)
+  uint8_t lal[FCAP];  // 0 dead, 1 strong, 2 undecided (leaves the image)
+  uint32_t xw[8];
+  uint32_t xf[2 * NT / WAVE], wl[NT / WAVE], fl[NT / WAVE];
+  uint64_t xm[4];  // candidate masks (two waves): [w] strong, [2 + w] strong and far
+};
+enum : uint32_t { FC_OK = 0, FC_DENSE = 1, FC_ABLATE = 2 };
+
+// The fast claims of interior tile t: writes the per-thread records (P.ent*) and P.claim[t], and
+// returns this thread's record (eb, en, ecn) and, in thread NT - 1, the claim. FC_DENSE: more than
+// FCAP live positions (the tile went to the general kernel's work list; nothing written).
+__device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const TileGeo &G, uint64_t t, FastLds &S,
+                                                uint32_t &eb_o, uint32_t &en_o, uint32_t &ecn_o, uint64_t &cl_o) {
+  uint8_t *buf = S.buf;
+  uint64_t *lmw = S.lmw, *dmw = S.dmw, *xm = S.xm;
+  uint16_t *loff = S.loff, *lpos = S.lpos;
+  uint32_t *hmx = S.hmx, *lnd = S.lnd, *xw = S.xw, *xf = S.xf, *wl = S.wl, *fl = S.fl;
+  uint8_t *lal = S.lal;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-  const uint64_t t = blockIdx.x;
-  const uint64_t ntiles = P.tile_prefix[P.nstreams];
-  const TileGeo G = tile_geo(P, t);
-  if (t >= ntiles) return;  // (whole workgroup)
-  if (G.A < G.so || G.A + IMG > G.se) {  // edge tile: the general kernel
-    push_work(P, t);
-    return;
-  }
   // ---- stage, masks, live positions (varints of 1..3 bytes) --------------------------------
   uint4 v[SEGB / 16], hv;
   {
@@ -980,7 +986,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   const uint64_t live = X0 | (M0 & (Xs1 | (Ms1 & Xs2)));
 #if DRP_ABLATE_F == 1
   abl_out(P, t, (uint64_t)(live));
-  return;
+  return FC_ABLATE;
 #endif
   // Halo nodes (DRP_HALO_NODES): the halo's live positions join the list as HV more "threads", so
   // the survival check of the tile's last frames does not stop at the tile end (their chains
@@ -1016,7 +1022,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   const uint32_t total = ttotal + (DRP_HALO_NODES ? xw[2] : 0u);
   if (total > FCAP) {  // very dense tile: the general kernel's per-thread checks
     push_work(P, t);
-    return;
+    return FC_DENSE;
   }
   loff[tid] = (uint16_t)off;
   {
@@ -1097,7 +1103,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   bsync();
 #if DRP_ABLATE_F == 2
   abl_out(P, t, (uint64_t)(ncode[0] + na[1]));
-  return;
+  return FC_ABLATE;
 #endif
   lmw[tid] = 0;  // (now the strong masks)
   dmw[tid] = 0;
@@ -1140,13 +1146,13 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   }
 #if DRP_ABLATE_F == 3
   abl_out(P, t, (uint64_t)(g + defer));
-  return;
+  return FC_ABLATE;
 #endif
   uint32_t n = 0, R = RX_NONE;
   if (g != RX_NONE) R = fwalk(lnd, g, s1r, n);
 #if DRP_ABLATE_F == 4
   abl_out(P, t, (uint64_t)(R + n));
-  return;
+  return FC_ABLATE;
 #endif
   // rule 2: a chain that starts by jumping past the tile only where nothing later can start one
   uint64_t S0m, S1m;
@@ -1179,7 +1185,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow, P.stats);
 #if DRP_ABLATE_F == 5
   abl_out(P, t, (uint64_t)(R + E));
-  return;
+  return FC_ABLATE;
 #endif
   // restarts from deferred candidates, decided in HBM (big frames), as in spec_claims
   const Img m{buf, P.bytes, G.A, G.se};
@@ -1212,7 +1218,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   }
 #if DRP_ABLATE_F == 6
   abl_out(P, t, (uint64_t)(R + E + need));
-  return;
+  return FC_ABLATE;
 #endif
   // rule 3: the chain's last frame may jump over threads holding strong candidates; keep the
   // chain they start when it is the denser one (>= 2 frames)
@@ -1241,10 +1247,14 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   {
     const bool carrier = rx_node(E) && rx_off(E) < s1r;
     const uint64_t ix = t * NT + tid;
-    P.ent[ix] = carrier ? (uint8_t)(((rx_off(E) - lb) & 63u) | (rs ? 0x40u : 0u)) : (uint8_t)0xFF;
-    P.ent_n[ix] = carrier ? (uint8_t)(n & 0xFFFFu) : (uint8_t)0;
-    P.ent_c[ix] = carrier ? (uint8_t)(n >> 16) : (uint8_t)0;
+    eb_o = carrier ? (((rx_off(E) - lb) & 63u) | (rs ? 0x40u : 0u)) : 0xFFu;
+    en_o = carrier ? (n & 0xFFFFu) : 0u;
+    ecn_o = carrier ? (n >> 16) : 0u;
+    P.ent[ix] = (uint8_t)eb_o;
+    P.ent_n[ix] = (uint8_t)en_o;
+    P.ent_c[ix] = (uint8_t)ecn_o;
   }
+  cl_o = 0;
   if (tid == NT - 1) {
     uint64_t cl = C_ID;
     if (R < RX_DEAD && !rx_node(R)) {
@@ -1259,12 +1269,110 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
       cl = G.A + rx_off(R);
     }
     P.claim[t] = cl;
+    cl_o = cl;
   }
+  return FC_OK;
+}
+
+__global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) {
+  __shared__ FastLds S;
+  const uint64_t t = blockIdx.x;
+  const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  const TileGeo G = tile_geo(P, t);
+  if (t >= ntiles) return;  // (whole workgroup)
+  if (G.A < G.so || G.A + IMG > G.se) {  // edge tile: the general kernel
+    push_work(P, t);
+    return;
+  }
+  uint32_t eb, en, ecn;
+  uint64_t cl;
+  (void)fast_claims(P, G, t, S, eb, en, ecn, cl);
 }
 
 // ==== kernel 2: exact entries, verification, frame counts =====================================
 // e_t = the nearest claim before t that is not identity (or the stream entry); claims are final,
 // so nothing here waits. Publishes incl_e[t] = e_{t+1} for kernel 3 and for later tiles.
+// ==== kernel 2, records-only form (default): 8 lanes per tile, 32 tiles per workgroup ===========
+// verify_counts' fast check from kernel 1's per-thread records alone: e_t from the previous claims
+// (up to 32 identity claims back), thread k = the one holding e_t must have it as its predicted
+// entry and no later thread may restart the chain; then the tile's counts are the sums of the
+// records from thread k on (byte sums with v_dot4). Each lane holds 16 threads' records. A tile
+// that does not pass (a re-walk is needed, a miss, a longer identity run) goes to a list that
+// verify_counts then takes, so results are verify_counts' in every case. Threads before k are
+// left to emit_tiles through tile_k (the records stay as kernel 1 wrote them).
+constexpr uint32_t VL_BLK = 256, VL_G = 8;
+__device__ __forceinline__ uint32_t bytes_from(uint32_t s, uint32_t d) {  // byte mask of dword d: index >= s
+  return s <= 4u * d ? 0xFFFFFFFFu : (s >= 4u * d + 4u ? 0u : 0xFFFFFFFFu << (8u * (s - 4u * d)));
+}
+__device__ __forceinline__ uint32_t restart_bytes(uint32_t x) {  // 4-bit mask: byte b has (b & 0xC0) == 0x40
+  const uint32_t y = (x & 0xC0C0C0C0u) ^ 0x40404040u;
+  return msb4(~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u);
+}
+__global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
+  const uint32_t tid = threadIdx.x, r = tid & (VL_G - 1u), gb = (tid & 63u) & ~(VL_G - 1u);
+  const uint64_t t = ((uint64_t)blockIdx.x * VL_BLK + tid) / VL_G;
+  const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  if (t >= ntiles) return;  // (whole 8-lane group: no barriers or cross-group exchanges below)
+  const TileGeo G = tile_geo(P, t);
+  const uint64_t ix = t * NT + 16u * r;
+  const uint4 e4 = *reinterpret_cast<const uint4 *>(P.ent + ix);
+  const uint4 n4 = *reinterpret_cast<const uint4 *>(P.ent_n + ix);
+  const uint4 c4 = *reinterpret_cast<const uint4 *>(P.ent_c + ix);
+  const uint64_t claim = P.claim[t];
+  uint64_t et = G.e0;
+  bool found = t == G.tf;
+  for (uint32_t step = 0; !found && step < 4u; step++) {
+    const int64_t j = (int64_t)t - 1 - (int64_t)(VL_G * step + r);
+    const bool virt = j < (int64_t)G.tf;
+    const uint64_t c = virt ? G.e0 : P.claim[j];
+    const uint32_t gm = (uint32_t)(__ballot(virt || c != C_ID) >> gb) & 0xFFu;
+    if (gm) {
+      const uint32_t src = gb + (uint32_t)__builtin_ctz(gm);
+      et = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(c >> 32), (int)src, WAVE) << 32) |
+           (uint32_t)__shfl((int)(uint32_t)c, (int)src, WAVE);
+      found = true;
+    }
+  }
+  const bool bogus = is_pos(et) && et < G.A;
+  const bool inside = is_pos(et) && !bogus && et < G.A + TILE;
+  const uint32_t k = inside ? (uint32_t)((et - G.A) / SEGB) : NT;
+  const uint32_t kr = k / 16u, ki = k % 16u;
+  const uint32_t ew[4] = {e4.x, e4.y, e4.z, e4.w}, nw[4] = {n4.x, n4.y, n4.z, n4.w}, cw[4] = {c4.x, c4.y, c4.z, c4.w};
+  uint32_t bad = 0, sf = 0, sc = 0, rsm = 0;
+  const uint32_t s = r > kr ? 0u : (r == kr ? ki : 16u);  // this lane's threads from k on
+#pragma unroll
+  for (uint32_t d = 0; d < 4; d++) {
+    const uint32_t m = bytes_from(s, d);
+    sf = __builtin_amdgcn_udot4(nw[d] & m, 0x01010101u, sf, false);
+    sc = __builtin_amdgcn_udot4(cw[d] & m, 0x01010101u, sc, false);
+    rsm |= restart_bytes(ew[d]) << (4u * d);
+  }
+  if (inside) {
+    if (r == kr) {
+      const uint32_t b = (ew[ki >> 2] >> (8u * (ki & 3u))) & 0xFFu;
+      bad = (b & 0x80u) || (b & 63u) != (uint32_t)((et - G.A) % SEGB) || (rsm >> ki) > 1u;
+    } else if (r > kr) {
+      bad = rsm != 0;
+    }
+  }
+#pragma unroll
+  for (uint32_t d = 1; d < VL_G; d <<= 1) {
+    sf += shfl_xor32(sf, d);
+    sc += shfl_xor32(sc, d);
+    bad |= shfl_xor32(bad, d);
+  }
+  const bool miss = !inside && !bogus && claim != C_ID && claim != et;
+  if (r != 0) return;
+  if (!found || bad || bogus || miss || (inside && claim == C_ID)) {
+    P.vlist[atomicAdd(P.vlist_n, 1u)] = (uint32_t)t;  // verify_counts decides this tile
+    return;
+  }
+  P.tile_exit[t] = inside ? claim : et;
+  P.tile_count[t] = sf;
+  P.tile_nch[t] = sc;
+  P.tile_k[t] = (uint8_t)k;
+}
+
 __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint64_t xr[NT / WAVE];
@@ -1272,11 +1380,15 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   __shared__ uint64_t sh_e;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wid = tid >> 6;
-  const uint64_t t = blockIdx.x;
   uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  // every tile (one per workgroup), or the tiles verify_lite listed (a few per workgroup)
+  const uint32_t nwork = P.vlist ? *P.vlist_n : 0u;
+  for (uint32_t wi = blockIdx.x; P.vlist ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
+  const uint64_t t = P.vlist ? P.vlist[wi] : wi;
+  bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
-  if (t >= ntiles) return;  // (whole workgroup)
+  if (t >= ntiles) continue;  // (whole workgroup)
   const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
   // every load this tile needs goes out first (their latencies overlap)
   const uint64_t ix = t * NT + tid;
@@ -1418,6 +1530,8 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     P.tile_exit[t] = exit_t;
     P.tile_count[t] = count_t;
     P.tile_nch[t] = nch_t;
+    if (P.tile_k) P.tile_k[t] = 0;  // (this kernel rewrote the records of the threads before e_t)
+  }
   }
 }
 
@@ -1581,7 +1695,8 @@ __global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P)
   const uint64_t se = G.se, A = G.A;
   // the records load with the tile bytes, not after them
   const uint64_t base = P.tile_base[t];
-  const uint8_t eb = P.ent[t * NT + tid];     // exact entry of this thread's bytes (kernel 2)
+  const uint32_t k0 = P.tile_k ? P.tile_k[t] : 0u;  // threads before e_t's (verify_lite)
+  const uint8_t eb = tid < k0 ? (uint8_t)0xFF : P.ent[t * NT + tid];  // exact entry of this thread's bytes
   const uint8_t en = P.ent_n[t * NT + tid];   // exact frames from it (kernel 2)
   stage(P, G, buf);
   const Img m{buf, P.bytes, A, se};
@@ -1627,6 +1742,322 @@ __global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P)
   (void)nbl;
   badf = lane_min64(badf);
   if (lane == 0 && badf != ~0ull) atomicMin((unsigned long long *)&P.payload_err[G.s], (unsigned long long)badf);
+}
+
+// ==== fused default path: claims, proof, output base and emission in one pass ===================
+// Each tile computes its claim (fast form, or read from the edge pre-pass), publishes it, then
+// takes e_t = the nearest non-identity published claim before it (or the stream entry) and runs
+// verify_counts' record check on its own per-thread records. Passing that check on a constant
+// claim array is the same proof as a miss-free verify pass (claims never change inside this
+// kernel), so the tile's count is exact; a decoupled look-back over the tiles' counts gives its
+// output base, and the tile emits its frames from the LDS image it already holds. The wire is
+// read once. Anything that does not pass (a failed check, a dense tile, a wait that runs out)
+// marks the tile blocked and sets P.slow: the host then runs the split path (verify, repair
+// passes, scans, emit_tiles over every tile), which overwrites whatever was emitted here.
+// Waits are bounded and only on lower tile indices (dispatched earlier), so nothing hangs.
+constexpr uint64_t FS_AGG = 1ull << 62, FS_INC = 2ull << 62, FS_BLK = 3ull << 62, FS_VAL = (1ull << 62) - 1;
+constexpr uint64_t FCL_UNK = RDY | C_ID | MARK_TERM;  // published claim: unknown here (dense tile)
+#ifndef DRP_FUSED_SPIN
+#define DRP_FUSED_SPIN (1u << 13)  // look-back polls before a tile gives up (blocked -> split path)
+#endif
+#ifndef DRP_FUSED
+#define DRP_FUSED 0  // 1: the fused pass first (measured slower: see DESIGN.md), split path on failure
+#endif
+
+// Polls: one lane loads the nearest word until it is published (a 64-lane poll of the window
+// would put 64 uncached loads per waiting tile on the few HBM lines all resident tiles watch);
+// the whole window is read only to pass over identity claims / aggregates.
+__device__ __forceinline__ uint64_t poll1(const uint64_t *p, uint32_t &spin) {
+  for (uint32_t nap = 1;; nap = nap < 8 ? nap * 2 : 8) {
+    uint64_t w = 0;
+    if ((threadIdx.x & 63u) == 0) w = ld_agent(p);
+    w = readlane64(w, 0);
+    if (w || ++spin > DRP_FUSED_SPIN) return w;
+    for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// e_t for tile t (wave 0): the nearest published non-identity claim before t in its stream, or the
+// stream entry. blk: an unknown claim on the way, or the wait ran out (to = true).
+__device__ __forceinline__ uint64_t fused_entry(const DecodeParams &P, const TileGeo &G, uint64_t t, bool &blk,
+                                                bool &to) {
+  const uint32_t lane = threadIdx.x & 63u;
+  blk = false;
+  to = false;
+  if (t == G.tf) return G.e0;
+  uint32_t spin = 0;
+  {
+    const uint64_t w = poll1(&P.fcl[t - 1], spin);
+    if (!w) {
+      blk = to = true;
+      return NONE;
+    }
+    if ((w & ~RDY) != C_ID) {
+      if (w == FCL_UNK) blk = true;
+      return w & ~RDY;
+    }
+  }
+  int64_t j0 = (int64_t)t - 2;  // t - 1 is an identity tile: look further back
+  for (;;) {
+    const int64_t j = j0 - (int64_t)lane;
+    const bool virt = j < (int64_t)G.tf;
+    const uint64_t w = virt ? 0ull : ld_agent(&P.fcl[j]);
+    const uint64_t sm = __ballot(virt || (w != 0 && (w & ~RDY) != C_ID));
+    const uint64_t nr = __ballot(!virt && w == 0);
+    const uint64_t below = sm ? (1ull << __builtin_ctzll(sm)) - 1ull : ~0ull;
+    if (!(nr & below)) {
+      if (sm) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(sm);
+        const uint64_t v = readlane64(virt ? G.e0 : (w & ~RDY), k);
+        if (v == (FCL_UNK & ~RDY)) blk = true;
+        return v;
+      }
+      j0 -= WAVE;  // 64 identity claims: keep looking back
+      continue;
+    }
+    if (++spin > DRP_FUSED_SPIN) {
+      blk = to = true;
+      return NONE;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
+// exclusive output base of tile t > 0 (wave 0) from the published counts; ~0 when blocked
+__device__ __forceinline__ uint64_t fused_base(const DecodeParams &P, uint64_t t, bool &to) {
+  const uint32_t lane = threadIdx.x & 63u;
+  to = false;
+  uint32_t spin = 0;
+  const uint64_t w1 = poll1(&P.fst[t - 1], spin);
+  if (!w1) {
+    to = true;
+    return ~0ull;
+  }
+  if ((w1 >> 62) == 2u) return w1 & FS_VAL;  // the common case: t - 1 already has its prefix
+  if ((w1 >> 62) == 3u) return ~0ull;        // blocked
+  uint64_t acc = w1 & FS_VAL;  // t - 1's aggregate
+  int64_t j0 = (int64_t)t - 2;
+  for (;;) {
+    const int64_t j = j0 - (int64_t)lane;
+    const uint64_t w = j >= 0 ? ld_agent(&P.fst[j]) : FS_INC;  // (before tile 0: prefix 0)
+    const uint32_t st = (uint32_t)(w >> 62);
+    const uint64_t sm = __ballot(st >= 2u), nr = __ballot(st == 0u);
+    const uint32_t k = sm ? (uint32_t)__builtin_ctzll(sm) : 64u;
+    const uint64_t below = k >= 64u ? ~0ull : (1ull << k) - 1ull;
+    if (!(nr & below)) {
+      if (k < 64u && readlane32(st, k) == 3u) return ~0ull;  // blocked
+      acc += wave_sum64(lane <= k ? (w & FS_VAL) : 0ull);
+      if (k < 64u) return acc;
+      j0 -= WAVE;
+      continue;
+    }
+    if (++spin > DRP_FUSED_SPIN) {
+      to = true;
+      return ~0ull;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
+__global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_emit(DecodeParams P) {
+  __shared__ FastLds S;
+  __shared__ uint64_t fx[3];                // e_t, claim, base
+  __shared__ uint32_t fw[3 * (NT / WAVE) + 1];  // per wave: frames, changes, bad; blocked
+  static_assert(NT == 2 * WAVE, "two waves per tile");
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  const uint64_t t = blockIdx.x;
+  const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  const TileGeo G = tile_geo(P, t);
+  if (t >= ntiles) return;  // (whole workgroup)
+  const uint64_t ix = t * NT + tid;
+  uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
+#define FTR(k) \
+  if (P.trace && tid == 0) P.trace[t * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+  FTR(0);
+  if (P.trace && tid == 0)
+    P.trace[t * 8 + 5] = (uint64_t)__builtin_amdgcn_s_getreg(4 << 0 | 0 << 6 | 31 << 11) |
+                         ((uint64_t)(__builtin_amdgcn_s_getreg(20 << 0 | 0 << 6 | 15 << 11) & 15u) << 40);
+  uint32_t eb, en, ecn;
+  uint64_t cl;
+  if (G.A < G.so || G.A + IMG > G.se) {
+    // edge tile: claim and records from the pre-pass (spec_claims over the edge list)
+    cl = P.claim[t];
+    eb = P.ent[ix];
+    en = P.ent_n[ix];
+    ecn = P.ent_c[ix];
+    if (tid == NT - 1) st_agent(&P.fcl[t], cl | RDY);
+    stage(P, G, S.buf);
+  } else {
+    const uint32_t r = fast_claims(P, G, t, S, eb, en, ecn, cl);
+    if (r == FC_ABLATE) return;
+    if (r == FC_DENSE) {  // the general kernel takes it after this kernel: unknown here
+      if (tid == 0) {
+        st_agent(&P.fcl[t], FCL_UNK);
+        st_agent(&P.fst[t], FS_BLK);
+        atomicOr(P.slow, 1u);
+      }
+      return;
+    }
+    if (tid == NT - 1) st_agent(&P.fcl[t], cl | RDY);
+  }
+  // ---- e_t and the record check (verify_counts' fast path) ----------------------------------
+  PHASE(17);
+  FTR(1);
+  if (wid == 0) {
+    bool blk, to;
+    const uint64_t e = fused_entry(P, G, t, blk, to);
+    if (lane == 0) {
+      fx[0] = e;
+      fw[3 * (NT / WAVE)] = blk;
+      if (to) atomicOr(P.slow, 2u);
+    }
+  }
+  if (tid == NT - 1) fx[1] = cl;
+  bsync();
+  const uint64_t et = fx[0], claim = fx[1];
+  const bool blocked = fw[3 * (NT / WAVE)] != 0;
+  PHASE(18);
+  FTR(2);
+  const bool bogus = is_pos(et) && et < G.A;
+  const bool inside = is_pos(et) && !bogus && et < G.A + TILE;
+  const uint32_t k = inside ? (uint32_t)((et - G.A) / SEGB) : NT;
+  uint32_t bad = 0;
+  if (inside) {
+    if (tid == k && ((eb & 0x80u) || (eb & 63u) != (uint32_t)((et - G.A) % SEGB))) bad = 1;
+    if (tid > k && eb != 0xFFu && (eb & 0x40u)) bad = 1;
+  }
+  bool mine = tid >= k && eb != 0xFFu && !blocked;
+  uint32_t n = mine ? en : 0u;
+  uint32_t ni = wave_scan_dpp(n);
+  {
+    const uint32_t nc = wave_sum32(mine ? ecn : 0u);
+    const uint32_t b = __ballot(bad != 0) != 0;
+    if (lane == 63) fw[wid] = ni;
+    if (lane == 0) {
+      fw[NT / WAVE + wid] = nc;
+      fw[2 * (NT / WAVE) + wid] = b;
+    }
+  }
+  bsync();
+  uint32_t count_t = fw[0] + fw[1], nch_t = fw[2] + fw[3];
+  uint32_t woff = wid ? fw[0] : 0u;
+  bool badt = (fw[4] | fw[5]) != 0 || (inside && claim == C_ID);
+  uint64_t exit_t = inside ? claim : et;
+  const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
+  if (badt && inside && !blocked) {
+    // The records disagree with e_t (the predicted chain entered the tile elsewhere and joined the
+    // stream's chain later): the exact chain from e_t over the image, as verify_counts' slow path.
+    const Img m{S.buf, P.bytes, G.A, G.se};
+    uint64_t E = !(eb & 0x80u) ? lb + (eb & 63u) : NONE;  // (seeds: fewer rounds, same result)
+    uint32_t nn = 0;
+    uint64_t R = walk(m, E, s1, nn);
+    bsync();  // (fw reads above are done)
+    link<true>(m, s1, NONE, et, E, R, nn, S.xm, S.xf, P.overflow);
+    mine = is_pos(E) && E < s1;
+    eb = mine ? (uint32_t)(E - lb) : 0xFFu;
+    n = mine ? (nn & 0xFFFFu) : 0u;
+    ni = wave_scan_dpp(n);
+    const uint32_t nc = wave_sum32(mine ? (nn >> 16) : 0u);
+    if (lane == 63) fw[wid] = ni;
+    if (lane == 0) fw[NT / WAVE + wid] = nc;
+    if (tid == NT - 1) fx[1] = R;
+    bsync();
+    count_t = fw[0] + fw[1];
+    nch_t = fw[2] + fw[3];
+    woff = wid ? fw[0] : 0u;
+    const uint64_t Rl = fx[1];
+    exit_t = (Rl & MARK_TERM) ? (Rl & ~M_ERR) : Rl;
+    badt = exit_t != (claim == C_ID ? et : claim) || ((Rl & MARK_TERM) && (Rl & M_ERR));
+  }
+  const bool miss = !inside && !bogus && claim != C_ID && claim != et;
+  const bool ok = !blocked && !badt && !bogus && !miss;
+  // ---- output base: publish the count, look back over the predecessors' counts ---------------
+  PHASE(19);
+  if (wid == 0) {
+    uint64_t base = ~0ull;
+    if (ok) {
+      if (lane == 0) st_agent(&P.fst[t], FS_AGG | count_t);
+      bool to = false;
+      base = t ? fused_base(P, t, to) : 0ull;
+      if (lane == 0) {
+        st_agent(&P.fst[t], base != ~0ull ? (FS_INC | (base + count_t)) : FS_BLK);
+        if (to) atomicOr(P.slow, 2u);
+      }
+    } else if (lane == 0) {
+      st_agent(&P.fst[t], FS_BLK);
+      if (!blocked) {
+        atomicOr(P.slow, 4u);  // this tile's own check failed (blocked ones: upstream)
+        if (P.stats) {  // debug capture (DRP_STATS=1): the first failed checks
+          const unsigned long long q = atomicAdd(&P.stats[24], 1ull);
+          if (q < 3) {
+            P.stats[25 + 4 * q] = t;
+            P.stats[26 + 4 * q] = (badt ? 1u : 0u) | (bogus ? 2u : 0u) | (miss ? 4u : 0u);
+            P.stats[27 + 4 * q] = et;
+            P.stats[28 + 4 * q] = claim;
+          }
+        }
+      }
+    }
+    if (lane == 0) fx[2] = base;
+  }
+  bsync();
+  const uint64_t base = fx[2];
+  PHASE(20);
+  FTR(3);
+  if (base == ~0ull) return;  // (uniform) the split path emits this tile
+  if (tid == NT - 1) {
+    P.tile_exit[t] = exit_t;
+    P.tile_count[t] = count_t;
+    P.tile_nch[t] = nch_t;
+    P.tile_base[t] = base;
+    if (base + count_t > P.cap) atomicOr(P.overflow, 1u);
+  }
+  // ---- emission from the LDS image (as emit_tiles) ---------------------------------------------
+  const Img m{S.buf, P.bytes, G.A, G.se};
+  uint16_t *lst = reinterpret_cast<uint16_t *>(S.lnd);
+  constexpr uint32_t FLCAP = sizeof(S.lnd) / 2;
+  const bool listed = count_t <= FLCAP;
+  uint32_t nchx = 0, nbl = 0;
+  uint64_t badf = ~0ull;
+  if (n) {
+    uint32_t i = woff + ni - n;
+    uint64_t p = lb + (eb & 63u);
+    while (p < s1 && p < G.se) {
+      const Hdr h = hdr_fast(m, p);
+      if (h.kind != H_VALID && h.kind != H_TAIL_BLOB) break;
+      if (h.id != 0) {
+        if (listed) lst[i] = (uint16_t)(p - G.A);
+        else emit_frame(P, m, p, base + i, nchx, nbl, badf);
+        i++;
+      }
+      if (h.kind != H_VALID) break;
+      p = h.succ;
+    }
+  }
+  if (listed) {
+    bsync();
+    for (uint32_t i = tid; i < count_t; i += NT) emit_frame(P, m, G.A + lst[i], base + i, nchx, nbl, badf);
+  }
+  badf = lane_min64(badf);
+  if (lane == 0 && badf != ~0ull) atomicMin((unsigned long long *)&P.payload_err[G.s], (unsigned long long)badf);
+  PHASE(21);
+  FTR(4);
+}
+
+// the stream-edge tiles (image not inside the stream): first tile and the last two or three
+__global__ void edge_list_kernel(const uint64_t *tile_prefix, const uint64_t *stream_off, uint64_t nstreams,
+                                 uint32_t *list, uint32_t *n) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nstreams) return;
+  const uint64_t tf = tile_prefix[s], tl = tile_prefix[s + 1];
+  if (tl <= tf) return;
+  const uint64_t so = stream_off[s], se = stream_off[s + 1];
+  const uint64_t a0 = so & ~(uint64_t)(TILE - 1);
+  const uint64_t t1 = tl > tf + 3 ? tl - 3 : tf + 1;
+  for (uint64_t t = tf; t < tl; t = (t == tf ? t1 : t + 1)) {
+    const uint64_t A = a0 + (t - tf) * TILE;
+    if (A < so || A + IMG > se) list[atomicAdd(n, 1u)] = (uint32_t)t;
+  }
 }
 
 // per-stream change / blob counts (one thread per stream)
@@ -1713,8 +2144,59 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
   Q.work = nullptr;
   hipLaunchKernelGGL(spec::spec_claims, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
 #endif
-  hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  if (Q.vlist) {  // records-only verification, then verify_counts on the tiles it lists
+    const uint64_t nb = (nt_max * spec::VL_G + spec::VL_BLK - 1) / spec::VL_BLK;
+    hipLaunchKernelGGL(spec::verify_lite, dim3((uint32_t)nb), dim3(spec::VL_BLK), 0, st, Q);
+    hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0, st,
+                       Q);
+  } else {
+    hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  }
   return hipGetLastError();
+}
+
+extern "C" int drp_spec_fused(void) { return DRP_FUSED; }
+
+// The fused pass: edge-tile claims (general kernel over the edge list), then claims + proof +
+// output base + emission for every tile, then the general kernel over the dense tiles the fused
+// kernel listed (their records feed the split path, which P.slow then asks for).
+extern "C" hipError_t drp_launch_spec_fused(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
+                                            uint32_t *tile_stream, uint32_t *edge_list, uint32_t *edge_n,
+                                            hipStream_t st) {
+  if (nt_max == 0) return hipSuccess;
+  DecodeParams Q = *P;
+  Q.tile_stream = nullptr;
+  if (nstreams > 1) {
+    const uint32_t blk = 256;
+    hipLaunchKernelGGL(spec::tile_stream_kernel, dim3((uint32_t)((nt_max + blk - 1) / blk)), dim3(blk), 0, st,
+                       P->tile_prefix, nstreams, nt_max, tile_stream);
+    Q.tile_stream = tile_stream;
+  }
+  {
+    const uint32_t blk = 256;
+    hipLaunchKernelGGL(spec::edge_list_kernel, dim3((uint32_t)((nstreams + blk - 1) / blk)), dim3(blk), 0, st,
+                       P->tile_prefix, P->stream_off, nstreams, edge_list, edge_n);
+    DecodeParams E = Q;
+    E.work = edge_list;
+    E.work_n = edge_n;
+    const uint64_t ne = 3 * nstreams < nt_max ? 3 * nstreams : nt_max;
+    hipLaunchKernelGGL(spec::spec_claims, dim3((uint32_t)(ne < 16384 ? ne : 16384)), dim3(spec::NT), 0, st, E);
+  }
+  hipLaunchKernelGGL(spec::claims_emit, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  const uint32_t gw = (uint32_t)(nt_max < 16384 ? nt_max : 16384);
+  hipLaunchKernelGGL(spec::spec_claims, dim3(gw), dim3(spec::NT), 0, st, Q);
+  return hipGetLastError();
+}
+
+// After a fused pass that needed no split path: change-count bases and per-stream counts.
+extern "C" hipError_t drp_launch_spec_fused_tail(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
+                                                 uint64_t *scan_tmp, hipStream_t st) {
+  if (nt_max == 0) return hipSuccess;
+  hipError_t e = drp_launch_tile_scan(P->tile_nch, P->tile_prefix, nstreams, nt_max, scan_tmp, P->tile_nch_base,
+                                      ~0ull, P->overflow, st);
+  if (e != hipSuccess) return e;
+  return drp_launch_stream_counts(P->tile_prefix, nstreams, P->tile_count, P->tile_base, P->tile_nch,
+                                  P->tile_nch_base, P->scount, st);
 }
 
 // One more verify pass over the repaired claims (the caller clears incl_e and the flags first).
@@ -1723,6 +2205,7 @@ extern "C" hipError_t drp_launch_spec_verify(const DecodeParams *P, uint64_t nt_
   if (nt_max == 0) return hipSuccess;
   DecodeParams Q = *P;
   Q.tile_stream = nstreams > 1 ? tile_stream : nullptr;
+  Q.vlist = nullptr;  // every tile
   hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
   return hipGetLastError();
 }
