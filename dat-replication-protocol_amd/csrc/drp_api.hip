@@ -197,7 +197,7 @@ int drp_set_strict(drp_ctx *c, int strict) {
 // scratch layout for a decode of `nbytes` over `ns` streams
 struct DecLayout {
   uint64_t ntiles_max;
-  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, tstream, ent, tk, scan_tmp, total;
+  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, tstream, ent, tk, fmiss, segw, scan_tmp, total;
   uint64_t nsg;
 };
 static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
@@ -216,6 +216,8 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.tstream = o; o += al(L.ntiles_max * 4);    // tile -> stream (speculative kernel)
   L.ent = o; o += al(L.ntiles_max * 128 * 3);  // per-thread entries + counts (speculative kernel)
   L.tk = o; o += al(L.ntiles_max);             // first entry thread per tile (verify_lite)
+  L.fmiss = o; o += al(ns * 8);                  // first missed tile per stream (verify)
+  L.segw = o; o += al((2 * 64 * 1024 + 1025) * 8);  // segmented repair: candidates + entries
   L.scan_tmp = o; o += al((L.ntiles_max / 4096 + 2) * 8);  // tile scans: block sums
   L.total = o;
   return L;
@@ -343,7 +345,8 @@ int run_decode_exact_once(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, con
   c->timing.finalize_ms = 0;
   c->timing.spec_repairs = 0;
   c->timing.strict_reruns = 0;
-  c->timing.split_path = 32u;
+  c->timing.verify_relisted = 0;
+  c->timing.seg_repairs = 0;
   TRACE("decode done: tiles=%u flags=%u", h[0], h[1]);
   if (dstats) {
     unsigned long long hs[40];
@@ -393,7 +396,8 @@ int run_decode_exact(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const ui
 
 // The default decode: speculate-and-verify kernel (drp_decode_spec.hip). Returns DRP_E_RETRY
 // when a prediction failed (or a bounded wait expired): the caller then runs the exact kernel.
-constexpr int kSpecRepairPasses = 16;  // one verify pass each (0.7 ms on C5), vs ~1.5 s for an exact re-run there
+constexpr int kSpecRepairPasses = 16;
+constexpr int kSegRepairAfter = 3;  // verify passes before the segmented repair of the streams still missing  // one verify pass each (0.7 ms on C5), vs ~1.5 s for an exact re-run there
 
 int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
                     const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
@@ -413,9 +417,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   uint64_t *sgscan = c->scratch.at<uint64_t>(L.scan_tmp);
   hipStream_t st = c->st;
   CHK(hipEventRecord(c->ev[0], st));
-  const bool fused = drp_spec_fused() != 0;
   CHK(hipMemsetAsync(rec, 0, 2 * NT * 8, st));  // claim, incl_e
-  if (fused) CHK(hipMemsetAsync(rec + 3 * NT, 0, 2 * NT * 8, st));  // fcl, fst
   CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
   CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
   CHK(hipMemsetAsync(ctrl, 0, 32, st));
@@ -458,74 +460,69 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.ent_c = P.ent_n + NT * 128;
   P.tile_nch = tiles + 3 * NT;
   P.tile_nch_base = tiles + 4 * NT;
-  P.fcl = rec + 3 * NT;
-  P.fst = rec + 4 * NT;
-  P.slow = ctrl + 4;
-  uint32_t *edge_list = reinterpret_cast<uint32_t *>(rec + 2 * NT) + NT;  // (after the dense work list)
-  if (!fused) {  // (the same region: verify_lite's list of tiles for verify_counts)
-    P.vlist = edge_list;
-    P.vlist_n = ctrl + 5;
-    P.tile_k = c->scratch.at<uint8_t>(L.tk);
-  }
+  P.vlist = reinterpret_cast<uint32_t *>(rec + 2 * NT) + NT;  // (after the dense work list)
+  P.vlist_n = ctrl + 5;
+  P.tile_k = c->scratch.at<uint8_t>(L.tk);
+  P.first_miss = c->scratch.at<uint64_t>(L.fmiss);
+  CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
   unsigned long long *dstats = nullptr;
   if (getenv("DRP_STATS")) {
     CHK(hipMalloc((void **)&dstats, 64 * 8));
     CHK(hipMemsetAsync(dstats, 0, 64 * 8, st));
     P.stats = dstats;
   }
-  unsigned long long *dtrace = nullptr;
-  if (dstats && getenv("DRP_TRACE_FILE")) {  // per-tile timestamps of the fused kernel
-    CHK(hipMalloc((void **)&dtrace, NT * 64));
-    CHK(hipMemsetAsync(dtrace, 0, NT * 64, st));
-    P.trace = dtrace;
-  }
+  c->timing.seg_repairs = 0;
   CHK(hipEventRecord(c->ev[1], st));
   // claims + verification, then the prediction check on the host (one flag word) before any
   // output is written: a failed prediction is repaired in place first. Verify patched the
   // missed tiles' claims, so verify runs again (each pass fixes at least the first missed tile,
   // whose entry is exact) until a pass has no miss. Only when that does not settle within a
   // few passes (e.g. a protocol error on the exact chain) does the caller run the exact kernel.
-  // Default: the fused pass (claims, proof, output base and emission, wire read once). Any tile it
-  // could not prove or place (P.slow) sends the whole call down the split path, starting with a
-  // verify pass over every tile's claims and records.
   uint32_t h[8];
-  bool split = true;
-  uint32_t slow = 0;
-  if (fused) {
-    CHK(drp_launch_spec_fused(&P, NT, ns, tstream, edge_list, ctrl + 3, st));
-    CHK(hipMemcpyAsync(h, ctrl, 32, hipMemcpyDeviceToHost, st));
-    CHK(hipStreamSynchronize(st));
-    slow = h[4];
-    if ((h[1] & drp_spec_retry_mask()) == 0 && slow == 0) {
-      split = false;
-    } else if ((h[1] & drp_spec_retry_mask()) == 0) {
-      TRACE("decode_spec: fused pass incomplete (slow=%#x), split path", slow);
-      CHK(hipMemsetAsync(P.overflow, 0, 4, st));
-      CHK(drp_launch_spec_verify(&P, NT, ns, tstream, st));
-      CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
-      CHK(hipStreamSynchronize(st));
-    }
-  } else {
-    CHK(drp_launch_spec_head(&P, NT, ns, tstream, st));
-    CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
-    CHK(hipStreamSynchronize(st));
-  }
+  CHK(drp_launch_spec_head(&P, NT, ns, tstream, st));
+  CHK(hipMemcpyAsync(h, ctrl, 32, hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  const uint32_t relisted = h[5];
   const uint32_t miss = drp_spec_miss_bit();
   int pass = 0;
-  if (split && (h[1] & drp_spec_retry_mask()) == miss) {
+  bool seg_done = false;
+  if ((h[1] & drp_spec_retry_mask()) == miss) {
     for (; pass < kSpecRepairPasses && (h[1] & miss); pass++) {
+      if (pass >= kSegRepairAfter && !seg_done) {
+        // the misses keep coming one tile per pass (wrong predictions that agree with each
+        // other): recompute the claims of each stream from its first missed tile by exact
+        // chain walks (drp_decode_spec.hip, segmented repair), then verify them
+        seg_done = true;
+        std::vector<uint64_t> fm(ns), tp(ns + 1);
+        CHK(hipMemcpyAsync(fm.data(), P.first_miss, ns * 8, hipMemcpyDeviceToHost, st));
+        CHK(hipMemcpyAsync(tp.data(), tile_prefix, (ns + 1) * 8, hipMemcpyDeviceToHost, st));
+        CHK(hipStreamSynchronize(st));
+        for (uint64_t s = 0; s < ns; s++)
+          if (fm[s] != ~0ull) {
+            TRACE("decode_spec: segmented repair of stream %llu from tile %llu to %llu", (unsigned long long)s,
+                  (unsigned long long)fm[s], (unsigned long long)tp[s + 1]);
+            CHK(drp_launch_seg_repair(&P, s, fm[s], tp[s + 1], c->scratch.at<uint64_t>(L.segw), st));
+            c->timing.seg_repairs++;
+          }
+      }
       CHK(hipMemsetAsync(P.incl_e, 0, NT * 8, st));
       CHK(hipMemsetAsync(P.overflow, 0, 4, st));
+      CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
+      CHK(hipMemsetAsync(P.vlist_n, 0, 4, st));
       CHK(drp_launch_spec_verify(&P, NT, ns, tstream, st));
       CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
       CHK(hipStreamSynchronize(st));
+      if (trace_on()) {
+        uint64_t f0 = 0;
+        CHK(hipMemcpy(&f0, P.first_miss, 8, hipMemcpyDeviceToHost));
+        TRACE("decode_spec: pass %d flags=%#x first miss (stream 0) %lld", pass + 1, h[1], (long long)f0);
+      }
     }
     TRACE("decode_spec: %d repair pass(es), flags=%#x", pass, h[1]);
   }
   const bool retry = (h[1] & drp_spec_retry_mask()) != 0;
   if (!retry) {
-    if (split) CHK(drp_launch_spec_tail(&P, NT, ns, tstream, sgscan, st));
-    else CHK(drp_launch_spec_fused_tail(&P, NT, ns, sgscan, st));
+    CHK(drp_launch_spec_tail(&P, NT, ns, tstream, sgscan, st));
     CHK(hipEventRecord(c->ev[2], st));
     CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
                             scount, fr->type, co->flags, cap, res, st));
@@ -546,7 +543,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   c->timing.strict_reruns = 0;
   c->timing.exact_retries = 0;
   c->timing.spec_repairs = (uint32_t)pass;
-  c->timing.split_path = fused ? slow | (split && !slow ? 8u : 0u) : 16u;
+  c->timing.verify_relisted = relisted;
   TRACE("decode_spec done: tiles=%u flags=%#x", h[0], h[1]);
   if (dstats) {
     unsigned long long hs[64];
@@ -560,24 +557,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     for (int k = 0; k < 14; k++)
       if (ph[k][0]) fprintf(stderr, " %s=%.0f", ph[k], (double)hs[40 + k] / (double)(h[0] ? h[0] : 1));
     fprintf(stderr, " repairs=%d (avg cycles per tile) link_rounds=%llu\n", pass, hs[56]);
-    static const char *fph[] = {"claims", "entry", "check", "base", "emit"};
-    fprintf(stderr, "[drp-spec] fused: slow=%#x", slow);
-    for (int k = 0; k < 5; k++) fprintf(stderr, " %s=%.0f", fph[k], (double)hs[57 + k] / (double)(h[0] ? h[0] : 1));
-    fprintf(stderr, " failed checks=%llu", hs[24]);
-    for (unsigned k = 0; k < 3 && k < hs[24]; k++)
-      fprintf(stderr, " | t=%llu why=%llu e=%#llx claim=%#llx", hs[25 + 4 * k], hs[26 + 4 * k], hs[27 + 4 * k],
-              hs[28 + 4 * k]);
-    fprintf(stderr, "\n");
     (void)hipFree(dstats);
-  }
-  if (dtrace) {
-    std::vector<unsigned long long> ht(NT * 8);
-    CHK(hipMemcpy(ht.data(), dtrace, NT * 64, hipMemcpyDeviceToHost));
-    if (FILE *f = fopen(getenv("DRP_TRACE_FILE"), "wb")) {
-      fwrite(ht.data(), 8, ht.size(), f);
-      fclose(f);
-    }
-    (void)hipFree(dtrace);
   }
   if (h[1] & drp_spec_retry_mask()) return DRP_E_RETRY;
   if (h[1]) return DRP_E_CAPACITY;

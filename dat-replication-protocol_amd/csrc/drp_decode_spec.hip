@@ -923,7 +923,7 @@ __device__ __forceinline__ void push_work(const DecodeParams &P, uint64_t t) {
 }
 
 constexpr uint32_t HV = DRP_HALO_NODES ? HALO / SEGB : 0;  // halo "threads" with nodes
-// LDS of the fast claims form (one struct so the fused kernel can share it)
+// LDS of the fast claims form
 struct FastLds {
   __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   uint64_t lmw[NT + HV];   // live masks; then strong masks
@@ -1506,7 +1506,9 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     const uint64_t Rl = xr[0];
     exit_t = (Rl & MARK_TERM) ? (Rl & ~M_ERR) : Rl;
     const uint64_t want = claim == C_ID ? et : claim;
-    miss = exit_t != want || ((Rl & MARK_TERM) && (Rl & M_ERR));
+    // an error on the exact chain is a miss unless the claim already ends the chain there (a
+    // repaired claim, or the segmented repair's): then the tile's exit is exact
+    miss = exit_t != want || ((Rl & MARK_TERM) && (Rl & M_ERR) && claim != exit_t);
   }
   PHASE(10);
   if (tid == NT - 1) {
@@ -1517,6 +1519,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
       // the host re-runs verify until a pass has no miss (claims are only written on a miss,
       // so a miss-free pass saw a constant claim array and its proof holds).
       P.claim[t] = inside ? exit_t : C_ID;
+      if (P.first_miss) atomicMin((unsigned long long *)&P.first_miss[G.s], (unsigned long long)t);
       if (P.stats) {  // debug capture (DRP_STATS=1): the first misses
         const unsigned long long q = atomicAdd(&P.stats[0], 1ull);
         if (q < 5) {
@@ -1659,25 +1662,26 @@ __device__ __forceinline__ void emit_frame(const DecodeParams &P, const Img &m, 
   const uint64_t pl = h.L - 1;
   if (h.id == 1) nch++; else nbl++;
   if (f >= P.cap) return;
-  P.payload_off[f] = po;
-  P.payload_len[f] = pl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pl;
-  P.type[f] = (uint8_t)(h.id | (h.kind == H_TAIL_BLOB ? DRP_FRAME_PARTIAL : 0u));
+  const DecodeParams *K = &P;
+  K->payload_off[f] = po;
+  K->payload_len[f] = pl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pl;
+  K->type[f] = (uint8_t)(h.id | (h.kind == H_TAIL_BLOB ? DRP_FRAME_PARTIAL : 0u));
   if (h.id != 1) return;
   const LdsReader rd{m.lds, m.A, umin64(m.A + IMG, m.se)};
   ChangeCols c = decode_change(rd, po, pl);
   if (c.err == ERR_UNREACHABLE) c = decode_change_hbm(P.bytes, m.se, po, pl);
-  P.key_off[f] = c.key_off;
-  P.key_len[f] = c.key_len;
-  P.subset_off[f] = c.subset_off;
-  P.subset_len[f] = c.subset_len;
-  P.value_off[f] = c.value_off;
-  P.value_len[f] = c.value_len;
-  P.change[f] = c.change;
-  P.from[f] = c.from;
-  P.to[f] = c.to;
+  K->key_off[f] = c.key_off;
+  K->key_len[f] = c.key_len;
+  K->subset_off[f] = c.subset_off;
+  K->subset_len[f] = c.subset_len;
+  K->value_off[f] = c.value_off;
+  K->value_len[f] = c.value_len;
+  K->change[f] = c.change;
+  K->from[f] = c.from;
+  K->to[f] = c.to;
   uint32_t fl = c.flags;
   if (c.err == DRP_ERR_REQUIRED) fl |= DRP_F_MISSING;
-  P.flags[f] = (uint8_t)fl;
+  K->flags[f] = (uint8_t)fl;
   if (c.err) badf = f < badf ? f : badf;
 }
 
@@ -1744,320 +1748,203 @@ __global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P)
   if (lane == 0 && badf != ~0ull) atomicMin((unsigned long long *)&P.payload_err[G.s], (unsigned long long)badf);
 }
 
-// ==== fused default path: claims, proof, output base and emission in one pass ===================
-// Each tile computes its claim (fast form, or read from the edge pre-pass), publishes it, then
-// takes e_t = the nearest non-identity published claim before it (or the stream entry) and runs
-// verify_counts' record check on its own per-thread records. Passing that check on a constant
-// claim array is the same proof as a miss-free verify pass (claims never change inside this
-// kernel), so the tile's count is exact; a decoupled look-back over the tiles' counts gives its
-// output base, and the tile emits its frames from the LDS image it already holds. The wire is
-// read once. Anything that does not pass (a failed check, a dense tile, a wait that runs out)
-// marks the tile blocked and sets P.slow: the host then runs the split path (verify, repair
-// passes, scans, emit_tiles over every tile), which overwrites whatever was emitted here.
-// Waits are bounded and only on lower tile indices (dispatched earlier), so nothing hangs.
-constexpr uint64_t FS_AGG = 1ull << 62, FS_INC = 2ull << 62, FS_BLK = 3ull << 62, FS_VAL = (1ull << 62) - 1;
-constexpr uint64_t FCL_UNK = RDY | C_ID | MARK_TERM;  // published claim: unknown here (dense tile)
-#ifndef DRP_FUSED_SPIN
-#define DRP_FUSED_SPIN (1u << 13)  // look-back polls before a tile gives up (blocked -> split path)
-#endif
-#ifndef DRP_FUSED
-#define DRP_FUSED 0  // 1: the fused pass first (measured slower: see DESIGN.md), split path on failure
-#endif
+// ==== segmented repair: exact claims for an unsettled stream range ==============================
+// Verify passes fix only the first tile of a run of wrong predictions that agree with each other
+// (each pass proves one more entry), so a stream crafted with a second valid framing beside the
+// real one (tests/_streams.shadow_stream) would need one pass per tile. After a few passes the
+// host recomputes the claims of such a stream from its first missed tile t0 on, by exact chain
+// walks, in three launches:
+//   1. seg_walk    per segment of G tiles: up to 64 candidate entries near the segment start
+//                  (positions of its first tile whose header and next header parse; segment 0
+//                  also takes e_t0), walked in parallel, one lane each, through the segment's
+//                  tiles staged in LDS (tiles no chain starts a frame in are skipped); their
+//                  exits at the segment end.
+//   2. seg_stitch  one wave, segment by segment: the exact entry is one of the candidates (its
+//                  exit is the next entry) or is walked from global memory (rare: an entry
+//                  deeper in the segment than its first tile, inside a long blob).
+//   3. seg_claims  per segment, the one exact chain from its entry: each tile's claim (the first
+//                  chain position past it, the chain's end, or identity).
+// A verify pass then proves the new claims as usual. Cost: two streaming passes over the range
+// spread over the CUs plus a short serial stitch, however the predictions failed.
+constexpr uint32_t SEG_CAND = 64, SEG_GMAX = 1024;
+struct SegRange {
+  uint64_t s, t0, tl, G, nseg;  // stream, tiles [t0, tl), tiles per segment, segments
+  uint64_t *cand;               // per segment: 64 starts, then 64 exits
+  uint64_t *seg_entry;          // [nseg + 1] exact entry of each segment (and the final exit)
+};
 
-// Polls: one lane loads the nearest word until it is published (a 64-lane poll of the window
-// would put 64 uncached loads per waiting tile on the few HBM lines all resident tiles watch);
-// the whole window is read only to pass over identity claims / aggregates.
-__device__ __forceinline__ uint64_t poll1(const uint64_t *p, uint32_t &spin) {
-  for (uint32_t nap = 1;; nap = nap < 8 ? nap * 2 : 8) {
-    uint64_t w = 0;
-    if ((threadIdx.x & 63u) == 0) w = ld_agent(p);
-    w = readlane64(w, 0);
-    if (w || ++spin > DRP_FUSED_SPIN) return w;
-    for (uint32_t z = 0; z < nap; z++) __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// e_t for tile t (wave 0): the nearest published non-identity claim before t in its stream, or the
-// stream entry. blk: an unknown claim on the way, or the wait ran out (to = true).
-__device__ __forceinline__ uint64_t fused_entry(const DecodeParams &P, const TileGeo &G, uint64_t t, bool &blk,
-                                                bool &to) {
-  const uint32_t lane = threadIdx.x & 63u;
-  blk = false;
-  to = false;
-  if (t == G.tf) return G.e0;
-  uint32_t spin = 0;
-  {
-    const uint64_t w = poll1(&P.fcl[t - 1], spin);
-    if (!w) {
-      blk = to = true;
-      return NONE;
-    }
-    if ((w & ~RDY) != C_ID) {
-      if (w == FCL_UNK) blk = true;
-      return w & ~RDY;
-    }
-  }
-  int64_t j0 = (int64_t)t - 2;  // t - 1 is an identity tile: look further back
-  for (;;) {
-    const int64_t j = j0 - (int64_t)lane;
-    const bool virt = j < (int64_t)G.tf;
-    const uint64_t w = virt ? 0ull : ld_agent(&P.fcl[j]);
-    const uint64_t sm = __ballot(virt || (w != 0 && (w & ~RDY) != C_ID));
-    const uint64_t nr = __ballot(!virt && w == 0);
-    const uint64_t below = sm ? (1ull << __builtin_ctzll(sm)) - 1ull : ~0ull;
-    if (!(nr & below)) {
-      if (sm) {
-        const uint32_t k = (uint32_t)__builtin_ctzll(sm);
-        const uint64_t v = readlane64(virt ? G.e0 : (w & ~RDY), k);
-        if (v == (FCL_UNK & ~RDY)) blk = true;
-        return v;
-      }
-      j0 -= WAVE;  // 64 identity claims: keep looking back
-      continue;
-    }
-    if (++spin > DRP_FUSED_SPIN) {
-      blk = to = true;
-      return NONE;
-    }
-    __builtin_amdgcn_s_sleep(4);
-  }
-}
-
-// exclusive output base of tile t > 0 (wave 0) from the published counts; ~0 when blocked
-__device__ __forceinline__ uint64_t fused_base(const DecodeParams &P, uint64_t t, bool &to) {
-  const uint32_t lane = threadIdx.x & 63u;
-  to = false;
-  uint32_t spin = 0;
-  const uint64_t w1 = poll1(&P.fst[t - 1], spin);
-  if (!w1) {
-    to = true;
-    return ~0ull;
-  }
-  if ((w1 >> 62) == 2u) return w1 & FS_VAL;  // the common case: t - 1 already has its prefix
-  if ((w1 >> 62) == 3u) return ~0ull;        // blocked
-  uint64_t acc = w1 & FS_VAL;  // t - 1's aggregate
-  int64_t j0 = (int64_t)t - 2;
-  for (;;) {
-    const int64_t j = j0 - (int64_t)lane;
-    const uint64_t w = j >= 0 ? ld_agent(&P.fst[j]) : FS_INC;  // (before tile 0: prefix 0)
-    const uint32_t st = (uint32_t)(w >> 62);
-    const uint64_t sm = __ballot(st >= 2u), nr = __ballot(st == 0u);
-    const uint32_t k = sm ? (uint32_t)__builtin_ctzll(sm) : 64u;
-    const uint64_t below = k >= 64u ? ~0ull : (1ull << k) - 1ull;
-    if (!(nr & below)) {
-      if (k < 64u && readlane32(st, k) == 3u) return ~0ull;  // blocked
-      acc += wave_sum64(lane <= k ? (w & FS_VAL) : 0ull);
-      if (k < 64u) return acc;
-      j0 -= WAVE;
-      continue;
-    }
-    if (++spin > DRP_FUSED_SPIN) {
-      to = true;
-      return ~0ull;
-    }
-    __builtin_amdgcn_s_sleep(4);
-  }
-}
-
-__global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_emit(DecodeParams P) {
-  __shared__ FastLds S;
-  __shared__ uint64_t fx[3];                // e_t, claim, base
-  __shared__ uint32_t fw[3 * (NT / WAVE) + 1];  // per wave: frames, changes, bad; blocked
-  static_assert(NT == 2 * WAVE, "two waves per tile");
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-  const uint64_t t = blockIdx.x;
-  const uint64_t ntiles = P.tile_prefix[P.nstreams];
-  const TileGeo G = tile_geo(P, t);
-  if (t >= ntiles) return;  // (whole workgroup)
-  const uint64_t ix = t * NT + tid;
-  uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
-#define FTR(k) \
-  if (P.trace && tid == 0) P.trace[t * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
-  FTR(0);
-  if (P.trace && tid == 0)
-    P.trace[t * 8 + 5] = (uint64_t)__builtin_amdgcn_s_getreg(4 << 0 | 0 << 6 | 31 << 11) |
-                         ((uint64_t)(__builtin_amdgcn_s_getreg(20 << 0 | 0 << 6 | 15 << 11) & 15u) << 40);
-  uint32_t eb, en, ecn;
-  uint64_t cl;
-  if (G.A < G.so || G.A + IMG > G.se) {
-    // edge tile: claim and records from the pre-pass (spec_claims over the edge list)
-    cl = P.claim[t];
-    eb = P.ent[ix];
-    en = P.ent_n[ix];
-    ecn = P.ent_c[ix];
-    if (tid == NT - 1) st_agent(&P.fcl[t], cl | RDY);
-    stage(P, G, S.buf);
+__device__ __forceinline__ Hdr hdr_global(const uint8_t *g, uint64_t p, uint64_t se) {  // (as Img::at from HBM)
+  uint64_t w0, w1;
+  const uint64_t a = p & ~15ull;
+  const uint4 u = ld16(g, a, se), v = ld16(g, a + 16, se);
+  const uint64_t q0 = ((uint64_t)u.y << 32) | u.x, q1 = ((uint64_t)u.w << 32) | u.z;
+  const uint64_t q2 = ((uint64_t)v.y << 32) | v.x, q3 = ((uint64_t)v.w << 32) | v.z;
+  const uint32_t o = (uint32_t)(p & 15);
+  if (o < 8) {
+    w0 = funnel(q0, q1, 8 * o);
+    w1 = funnel(q1, q2, 8 * o);
   } else {
-    const uint32_t r = fast_claims(P, G, t, S, eb, en, ecn, cl);
-    if (r == FC_ABLATE) return;
-    if (r == FC_DENSE) {  // the general kernel takes it after this kernel: unknown here
-      if (tid == 0) {
-        st_agent(&P.fcl[t], FCL_UNK);
-        st_agent(&P.fst[t], FS_BLK);
-        atomicOr(P.slow, 1u);
-      }
-      return;
-    }
-    if (tid == NT - 1) st_agent(&P.fcl[t], cl | RDY);
+    w0 = funnel(q1, q2, 8 * (o - 8));
+    w1 = funnel(q2, q3, 8 * (o - 8));
   }
-  // ---- e_t and the record check (verify_counts' fast path) ----------------------------------
-  PHASE(17);
-  FTR(1);
-  if (wid == 0) {
-    bool blk, to;
-    const uint64_t e = fused_entry(P, G, t, blk, to);
-    if (lane == 0) {
-      fx[0] = e;
-      fw[3 * (NT / WAVE)] = blk;
-      if (to) atomicOr(P.slow, 2u);
-    }
-  }
-  if (tid == NT - 1) fx[1] = cl;
-  bsync();
-  const uint64_t et = fx[0], claim = fx[1];
-  const bool blocked = fw[3 * (NT / WAVE)] != 0;
-  PHASE(18);
-  FTR(2);
-  const bool bogus = is_pos(et) && et < G.A;
-  const bool inside = is_pos(et) && !bogus && et < G.A + TILE;
-  const uint32_t k = inside ? (uint32_t)((et - G.A) / SEGB) : NT;
-  uint32_t bad = 0;
-  if (inside) {
-    if (tid == k && ((eb & 0x80u) || (eb & 63u) != (uint32_t)((et - G.A) % SEGB))) bad = 1;
-    if (tid > k && eb != 0xFFu && (eb & 0x40u)) bad = 1;
-  }
-  bool mine = tid >= k && eb != 0xFFu && !blocked;
-  uint32_t n = mine ? en : 0u;
-  uint32_t ni = wave_scan_dpp(n);
-  {
-    const uint32_t nc = wave_sum32(mine ? ecn : 0u);
-    const uint32_t b = __ballot(bad != 0) != 0;
-    if (lane == 63) fw[wid] = ni;
-    if (lane == 0) {
-      fw[NT / WAVE + wid] = nc;
-      fw[2 * (NT / WAVE) + wid] = b;
-    }
-  }
-  bsync();
-  uint32_t count_t = fw[0] + fw[1], nch_t = fw[2] + fw[3];
-  uint32_t woff = wid ? fw[0] : 0u;
-  bool badt = (fw[4] | fw[5]) != 0 || (inside && claim == C_ID);
-  uint64_t exit_t = inside ? claim : et;
-  const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
-  if (badt && inside && !blocked) {
-    // The records disagree with e_t (the predicted chain entered the tile elsewhere and joined the
-    // stream's chain later): the exact chain from e_t over the image, as verify_counts' slow path.
-    const Img m{S.buf, P.bytes, G.A, G.se};
-    uint64_t E = !(eb & 0x80u) ? lb + (eb & 63u) : NONE;  // (seeds: fewer rounds, same result)
-    uint32_t nn = 0;
-    uint64_t R = walk(m, E, s1, nn);
-    bsync();  // (fw reads above are done)
-    link<true>(m, s1, NONE, et, E, R, nn, S.xm, S.xf, P.overflow);
-    mine = is_pos(E) && E < s1;
-    eb = mine ? (uint32_t)(E - lb) : 0xFFu;
-    n = mine ? (nn & 0xFFFFu) : 0u;
-    ni = wave_scan_dpp(n);
-    const uint32_t nc = wave_sum32(mine ? (nn >> 16) : 0u);
-    if (lane == 63) fw[wid] = ni;
-    if (lane == 0) fw[NT / WAVE + wid] = nc;
-    if (tid == NT - 1) fx[1] = R;
-    bsync();
-    count_t = fw[0] + fw[1];
-    nch_t = fw[2] + fw[3];
-    woff = wid ? fw[0] : 0u;
-    const uint64_t Rl = fx[1];
-    exit_t = (Rl & MARK_TERM) ? (Rl & ~M_ERR) : Rl;
-    badt = exit_t != (claim == C_ID ? et : claim) || ((Rl & MARK_TERM) && (Rl & M_ERR));
-  }
-  const bool miss = !inside && !bogus && claim != C_ID && claim != et;
-  const bool ok = !blocked && !badt && !bogus && !miss;
-  // ---- output base: publish the count, look back over the predecessors' counts ---------------
-  PHASE(19);
-  if (wid == 0) {
-    uint64_t base = ~0ull;
-    if (ok) {
-      if (lane == 0) st_agent(&P.fst[t], FS_AGG | count_t);
-      bool to = false;
-      base = t ? fused_base(P, t, to) : 0ull;
-      if (lane == 0) {
-        st_agent(&P.fst[t], base != ~0ull ? (FS_INC | (base + count_t)) : FS_BLK);
-        if (to) atomicOr(P.slow, 2u);
-      }
-    } else if (lane == 0) {
-      st_agent(&P.fst[t], FS_BLK);
-      if (!blocked) {
-        atomicOr(P.slow, 4u);  // this tile's own check failed (blocked ones: upstream)
-        if (P.stats) {  // debug capture (DRP_STATS=1): the first failed checks
-          const unsigned long long q = atomicAdd(&P.stats[24], 1ull);
-          if (q < 3) {
-            P.stats[25 + 4 * q] = t;
-            P.stats[26 + 4 * q] = (badt ? 1u : 0u) | (bogus ? 2u : 0u) | (miss ? 4u : 0u);
-            P.stats[27 + 4 * q] = et;
-            P.stats[28 + 4 * q] = claim;
-          }
-        }
-      }
-    }
-    if (lane == 0) fx[2] = base;
-  }
-  bsync();
-  const uint64_t base = fx[2];
-  PHASE(20);
-  FTR(3);
-  if (base == ~0ull) return;  // (uniform) the split path emits this tile
-  if (tid == NT - 1) {
-    P.tile_exit[t] = exit_t;
-    P.tile_count[t] = count_t;
-    P.tile_nch[t] = nch_t;
-    P.tile_base[t] = base;
-    if (base + count_t > P.cap) atomicOr(P.overflow, 1u);
-  }
-  // ---- emission from the LDS image (as emit_tiles) ---------------------------------------------
-  const Img m{S.buf, P.bytes, G.A, G.se};
-  uint16_t *lst = reinterpret_cast<uint16_t *>(S.lnd);
-  constexpr uint32_t FLCAP = sizeof(S.lnd) / 2;
-  const bool listed = count_t <= FLCAP;
-  uint32_t nchx = 0, nbl = 0;
-  uint64_t badf = ~0ull;
-  if (n) {
-    uint32_t i = woff + ni - n;
-    uint64_t p = lb + (eb & 63u);
-    while (p < s1 && p < G.se) {
-      const Hdr h = hdr_fast(m, p);
-      if (h.kind != H_VALID && h.kind != H_TAIL_BLOB) break;
-      if (h.id != 0) {
-        if (listed) lst[i] = (uint16_t)(p - G.A);
-        else emit_frame(P, m, p, base + i, nchx, nbl, badf);
-        i++;
-      }
-      if (h.kind != H_VALID) break;
-      p = h.succ;
-    }
-  }
-  if (listed) {
-    bsync();
-    for (uint32_t i = tid; i < count_t; i += NT) emit_frame(P, m, G.A + lst[i], base + i, nchx, nbl, badf);
-  }
-  badf = lane_min64(badf);
-  if (lane == 0 && badf != ~0ull) atomicMin((unsigned long long *)&P.payload_err[G.s], (unsigned long long)badf);
-  PHASE(21);
-  FTR(4);
+  return parse_win(w0, w1, p, se);
 }
 
-// the stream-edge tiles (image not inside the stream): first tile and the last two or three
-__global__ void edge_list_kernel(const uint64_t *tile_prefix, const uint64_t *stream_off, uint64_t nstreams,
-                                 uint32_t *list, uint32_t *n) {
-  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nstreams) return;
-  const uint64_t tf = tile_prefix[s], tl = tile_prefix[s + 1];
-  if (tl <= tf) return;
-  const uint64_t so = stream_off[s], se = stream_off[s + 1];
-  const uint64_t a0 = so & ~(uint64_t)(TILE - 1);
-  const uint64_t t1 = tl > tf + 3 ? tl - 3 : tf + 1;
-  for (uint64_t t = tf; t < tl; t = (t == tf ? t1 : t + 1)) {
-    const uint64_t A = a0 + (t - tf) * TILE;
-    if (A < so || A + IMG > se) list[atomicAdd(n, 1u)] = (uint32_t)t;
+__device__ __forceinline__ TileGeo seg_geo(const DecodeParams &P, uint64_t s) {
+  TileGeo G;
+  G.s = s;
+  G.tf = P.tile_prefix[s];
+  G.so = P.stream_off[s];
+  G.se = P.stream_off[s + 1];
+  G.A = 0;
+  G.e0 = G.so + (P.entry ? P.entry[s] : 0ull);
+  return G;
+}
+__device__ __forceinline__ uint64_t seg_tile_a(const TileGeo &G, uint64_t u) {
+  return (G.so & ~(uint64_t)(TILE - 1)) + (u - G.tf) * TILE;
+}
+// the segment's end: the next segment's first tile, or the stream end
+__device__ __forceinline__ uint64_t seg_end(const TileGeo &G, const SegRange &R, uint64_t seg) {
+  const uint64_t tb = R.t0 + (seg + 1) * R.G;
+  return tb >= R.tl ? G.se : seg_tile_a(G, tb);
+}
+// chain step inside the staged tile: advance p while it starts a frame before lim (the tile end,
+// or the segment end); a header that ends the chain returns MARK_TERM (| M_ERR) | p
+__device__ __forceinline__ uint64_t seg_advance(const Img &m, uint64_t p, uint64_t lim) {
+  while (is_pos(p) && p < lim && p < m.se) {
+    const Hdr h = m.at(p);
+    if (h.kind != H_VALID) return term_of(h, p);
+    p = h.succ;
   }
+  return p;
+}
+
+__global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+  __shared__ uint64_t cpos[SEG_CAND];
+  __shared__ uint32_t xw[NT / WAVE];
+  __shared__ uint64_t nxt;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  const uint64_t seg = blockIdx.x;
+  TileGeo G = seg_geo(P, R.s);
+  const uint64_t ta = R.t0 + seg * R.G, send = seg_end(G, R, seg);
+  G.A = seg_tile_a(G, ta);
+  uint64_t e0 = NONE;  // segment 0: the exact entry of t0 (nearest non-identity claim before it)
+  if (seg == 0) {
+    e0 = G.e0;
+    for (uint64_t j = R.t0; j > G.tf; j--) {
+      const uint64_t c = P.claim[j - 1];
+      if (c != C_ID) {
+        e0 = c;
+        break;
+      }
+    }
+    if (tid == 0) R.seg_entry[0] = e0;
+  }
+  // candidates: live positions of the first tile whose header, and next header, parse
+  const uint64_t live = stage_live(P, G, buf);
+  const Img m{buf, P.bytes, G.A, G.se};
+  const uint64_t lb = G.A + (uint64_t)tid * SEGB;
+  uint64_t ok = 0;
+  for (uint64_t bits = live; bits; bits &= bits - 1) {
+    const uint32_t o = (uint32_t)__builtin_ctzll(bits);
+    const uint64_t p = lb + o;
+    const Hdr h = m.at(p);
+    bool good = h.kind <= H_TAIL_BLOB;
+    if (h.kind == H_VALID && h.succ < G.se && h.succ + 16 <= G.A + IMG) good = m.at(h.succ).kind <= H_TAIL_BLOB;
+    if (good) ok |= 1ull << o;
+  }
+  const uint32_t cnt = (uint32_t)__builtin_popcountll(ok);
+  const uint32_t pre = wave_incl_scan32(cnt);
+  if (lane == 63) xw[wid] = pre;
+  bsync();
+  uint32_t idx = pre - cnt + (wid ? xw[0] : 0u);
+  const uint32_t first = (seg == 0 && is_pos(e0) && e0 < send) ? 1u : 0u;
+  const uint32_t nc = min((uint32_t)SEG_CAND, xw[0] + xw[1] + first);
+  if (first && tid == 0) cpos[0] = e0;
+  idx += first;
+  for (uint64_t bits = ok; bits && idx < SEG_CAND; bits &= bits - 1, idx++)
+    cpos[idx] = lb + (uint32_t)__builtin_ctzll(bits);
+  bsync();
+  uint64_t pos = (wid == 0 && lane < nc) ? cpos[lane] : NONE, start = pos;
+  // walk: the lanes' chains through the segment, tile by tile (a tile only when a chain is in it)
+  for (;;) {
+    if (wid == 0) {
+      const Img mt{buf, P.bytes, G.A, G.se};  // (the image of the tile staged last)
+      pos = seg_advance(mt, pos, umin64(G.A + TILE, send));
+      const uint64_t mn = lane_min64(is_pos(pos) && pos < send ? pos : NONE);
+      if (lane == 0) nxt = mn;
+    }
+    bsync();
+    const uint64_t q = nxt;
+    if (q == NONE) break;
+    G.A = seg_tile_a(G, ta + (q - seg_tile_a(G, ta)) / TILE);
+    stage(P, G, buf);  // (its barrier orders the walk's reads before the next image)
+  }
+  if (wid == 0) {
+    R.cand[seg * 2 * SEG_CAND + lane] = lane < nc ? start : NONE;
+    R.cand[seg * 2 * SEG_CAND + SEG_CAND + lane] = pos;
+  }
+}
+
+__global__ __launch_bounds__(WAVE) void seg_stitch(DecodeParams P, SegRange R) {
+  const uint32_t lane = threadIdx.x;
+  const TileGeo G = seg_geo(P, R.s);
+  uint64_t e = R.seg_entry[0];
+  for (uint64_t seg = 0; seg < R.nseg; seg++) {
+    const uint64_t send = seg_end(G, R, seg);
+    if (lane == 0) R.seg_entry[seg] = e;
+    if (!is_pos(e) || e >= send) continue;  // the chain ended, or jumps over the segment
+    const uint64_t st = R.cand[seg * 2 * SEG_CAND + lane];
+    const uint64_t hit = __ballot(st == e);
+    if (hit) {
+      e = readlane64(R.cand[seg * 2 * SEG_CAND + SEG_CAND + lane], (uint32_t)__builtin_ctzll(hit));
+      continue;
+    }
+    uint64_t p = e;  // not a candidate: walk it (one lane, headers from HBM)
+    if (lane == 0) {
+      while (p < send && p < G.se) {
+        const Hdr h = hdr_global(P.bytes, p, G.se);
+        if (h.kind != H_VALID) {
+          p = term_of(h, p);
+          break;
+        }
+        p = h.succ;
+      }
+    }
+    e = readlane64(p, 0);
+  }
+  if (lane == 0) R.seg_entry[R.nseg] = e;
+}
+
+__global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+  __shared__ uint64_t lcl[SEG_GMAX];
+  __shared__ uint64_t nxt;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t seg = blockIdx.x;
+  TileGeo G = seg_geo(P, R.s);
+  const uint64_t ta = R.t0 + seg * R.G, tb = umin64(ta + R.G, R.tl), send = seg_end(G, R, seg);
+  for (uint64_t i = tid; i < tb - ta; i += NT) lcl[i] = C_ID;
+  uint64_t p = R.seg_entry[seg];
+  if (tid == 0) nxt = (is_pos(p) && p < send) ? p : NONE;
+  bsync();
+  for (;;) {
+    const uint64_t q = nxt;
+    if (q == NONE) break;
+    const uint64_t u = ta + (q - seg_tile_a(G, ta)) / TILE;
+    G.A = seg_tile_a(G, u);
+    stage(P, G, buf);
+    if (tid == 0) {
+      const Img m{buf, P.bytes, G.A, G.se};
+      p = seg_advance(m, q, umin64(G.A + TILE, send));
+      // the tile's claim: the first chain position past it, or where the chain ends in it
+      lcl[u - ta] = (p & MARK_TERM) ? (p & ~M_ERR) : p;
+      nxt = (is_pos(p) && p < send) ? p : NONE;
+    }
+    bsync();
+  }
+  for (uint64_t i = tid; i < tb - ta; i += NT) P.claim[ta + i] = lcl[i];
 }
 
 // per-stream change / blob counts (one thread per stream)
@@ -2155,58 +2042,20 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
   return hipGetLastError();
 }
 
-extern "C" int drp_spec_fused(void) { return DRP_FUSED; }
-
-// The fused pass: edge-tile claims (general kernel over the edge list), then claims + proof +
-// output base + emission for every tile, then the general kernel over the dense tiles the fused
-// kernel listed (their records feed the split path, which P.slow then asks for).
-extern "C" hipError_t drp_launch_spec_fused(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
-                                            uint32_t *tile_stream, uint32_t *edge_list, uint32_t *edge_n,
-                                            hipStream_t st) {
-  if (nt_max == 0) return hipSuccess;
-  DecodeParams Q = *P;
-  Q.tile_stream = nullptr;
-  if (nstreams > 1) {
-    const uint32_t blk = 256;
-    hipLaunchKernelGGL(spec::tile_stream_kernel, dim3((uint32_t)((nt_max + blk - 1) / blk)), dim3(blk), 0, st,
-                       P->tile_prefix, nstreams, nt_max, tile_stream);
-    Q.tile_stream = tile_stream;
-  }
-  {
-    const uint32_t blk = 256;
-    hipLaunchKernelGGL(spec::edge_list_kernel, dim3((uint32_t)((nstreams + blk - 1) / blk)), dim3(blk), 0, st,
-                       P->tile_prefix, P->stream_off, nstreams, edge_list, edge_n);
-    DecodeParams E = Q;
-    E.work = edge_list;
-    E.work_n = edge_n;
-    const uint64_t ne = 3 * nstreams < nt_max ? 3 * nstreams : nt_max;
-    hipLaunchKernelGGL(spec::spec_claims, dim3((uint32_t)(ne < 16384 ? ne : 16384)), dim3(spec::NT), 0, st, E);
-  }
-  hipLaunchKernelGGL(spec::claims_emit, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
-  const uint32_t gw = (uint32_t)(nt_max < 16384 ? nt_max : 16384);
-  hipLaunchKernelGGL(spec::spec_claims, dim3(gw), dim3(spec::NT), 0, st, Q);
-  return hipGetLastError();
-}
-
-// After a fused pass that needed no split path: change-count bases and per-stream counts.
-extern "C" hipError_t drp_launch_spec_fused_tail(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
-                                                 uint64_t *scan_tmp, hipStream_t st) {
-  if (nt_max == 0) return hipSuccess;
-  hipError_t e = drp_launch_tile_scan(P->tile_nch, P->tile_prefix, nstreams, nt_max, scan_tmp, P->tile_nch_base,
-                                      ~0ull, P->overflow, st);
-  if (e != hipSuccess) return e;
-  return drp_launch_stream_counts(P->tile_prefix, nstreams, P->tile_count, P->tile_base, P->tile_nch,
-                                  P->tile_nch_base, P->scount, st);
-}
-
 // One more verify pass over the repaired claims (the caller clears incl_e and the flags first).
 extern "C" hipError_t drp_launch_spec_verify(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                              uint32_t *tile_stream, hipStream_t st) {
   if (nt_max == 0) return hipSuccess;
   DecodeParams Q = *P;
   Q.tile_stream = nstreams > 1 ? tile_stream : nullptr;
-  Q.vlist = nullptr;  // every tile
-  hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  if (Q.vlist) {  // records-only verification, verify_counts on the tiles it lists (caller zeroes vlist_n)
+    const uint64_t nb = (nt_max * spec::VL_G + spec::VL_BLK - 1) / spec::VL_BLK;
+    hipLaunchKernelGGL(spec::verify_lite, dim3((uint32_t)nb), dim3(spec::VL_BLK), 0, st, Q);
+    hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0, st,
+                       Q);
+  } else {
+    hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  }
   return hipGetLastError();
 }
 
@@ -2226,3 +2075,24 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
                                   Q.scount, st);
 }
 
+// Segmented repair of stream s from tile t0 (its first missed tile) to its end (the caller then
+// runs a verify pass). scratch: 2 * 64 * 1024 + 1025 words.
+extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, uint64_t t0, uint64_t tl,
+                                            uint64_t *scratch, hipStream_t st) {
+  if (tl <= t0) return hipSuccess;
+  spec::SegRange R;
+  R.s = s;
+  R.t0 = t0;
+  R.tl = tl;
+  const uint64_t n = tl - t0;
+  R.G = (n + 1023) / 1024;
+  if (R.G > spec::SEG_GMAX) return hipErrorInvalidValue;
+  R.nseg = (n + R.G - 1) / R.G;
+  R.cand = scratch;
+  R.seg_entry = scratch + 2 * spec::SEG_CAND * 1024;
+  DecodeParams Q = *P;
+  hipLaunchKernelGGL(spec::seg_walk, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);
+  hipLaunchKernelGGL(spec::seg_stitch, dim3(1), dim3(WAVE), 0, st, Q, R);
+  hipLaunchKernelGGL(spec::seg_claims, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);
+  return hipGetLastError();
+}

@@ -52,14 +52,11 @@ struct DecodeParams {
   uint32_t *work_n;             //  and their count (the fast claims kernel appends)
   uint64_t *tile_nch;           // change frames of tile t (per-stream counts come from a scan:
   uint64_t *tile_nch_base;      //  same-address atomics per tile serialise across the XCDs)
-  // fused kernel (claims_emit): published claims (claim | READY) and the output-base look-back
-  // words (aggregate / inclusive frame count / blocked); slow != 0 after it: run the split path
-  uint64_t *fcl, *fst;
-  uint32_t *slow;
   // verify_lite: tiles it leaves to verify_counts, and each tile's first entry thread (emit skips
   // the threads before it); null: verify_counts verifies every tile
   uint32_t *vlist, *vlist_n;
   uint8_t *tile_k;
+  uint64_t *first_miss;  // per stream: the first tile a verify pass repaired (~0: none)
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
   unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
 };
@@ -88,11 +85,8 @@ uint32_t drp_spec_retry_mask(void);
 uint32_t drp_spec_miss_bit(void);
 hipError_t drp_launch_spec_head(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                 uint32_t *tile_stream, hipStream_t st);
-int drp_spec_fused(void);
-hipError_t drp_launch_spec_fused(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
-                                 uint32_t *tile_stream, uint32_t *edge_list, uint32_t *edge_n, hipStream_t st);
-hipError_t drp_launch_spec_fused_tail(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
-                                      uint64_t *scan_tmp, hipStream_t st);
+hipError_t drp_launch_seg_repair(const drp::DecodeParams *P, uint64_t s, uint64_t t0, uint64_t tl, uint64_t *scratch,
+                                 hipStream_t st);
 hipError_t drp_launch_spec_verify(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                   uint32_t *tile_stream, hipStream_t st);
 hipError_t drp_launch_spec_tail(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,

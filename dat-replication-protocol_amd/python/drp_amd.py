@@ -67,7 +67,8 @@ class StreamStats(C.Structure):
 
 class Timing(C.Structure):
     _fields_ = [("decode_ms", C.c_float), ("finalize_ms", C.c_float), ("total_ms", C.c_float),
-                ("strict_reruns", U32), ("spec_repairs", U32), ("exact_retries", U32), ("split_path", U32)]
+                ("strict_reruns", U32), ("spec_repairs", U32), ("exact_retries", U32), ("verify_relisted", U32),
+                ("seg_repairs", U32), ("reserved", U32)]
 
 
 _lib = None

@@ -153,10 +153,9 @@ typedef struct drp_timing {
   uint32_t strict_reruns; /* 1: the speculative decode fell back to the exact kernel */
   uint32_t spec_repairs;  /* verify passes that repaired failed predictions in place */
   uint32_t exact_retries; /* 1: the exact kernel's bounded look-back wait expired and it was re-run */
-  uint32_t split_path;    /* 0: the fused pass decoded everything; else why the split path ran
-                             (bit 0 dense tile, 1 look-back wait ran out, 2 a record check failed,
-                             3 a claims-kernel link overflow, 4 built without the fused pass,
-                             5 the exact kernel decoded) */
+  uint32_t verify_relisted; /* tiles verify_lite handed to verify_counts (a re-walk or a longer look-back) */
+  uint32_t seg_repairs;     /* streams whose claims the segmented repair recomputed (miss cascades) */
+  uint32_t reserved;
 } drp_timing;
 
 /* ---- context ------------------------------------------------------------- */

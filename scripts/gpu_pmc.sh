@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC counter passes over a C2 decode (one rocprofv3 run per pass, as the pool requires).
-# Usage: gpurun --timeout 900 -- 'bash scripts/gpu_pmc.sh [frames]'
+# Usage: gpurun --timeout 900 -- 'bash scripts/gpu_pmc.sh [frames]'; summary: scripts/pmc_kernels.py
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc

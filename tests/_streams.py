@@ -141,3 +141,36 @@ def c3_edge_stream(j, blob_len=70000, tail_frames=40, seed=21):
 def random_stream_seeded(seed, nframes):
     """random_stream with a fresh seeded generator (fixture recipes)."""
     return random_stream(random.Random(seed), nframes, blob_p=0.05, blob_max=5000, subset_p=0.2)
+
+
+def shadow_stream(nframes, period=8192, shadow_at=100, small=10, seed=7, change_every=0):
+    """Adversarial for the speculative decode: two valid framings that never merge. Real blob
+    frames of `period` bytes; inside each payload, at `shadow_at`, a shadow chain of one
+    `small`-byte blob frame and one blob frame of `period - small` bytes, so the shadow chain
+    repeats with the same period, one frame denser than the real one. Every tile then holds a
+    strong, denser chain the prediction prefers, consistent from tile to tile: a miss cascade.
+    change_every > 0 makes every n-th real frame a Change frame (key + value) instead of a blob."""
+    out = bytearray(np.random.default_rng(seed).integers(0, 256, size=nframes * period, dtype=np.uint8).tobytes())
+    sh_small = varint(small - 1) + b"\x02"  # (small <= 128: a one-byte length)
+    sh_big_len = period - small
+    kb = len(varint(sh_big_len))
+    sh_big = varint(sh_big_len - kb) + b"\x02"
+    for i in range(nframes):
+        r = i * period
+        if change_every and i % change_every == 0:
+            key = b"k%09d" % i
+            head = b"\x12" + varint(len(key)) + key + b"\x18\x01\x20\x02\x28\x03"
+            vlen = period - len(varint(period - 3)) - 1 - len(head) - 3
+            pay = head + b"\x32" + varint(vlen)
+            kr = len(varint(period - 3))
+            hdr = varint(period - kr) + b"\x01"
+            assert len(hdr) + len(pay) + vlen == period, (len(hdr), len(pay), vlen)
+            out[r:r + len(hdr) + len(pay)] = hdr + pay
+        else:
+            kr = len(varint(period - 2))
+            hdr = varint(period - kr) + b"\x02"
+            out[r:r + len(hdr)] = hdr
+        s = r + shadow_at
+        out[s:s + len(sh_small)] = sh_small
+        out[s + small:s + small + len(sh_big)] = sh_big
+    return bytes(out)

@@ -1,0 +1,94 @@
+"""GPU: streams built to defeat the speculative decode's prediction (tests/_streams.shadow_stream:
+a second valid framing beside the real one, denser, consistent from tile to tile, so verify
+passes would fix one tile each) and streams with a protocol error early on (every later tile
+must become a pass-through tile). Both must settle through the segmented repair, stay bit-exact
+with the oracle, and never fall back to the exact kernel (~370 ms/GB on long random frames).
+Parity is pinned by the oracle (the reference has no such stream)."""
+import random
+import time
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import _streams as S
+
+pytestmark = pytest.mark.gpu
+
+CASCADES = [(8192, 20, 10, 0), (8192, 1000, 40, 0), (6000, 200, 40, 0), (6000, 3, 10, 3), (3000, 70, 4, 0),
+            (12000, 200, 4, 5)]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from _gpu import drp_amd
+    c = drp_amd.Ctx(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("period,at,small,chg", CASCADES)
+def test_cascade_parity(ctx, period, at, small, chg):
+    from _gpu import assert_same
+    wire = S.shadow_stream(int(16 * 2**20 / period), period=period, shadow_at=at, small=small, change_every=chg)
+    g = ctx.decode_batch(wire)
+    t = ctx.timing()
+    assert_same(g, O.decode_batch(wire), f"shadow {period}/{at}/{small}/{chg}")
+    assert t.strict_reruns == 0, "fell back to the exact kernel"
+
+
+def _c5_with_error(nframes, at, seed=5):
+    rng = random.Random(seed)
+    parts = [S.frame(S.change_payload(b"k%06d" % i, i + 1, i, i + 1, rng.randbytes(4096))) for i in range(nframes)]
+    bad = bytearray(parts[at])
+    bad[2] = 7  # the id byte after a 2-byte length: unknown type 7
+    parts[at] = bytes(bad)
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("at", [3, 500])
+def test_error_early_settles(ctx, at):
+    from _gpu import assert_same
+    wire = _c5_with_error(4000, at)
+    g = ctx.decode_batch(wire)
+    t = ctx.timing()
+    r = O.decode_batch(wire)
+    assert r["err_code"] != 0
+    assert_same(g, r, f"c5 error at {at}")
+    assert t.strict_reruns == 0, "fell back to the exact kernel"
+
+
+def test_cascade_512mb_under_50ms(ctx):
+    """A 512 MiB shadow stream (long random-payload frames: the exact kernel's slow case) decodes
+    on the device path in <= 50 ms, with the frame table checked against the generator."""
+    import ctypes as C
+
+    import torch
+
+    import bench
+    from _gpu import drp_amd
+    period = 6000
+    n = (512 << 20) // period
+    wire = S.shadow_stream(n, period=period, shadow_at=200, small=40)
+    dev = torch.device("cuda", 0)
+    w = torch.from_numpy(np.frombuffer(wire, np.uint8).copy()).to(dev)
+    so = torch.tensor([0, w.numel()], dtype=torch.int64, device=dev)
+    cap = n + 64
+    outs = bench.alloc_outputs(cap, dev)
+    res = torch.zeros(C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+    best = 1e9
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.decode_device(w, so, None, outs, cap, res)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    t = ctx.timing()
+    print(f"512 MiB shadow stream: {best * 1e3:.1f} ms, repair passes {t.spec_repairs}, "
+          f"segmented repairs {t.seg_repairs}, exact re-runs {t.strict_reruns}")
+    assert t.strict_reruns == 0 and t.seg_repairs >= 1
+    hdr = len(S.varint(period - 2)) + 1
+    off = outs["payload_off"][:n].cpu().numpy()
+    np.testing.assert_array_equal(off, np.arange(n, dtype=np.int64) * period + hdr)
+    assert (outs["type"][:n].cpu().numpy() == 2).all()
+    assert best <= 0.050, f"{best * 1e3:.1f} ms"
