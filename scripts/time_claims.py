@@ -1,0 +1,25 @@
+"""Decode C2 frames on the device a few times (for rocprofv3 kernel stats of ablated builds:
+their outputs are invalid by design). Usage: python scripts/time_claims.py [frames]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import ctypes as C  # noqa: E402
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import drp_amd  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 20_000_000
+dev = torch.device("cuda", 0)
+wire = bench.c2_on_device(n, seed=1234, dev=dev)
+so = torch.tensor([0, wire.numel()], dtype=torch.int64, device=dev)
+outs = bench.alloc_outputs(n + 64, dev)
+res = torch.zeros(C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+with drp_amd.Ctx(0) as ctx:
+    for _ in range(4):
+        ctx.decode_device(wire, so, None, outs, n + 64, res)
+    torch.cuda.synchronize()
+print("done")

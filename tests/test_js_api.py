@@ -227,3 +227,37 @@ def test_decoder_key_hash_option():
             po, ko, kl = int(r["payload_off"][k]), int(r["key_off"][k]), int(r["key_len"][k])
             raw.append(xxhash.xxh64_intdigest(wire[po + ko:po + ko + kl]))
     assert hashes == raw
+
+
+@pytest.mark.gpu
+@needs_node
+def test_encoder_input_policy():
+    """Encoder.change validates synchronously, as messages.Change.encode throws inside change()
+    (encode.js:102-117): key must be a string, change/from/to unsigned integers <= 2^53 - 1
+    (JS Number range; the reference's varint@3 would write larger doubles inexactly), missing
+    required fields throw; 2^53 - 1 is accepted. (GPU: the encoder opens its device context.)"""
+    code = r"""
+var enc = require(%r).encode()
+var cases = [
+  ['nokey', {change: 1, from: 0, to: 1}], ['numkey', {key: 5, change: 1, from: 0, to: 1}],
+  ['neg', {key: 'k', change: -1, from: 0, to: 1}], ['frac', {key: 'k', change: 1.5, from: 0, to: 1}],
+  ['big', {key: 'k', change: Math.pow(2, 53), from: 0, to: 1}], ['str', {key: 'k', change: '1', from: 0, to: 1}],
+  ['nofrom', {key: 'k', change: 1, to: 1}], ['max', {key: 'k', change: Number.MAX_SAFE_INTEGER, from: 0, to: 1}]]
+var out = {}
+cases.forEach(function (c) {
+  try { enc.change(c[1]); out[c[0]] = 'ok' } catch (e) { out[c[0]] = e.constructor.name + ': ' + e.message }
+})
+console.log(JSON.stringify(out))
+process.exit(0)
+""" % os.path.join(ROOT, "dat-replication-protocol_amd")
+    out = json.loads(subprocess.check_output([NODE, "-e", code], text=True, timeout=60))
+    assert out == {
+        "nokey": "Error: key is required",
+        "numkey": "TypeError: key must be a string",
+        "neg": "RangeError: change must be an unsigned integer",
+        "frac": "RangeError: change must be an unsigned integer",
+        "big": "RangeError: change must be an unsigned integer",
+        "str": "RangeError: change must be an unsigned integer",
+        "nofrom": "Error: from is required",
+        "max": "ok",
+    }
