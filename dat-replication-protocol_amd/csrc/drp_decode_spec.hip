@@ -58,7 +58,7 @@ constexpr uint32_t IMG = TILE + HALO;         // LDS image bytes (+32 slack)
 #define DRP_VALIDATE_ALL 0  // 1: validate a candidate's own change even behind a 1-byte varint
 #endif
 #ifndef DRP_K1_WAVES
-#define DRP_K1_WAVES 5  // min waves per SIMD for the claims kernel (LDS allows 5; 1.55 -> 1.34 ms at 20M frames)
+#define DRP_K1_WAVES 8  // min waves per SIMD for claims_fast (its occupancy without an LDS image, see DRP_K1_GIMG)
 #endif
 #ifndef DRP_LIST_PLAUSIBLE
 #define DRP_LIST_PLAUSIBLE 0  // 1: the list stage also checks Change payloads (the chain walks always do)
@@ -144,11 +144,12 @@ struct Img {
   const uint8_t *lds;  // LDS image: byte 0 = absolute position A
   const uint8_t *g;    // the batch in HBM (16-byte aligned)
   uint64_t A, se;
+  bool local = true;   // false: no LDS image (every header from HBM / L2)
   // header at absolute p < se: from LDS when its 16-byte window is inside the image,
   // else from HBM (two aligned 16-byte loads; only chains probed past the halo get here)
   __device__ __forceinline__ Hdr at(uint64_t p) const {
     uint64_t w0, w1;
-    if (p + 16 <= A + IMG) {
+    if (local && p + 16 <= A + IMG) {
       lds_win16(lds, (uint32_t)(p - A), w0, w1);
     } else {
       const uint64_t a = p & ~15ull;
@@ -196,7 +197,7 @@ bool change_ok(const uint8_t *lds, uint64_t A, uint64_t se, uint64_t po, uint64_
   return !cc.err || cc.err == ERR_UNREACHABLE;
 }
 __device__ __forceinline__ bool plausible(const Img &m, uint64_t p, const Hdr &h, bool any_len) {
-  if (h.id != 1 || (!any_len && h.vlen < 2) || h.succ > m.A + IMG) return true;
+  if (!m.local || h.id != 1 || (!any_len && h.vlen < 2) || h.succ > m.A + IMG) return true;
   return change_ok(m.lds, m.A, m.se, p + h.vlen + 1, h.L - 1);
 }
 
@@ -509,7 +510,10 @@ __device__ __forceinline__ uint64_t stage_live(const DecodeParams &P, const Tile
 constexpr uint32_t LLCAP = DRP_LLCAP;  // live positions per tile checked through the LDS list
 constexpr uint16_t NX_NEAR = 0xFFFD, NX_FAR = 0xFFFE, NX_DEAD = 0xFFFF;
 
-__global__ __launch_bounds__(NT, DRP_K1_WAVES) void spec_claims(DecodeParams P) {
+#ifndef DRP_K1G_WAVES
+#define DRP_K1G_WAVES 5  // min waves per SIMD for the general claims kernel (edge and dense tiles)
+#endif
+__global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint64_t xr[NT / WAVE];
   __shared__ uint32_t xf[NT / WAVE];
@@ -924,8 +928,18 @@ __device__ __forceinline__ void push_work(const DecodeParams &P, uint64_t t) {
 
 constexpr uint32_t HV = DRP_HALO_NODES ? HALO / SEGB : 0;  // halo "threads" with nodes
 // LDS of the fast claims form
+// claims_fast keeps no LDS image of the tile: every live position's header is parsed from the
+// L2 lines the tile load just brought in (the byte masks come from the loaded registers), so a
+// tile takes 6.2 KB of LDS instead of 15 and the kernel runs at 8 waves/SIMD (52 VGPRs) instead
+// of 5: the HBM stream of some workgroups overlaps the instruction-bound work of others
+// (C2 100M: 3.37 -> ~2.8 ms; C5: 3.77 -> ~2.4 ms).
+#ifndef DRP_K1_GIMG
+#define DRP_K1_GIMG 1  // 0: the LDS image (15 KB per tile, 5 waves/SIMD)
+#endif
 struct FastLds {
+#if !DRP_K1_GIMG
   __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+#endif
   uint64_t lmw[NT + HV];   // live masks; then strong masks
   uint64_t dmw[NT];        // undecided masks
   uint16_t loff[NT + HV];  // first list index of each thread
@@ -944,7 +958,11 @@ enum : uint32_t { FC_OK = 0, FC_DENSE = 1, FC_ABLATE = 2 };
 // FCAP live positions (the tile went to the general kernel's work list; nothing written).
 __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const TileGeo &G, uint64_t t, FastLds &S,
                                                 uint32_t &eb_o, uint32_t &en_o, uint32_t &ecn_o, uint64_t &cl_o) {
+#if DRP_K1_GIMG
+  uint8_t *buf = nullptr;
+#else
   uint8_t *buf = S.buf;
+#endif
   uint64_t *lmw = S.lmw, *dmw = S.dmw, *xm = S.xm;
   uint16_t *loff = S.loff, *lpos = S.lpos;
   uint32_t *hmx = S.hmx, *lnd = S.lnd, *xw = S.xw, *xf = S.xf, *wl = S.wl, *fl = S.fl;
@@ -958,10 +976,12 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     for (int k = 0; k < (int)(SEGB / 16); k++) v[k] = q[k];
     hv = tid < HALO / 16 ? *reinterpret_cast<const uint4 *>(P.bytes + G.A + TILE + tid * 16) : make_uint4(0, 0, 0, 0);
   }
+#if !DRP_K1_GIMG
 #pragma unroll
   for (int k = 0; k < (int)(SEGB / 16); k++) *reinterpret_cast<uint4 *>(buf + tid * SEGB + 16 * k) = v[k];
   if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = hv;
   if (tid < 2) *reinterpret_cast<uint4 *>(buf + IMG + tid * 16) = make_uint4(0, 0, 0, 0);
+#endif
   uint32_t mk[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) mk[k] = masks16(v[k]);
@@ -1048,7 +1068,11 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   constexpr uint32_t KPT = FCAP / NT;  // nodes per thread (at most)
   uint32_t ncode[KPT], npos[KPT];
   uint32_t na[KPT];
+#if DRP_K1_GIMG
+  const uint32_t *w32 = reinterpret_cast<const uint32_t *>(P.bytes + G.A);  // (L2: the tile was just read)
+#else
   const uint32_t *w32 = reinterpret_cast<const uint32_t *>(buf);
+#endif
 #pragma unroll
   for (uint32_t j = 0; j < KPT; j++) {
     const uint32_t i = tid + j * NT;
@@ -1188,7 +1212,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   return FC_ABLATE;
 #endif
   // restarts from deferred candidates, decided in HBM (big frames), as in spec_claims
-  const Img m{buf, P.bytes, G.A, G.se};
+  const Img m{buf, P.bytes, G.A, G.se, !DRP_K1_GIMG};
   uint32_t need = (E == RX_NONE && defer && !any_above(S0m, S1m, tid)) ? 1u : 0u;
   uint32_t js = (rx_node(E) && rx_off(E) < s1r) ? tid + 1 : 0u;  // last carrier + 1
   block_max2_u32(need, js, xf);
