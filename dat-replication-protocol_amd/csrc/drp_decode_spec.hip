@@ -457,6 +457,33 @@ __device__ __forceinline__ void stage(const DecodeParams &P, const TileGeo &G, u
   bsync();
 }
 
+// Stage the tile and its halo with LDS-DMA (global_load_lds_dwordx4: no VGPRs hold the image;
+// wave w's k-th load fills LDS bytes [4096 w + 1024 k, +1024) from the same offsets of the tile),
+// except near the end of the batch buffer (guarded register loads there).
+#ifndef DRP_EMIT_GLDS
+#define DRP_EMIT_GLDS 1
+#endif
+__device__ __forceinline__ void stage_glds(const DecodeParams &P, const TileGeo &G, uint8_t *buf) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  if (!DRP_EMIT_GLDS || G.A + IMG > P.nbytes) {
+    stage(P, G, buf);
+    return;
+  }
+  const uint8_t *g = P.bytes + G.A;
+#pragma unroll
+  for (uint32_t k = 0; k < TILE / (NT / WAVE) / 1024; k++) {
+    const uint32_t o = wid * (TILE / (NT / WAVE)) + k * 1024u;
+    __builtin_amdgcn_global_load_lds((const void *)(g + o + lane * 16u),
+                                     (__attribute__((address_space(3))) void *)(buf + o), 16, 0, 0);
+  }
+  if (wid == 0 && lane < HALO / 16)
+    __builtin_amdgcn_global_load_lds((const void *)(g + TILE + lane * 16u),
+                                     (__attribute__((address_space(3))) void *)(buf + TILE), 16, 0, 0);
+  if (tid < 2) *reinterpret_cast<uint4 *>(buf + IMG + tid * 16) = make_uint4(0, 0, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bsync();
+}
+
 // Stage the tile (64 B per thread, coalesced dwordx4) and its halo into LDS; returns the
 // thread's live mask: positions in [max(so, A), se) whose bytes can start a header with
 // id <= 2 (a varint terminator followed by a byte <= 2, reached through a run of MSB bytes).
@@ -1726,7 +1753,7 @@ __global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P)
   const uint32_t k0 = P.tile_k ? P.tile_k[t] : 0u;  // threads before e_t's (verify_lite)
   const uint8_t eb = tid < k0 ? (uint8_t)0xFF : P.ent[t * NT + tid];  // exact entry of this thread's bytes
   const uint8_t en = P.ent_n[t * NT + tid];   // exact frames from it (kernel 2)
-  stage(P, G, buf);
+  stage_glds(P, G, buf);
   const Img m{buf, P.bytes, A, se};
   const uint64_t lb = A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
   const uint64_t E = !(eb & 0x80) ? lb + (eb & 63) : NONE;
