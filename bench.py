@@ -545,7 +545,7 @@ def main():
     tile = args.tile or 8192
     exact = os.environ.get("DRP_DECODE") == "exact"
     kname = (f"decode_tiles<{tile // 64}>" if exact else
-             "speculative decode: spec_claims + verify_counts + tile scans + emit_tiles")
+             "speculative decode: claims_fast + verify_lite + tile scans + emit_tiles")
     gather = ("; drp_index_allgather (RCCL) of 32 B stream stats + index scan" if args.backend == "nccl" else
               "; gloo all-gather of 32 B stream stats + index scan") if dist else "; no collective (1 GPU)"
     if args.workload == "c2":

@@ -1,11 +1,15 @@
 """Per-kernel PMC summary of scripts/gpu_pmc.sh passes (gpurun_out/pmc/<pass>/): average per dispatch
-and per frame, FETCH_SIZE doubled per the gfx950 note. Usage: python scripts/pmc_kernels.py [frames]"""
+and per frame, FETCH_SIZE doubled per the gfx950 note (MI355X_MICROARCH.md: 128-B requests
+tallied at 64 B). Usage: python scripts/pmc_kernels.py [frames] [--write profiles/pmc_decode.json]"""
 import collections
 import csv
 import glob
+import json
 import sys
 
-frames = float(sys.argv[1]) if len(sys.argv) > 1 else 20e6
+KNAME = "speculative decode: claims_fast + verify_lite + tile scans + emit_tiles"  # = bench.py's kname
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+frames = float(args[0]) if args else 20e6
 tot = collections.defaultdict(float)
 disp = collections.defaultdict(set)
 for f in glob.glob("gpurun_out/pmc/*/**/*counter_collection.csv", recursive=True):
@@ -17,18 +21,30 @@ for f in glob.glob("gpurun_out/pmc/*/**/*counter_collection.csv", recursive=True
         tot[(k, r["Counter_Name"])] += float(r["Counter_Value"])
         disp[(k, r["Counter_Name"])].add((f, r["Dispatch_Id"]))
 kern = sorted({k for k, _ in tot})
+per = {}
 for k in kern:
     avg = {c: tot[(kk, c)] / len(disp[(kk, c)]) for kk, c in tot if kk == k}
     if "FETCH_SIZE" in avg:
         avg["FETCH_SIZE"] *= 2
     w = avg.get("SQ_WAVES", 0)
     out = [f"{k:22s}"]
-    for c in ["FETCH_SIZE", "WRITE_SIZE"]:
-        if c in avg:
-            out.append(f"{c[:5]}={avg[c] * 1024 / frames:6.1f}B/f")
+    rd = avg.get("FETCH_SIZE", 0) * 1024 / frames
+    wr = avg.get("WRITE_SIZE", 0) * 1024 / frames
+    per[k] = {"fetch_B_per_frame": round(rd, 2), "write_B_per_frame": round(wr, 2)}
+    out.append(f"FETCH={rd:6.1f}B/f WRITE={wr:6.1f}B/f")
     if w:
         out.append(f"waves={w:.0f}")
         for c in sorted(avg):
             if c.startswith("SQ_") and c != "SQ_WAVES":
                 out.append(f"{c[3:]}={avg[c] / w:.0f}")
+                per[k][c] = round(avg[c] / w, 1)
     print(" ".join(out))
+if "--write" in sys.argv:
+    path = sys.argv[sys.argv.index("--write") + 1]
+    dec = {k: v for k, v in per.items() if not k.startswith("enc")}
+    hbm = sum(v["fetch_B_per_frame"] + v["write_B_per_frame"] for v in dec.values())
+    json.dump({"kernel": KNAME, "workload": f"C2, {frames:g} frames (bench.py --frames {frames:g}), per dispatch",
+               "frames": frames, "note": "rocprofv3 --pmc, one pass per counter group (scripts/gpu_pmc.sh); "
+               "FETCH_SIZE doubled per MI355X_MICROARCH.md; per wave for SQ counters",
+               "hbm_bytes_per_frame": round(hbm, 2), "per_kernel": dec}, open(path, "w"), indent=1)
+    print("wrote", path, "hbm B/frame", round(hbm, 1))
