@@ -3,8 +3,8 @@
 //
 // Three passes over the rows: (1) frame sizes, (2) exclusive scan of the sizes
 // (per-block sums, then a single-block scan of the block sums), (3) one wave per frame
-// assembles its bytes: lane 0 writes the header and field prefixes, all 64 lanes copy the
-// key / subset / value bytes. Also the per-stream stats and global index scan used by the
+// assembles its bytes: the header and field prefixes are written lane-parallel from varints
+// packed in registers (lane j stores byte j), all 64 lanes copy the key / subset / value bytes. Also the per-stream stats and global index scan used by the
 // multi-GPU all-gather path.
 #include "drp_device.h"
 #include "drp_kernels.h"
@@ -159,6 +159,43 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
 #ifndef DRP_ENC_WAVES
 #define DRP_ENC_WAVES 65536  // waves of the write kernel (grid-stride over frames)
 #endif
+#ifndef DRP_ENC_LANEPREFIX
+#define DRP_ENC_LANEPREFIX 1  // 0: lane 0 writes the prefixes byte by byte from private arrays
+#endif
+
+// A varint (or one byte) packed into registers: bytes 0..7 in lo, 8..9 in hi.
+struct VSeg {
+  uint64_t lo;
+  uint32_t hi, n;
+};
+__device__ __forceinline__ VSeg vseg(uint64_t v) {
+  VSeg s{0ull, 0u, 0u};
+  for (;;) {
+    uint64_t b = v & 0x7F;
+    v >>= 7;
+    if (v) b |= 0x80;
+    if (s.n < 8) s.lo |= b << (8 * s.n);
+    else s.hi |= (uint32_t)b << (8 * (s.n - 8));
+    s.n++;
+    if (!v) return s;
+  }
+}
+__device__ __forceinline__ VSeg vbyte1(uint32_t b, bool present = true) { return VSeg{b, 0u, present ? 1u : 0u}; }
+// The concatenated segments, written lane-parallel: lane j stores byte j (segment lengths are
+// wave-uniform: every lane holds the same frame). Returns the total length.
+template <int N>
+__device__ __forceinline__ uint32_t put_segs(uint8_t *o, uint32_t lane, const VSeg (&g)[N]) {
+  uint32_t tot = 0, byte = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const uint32_t k = lane - tot;
+    if (lane >= tot && k < g[i].n) byte = (uint32_t)((k < 8 ? g[i].lo >> (8 * k) : (uint64_t)(g[i].hi >> (8 * (k - 8)))) & 0xFF);
+    tot += g[i].n;
+  }
+  if (lane < tot) o[lane] = (uint8_t)byte;
+  return tot;
+}
+
 // one wave per frame (grid-stride over frames)
 __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
   const uint32_t lane = lane_id();
@@ -170,6 +207,31 @@ __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
     uint8_t *o = P.out + P.frame_off[i];
     const uint32_t fl = s.flags[i];
     const uint64_t pl = payload_len(s, i);
+#if DRP_ENC_LANEPREFIX
+    const bool sub = (fl & DRP_F_SUBSET) != 0, val = (fl & DRP_F_VALUE) != 0;
+    uint64_t off;
+    {  // header (encode.js:124-137) + subset prefix
+      const VSeg g[4] = {vseg(pl + 1), vbyte1(DRP_TYPE_CHANGE), vbyte1(0x0a, sub),
+                         sub ? vseg(s.subset_len[i]) : VSeg{0ull, 0u, 0u}};
+      off = put_segs(o, lane, g);
+    }
+    if (sub) {
+      wave_copy(o + off, P.heap + s.subset_off[i], s.subset_len[i], lane);
+      off += s.subset_len[i];
+    }
+    {
+      const VSeg g[2] = {vbyte1(0x12), vseg(s.key_len[i])};
+      off += put_segs(o + off, lane, g);
+      wave_copy(o + off, P.heap + s.key_off[i], s.key_len[i], lane);
+      off += s.key_len[i];
+    }
+    {
+      const VSeg g[8] = {vbyte1(0x18), vseg(s.change[i]), vbyte1(0x20), vseg(s.from[i]), vbyte1(0x28), vseg(s.to[i]),
+                         vbyte1(0x32, val), val ? vseg(s.value_len[i]) : VSeg{0ull, 0u, 0u}};
+      off += put_segs(o + off, lane, g);
+    }
+    if (val) wave_copy(o + off, P.heap + s.value_off[i], s.value_len[i], lane);
+#else
     // header + subset prefix
     uint8_t pre[32];
     uint32_t h = venc(pl + 1, pre);
@@ -218,6 +280,7 @@ __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
       off += m;
     }
     if (fl & DRP_F_VALUE) wave_copy(o + off, P.heap + s.value_off[i], s.value_len[i], lane);
+#endif
   }
 }
 
