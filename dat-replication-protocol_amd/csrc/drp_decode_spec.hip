@@ -1736,23 +1736,68 @@ __device__ __forceinline__ void emit_frame(const DecodeParams &P, const Img &m, 
   if (c.err) badf = f < badf ? f : badf;
 }
 
-__global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P) {
+// A frame in the fast kernel: the frame table, and the Change columns when decode_change_fast
+// takes the payload (false: the tile goes to the general kernel).
+__device__ __forceinline__ bool emit_frame_fast(const DecodeParams &P, const Img &m, uint64_t p, uint64_t f,
+                                                uint64_t &badf) {
+  const Hdr h = hdr_fast(m, p);
+  if (f >= P.cap) return true;
+  const uint64_t po = p + h.vlen + 1, pl = h.L - 1;
+  P.payload_off[f] = po;
+  P.payload_len[f] = pl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pl;
+  P.type[f] = (uint8_t)(h.id | (h.kind == H_TAIL_BLOB ? DRP_FRAME_PARTIAL : 0u));
+  if (h.id != 1) return true;
+  const LdsReader rd{m.lds, m.A, umin64(m.A + IMG, m.se)};
+  ChangeCols c;
+  if (!decode_change_fast(rd, po, pl, c)) return false;
+  P.key_off[f] = c.key_off;
+  P.key_len[f] = c.key_len;
+  P.subset_off[f] = c.subset_off;
+  P.subset_len[f] = c.subset_len;
+  P.value_off[f] = c.value_off;
+  P.value_len[f] = c.value_len;
+  P.change[f] = c.change;
+  P.from[f] = c.from;
+  P.to[f] = c.to;
+  uint32_t fl = c.flags;
+  if (c.err == DRP_ERR_REQUIRED) fl |= DRP_F_MISSING;
+  P.flags[f] = (uint8_t)fl;
+  if (c.err) badf = f < badf ? f : badf;
+  return true;
+}
+
+#ifndef DRP_EMIT_FAST_WAVES
+#define DRP_EMIT_FAST_WAVES 6  // the fast emit kernel holds no general Change decoder: 6 waves/SIMD, no spills
+#endif
+#ifndef DRP_EMIT_SPLIT
+#define DRP_EMIT_SPLIT 1  // 0: one emit kernel with the general decoder inline (5 waves/SIMD)
+#endif
+// FAST (every tile): Change payloads in decode_change_fast's shapes are decoded here; a tile with
+// any other frame (or too many frames to list) is appended to P.vlist and re-emitted whole by the
+// general instance (!FAST, over that list), which rewrites the same values for the rest.
+template <bool FAST>
+__global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) void emit_tiles(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint16_t lst[LCAP];
   __shared__ uint32_t wsum[NT / WAVE];
+  __shared__ uint32_t defer;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wid = tid >> 6;
-  const uint64_t t = blockIdx.x;
   uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  const uint32_t nwork = (!FAST && P.vlist) ? *P.vlist_n : 0u;
+  for (uint32_t wi = blockIdx.x; (!FAST && P.vlist) ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
+  const uint64_t t = (!FAST && P.vlist) ? P.vlist[wi] : wi;
+  if (!FAST) bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
-  if (t >= ntiles) return;  // (whole workgroup)
+  if (t >= ntiles) continue;  // (whole workgroup)
   const uint64_t se = G.se, A = G.A;
   // the records load with the tile bytes, not after them
   const uint64_t base = P.tile_base[t];
   const uint32_t k0 = P.tile_k ? P.tile_k[t] : 0u;  // threads before e_t's (verify_lite)
   const uint8_t eb = tid < k0 ? (uint8_t)0xFF : P.ent[t * NT + tid];  // exact entry of this thread's bytes
   const uint8_t en = P.ent_n[t * NT + tid];   // exact frames from it (kernel 2)
+  if (FAST && tid == 0) defer = 0;
   stage_glds(P, G, buf);
   const Img m{buf, P.bytes, A, se};
   const uint64_t lb = A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
@@ -1772,6 +1817,10 @@ __global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P)
   uint32_t nch = 0, nbl = 0;
   uint64_t badf = ~0ull;
   const bool listed = count_t <= LCAP;
+  if (FAST && !listed) {  // very dense tile: the general kernel emits it per thread
+    if (tid == 0) P.vlist[atomicAdd(P.vlist_n, 1u)] = (uint32_t)t;
+    continue;
+  }
   // this thread's frames, in order: list them (or, for very dense tiles, emit them here)
   if (n) {
     uint32_t i = woff + ni - n;
@@ -1781,7 +1830,7 @@ __global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P)
       if (h.kind != H_VALID && h.kind != H_TAIL_BLOB) break;
       if (h.id != 0) {
         if (listed) lst[i] = (uint16_t)(p - A);
-        else emit_frame(P, m, p, base + i, nch, nbl, badf);
+        else if constexpr (!FAST) emit_frame(P, m, p, base + i, nch, nbl, badf);
         i++;
       }
       if (h.kind != H_VALID) break;
@@ -1790,13 +1839,25 @@ __global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P)
   }
   if (listed) {
     bsync();
-    for (uint32_t i = tid; i < count_t; i += NT) emit_frame(P, m, A + lst[i], base + i, nch, nbl, badf);
+    if constexpr (FAST) {
+      bool ok = true;
+      for (uint32_t i = tid; i < count_t; i += NT) ok &= emit_frame_fast(P, m, A + lst[i], base + i, badf);
+      if (!ok) defer = 1;
+      bsync();
+      if (defer) {  // the general kernel re-emits the whole tile (its payload errors too)
+        if (tid == 0) P.vlist[atomicAdd(P.vlist_n, 1u)] = (uint32_t)t;
+        continue;
+      }
+    } else {
+      for (uint32_t i = tid; i < count_t; i += NT) emit_frame(P, m, A + lst[i], base + i, nch, nbl, badf);
+    }
   }
   PHASE(13);
   (void)nch;
   (void)nbl;
   badf = lane_min64(badf);
   if (lane == 0 && badf != ~0ull) atomicMin((unsigned long long *)&P.payload_err[G.s], (unsigned long long)badf);
+  }
 }
 
 // ==== segmented repair: exact claims for an unsettled stream range ==============================
@@ -2119,7 +2180,16 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
   hipError_t e = drp_launch_tile_scan(Q.tile_count, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_base, Q.cap,
                                       Q.overflow, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(spec::emit_tiles, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  if (DRP_EMIT_SPLIT && Q.vlist) {  // the fast kernel, then the general one on the tiles it lists
+    e = hipMemsetAsync(Q.vlist_n, 0, 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(spec::emit_tiles<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+    hipLaunchKernelGGL(spec::emit_tiles<false>, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0,
+                       st, Q);
+  } else {
+    Q.vlist = nullptr;  // every tile in the general form
+    hipLaunchKernelGGL(spec::emit_tiles<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  }
   e = drp_launch_tile_scan(Q.tile_nch, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_nch_base, ~0ull, Q.overflow, st);
   if (e != hipSuccess) return e;
   return drp_launch_stream_counts(Q.tile_prefix, nstreams, Q.tile_count, Q.tile_base, Q.tile_nch, Q.tile_nch_base,

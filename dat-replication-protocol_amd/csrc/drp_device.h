@@ -337,6 +337,73 @@ bad:
   return c;
 }
 
+// decode_change restricted to the shapes encoders write (a one-byte field prefix of a known tag
+// and a 1..5-byte varint: every Change field up to 2^35), 32-bit offsets: true with the same
+// columns decode_change gives, or false for anything else (the caller then runs decode_change;
+// emit_tiles defers such tiles to a second kernel so the general decoder's registers stay out
+// of its main one).
+template <class R>
+__device__ __forceinline__ bool decode_change_fast(const R &rd, uint64_t pstart, uint64_t len, ChangeCols &c) {
+  c.key_off = c.key_len = c.subset_off = c.subset_len = c.value_off = c.value_len = 0;
+  c.change = c.from = c.to = 0;
+  c.flags = 0;
+  c.err = 0;
+  if (len > 0xFFFFFFFFull) return false;
+  const uint32_t n = (uint32_t)len;
+  uint32_t found = 0, off = 0;
+  while (off < n) {
+    const uint32_t avail = n - off;
+    if (avail < 2 || !rd.ok(pstart + off, 2)) return false;
+    uint32_t w, wn;
+    rd.win8(pstart + off, w, wn);
+    const uint32_t b0 = w & 0xFFu, tag = b0 >> 3;
+    const uint64_t x = ((((uint64_t)wn) << 32) | w) >> 8;  // bytes 1..7
+    const uint64_t tm = ~x & 0x8080808080ull;               // terminators among bytes 1..5
+    if (b0 >= 0x80u || tag < 1u || tag > 6u || !tm) return false;
+    const uint32_t k2 = ((uint32_t)__builtin_ctzll(tm) >> 3) + 1u;
+    if (k2 > avail - 1 || !rd.ok(pstart + off, 1 + k2)) return false;
+    const uint64_t v = ((x & 0x7Full) | ((x >> 1) & 0x3F80ull) | ((x >> 2) & 0x1FC000ull) | ((x >> 3) & 0xFE00000ull) |
+                        ((x >> 4) & 0x7F0000000ull)) &
+                       ((1ull << (7u * k2)) - 1ull);
+    if (tag == 3u || tag == 4u || tag == 5u) {
+      if (tag == 3u) {
+        c.change = v;
+        found |= 2;
+      } else if (tag == 4u) {
+        c.from = v;
+        found |= 4;
+      } else {
+        c.to = v;
+        found |= 8;
+      }
+      off += 1u + k2;
+    } else {
+      const uint32_t o2 = off + 1u + k2;
+      if (v > (uint64_t)(n - o2)) return false;
+      const uint32_t v32 = (uint32_t)v;
+      if (tag == 1u) {
+        c.subset_off = o2;
+        c.subset_len = v32;
+        c.flags |= DRP_F_SUBSET;
+      } else if (tag == 2u) {
+        c.key_off = o2;
+        c.key_len = v32;
+        found |= 1;
+      } else {
+        c.value_off = o2;
+        c.value_len = v32;
+        c.flags |= DRP_F_VALUE;
+      }
+      off = o2 + v32;
+    }
+  }
+  if (found != 15) {
+    c.err = DRP_ERR_REQUIRED;
+    c.flags |= DRP_F_BAD;
+  }
+  return true;
+}
+
 // ---- byte-class bit masks (live-position scan) ------------------------------------
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
