@@ -420,7 +420,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   CHK(hipMemsetAsync(rec, 0, 2 * NT * 8, st));  // claim, incl_e
   CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
   CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
-  CHK(hipMemsetAsync(ctrl, 0, 32, st));
+  CHK(hipMemsetAsync(ctrl, 0, 64, st));
   CHK(drp_launch_tile_prefix(B, stream_off, ns, tile_prefix, st));
   DecodeParams P;
   memset(&P, 0, sizeof(P));
@@ -464,6 +464,12 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.vlist_n = ctrl + 5;
   P.tile_k = c->scratch.at<uint8_t>(L.tk);
   P.first_miss = c->scratch.at<uint64_t>(L.fmiss);
+  // dirty lists (ping-pong, after the work list and vlist in rec): the tiles each verify pass's
+  // repairs handed to the next pass; counts at ctrl[8 + k], overflow words at ctrl[10 + k]
+  uint32_t *dl[2] = {reinterpret_cast<uint32_t *>(rec + 3 * NT), reinterpret_cast<uint32_t *>(rec + 3 * NT) + NT};
+  P.dlist = dl[0];
+  P.dlist_n = ctrl + 8;
+  P.dlist_cap = NT;
   CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
   unsigned long long *dstats = nullptr;
   if (getenv("DRP_STATS")) {
@@ -478,15 +484,18 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   // missed tiles' claims, so verify runs again (each pass fixes at least the first missed tile,
   // whose entry is exact) until a pass has no miss. Only when that does not settle within a
   // few passes (e.g. a protocol error on the exact chain) does the caller run the exact kernel.
-  uint32_t h[8];
+  uint32_t h[16];
   CHK(drp_launch_spec_head(&P, NT, ns, tstream, st));
-  CHK(hipMemcpyAsync(h, ctrl, 32, hipMemcpyDeviceToHost, st));
+  CHK(hipMemcpyAsync(h, ctrl, 64, hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
   const uint32_t relisted = h[5];
   const uint32_t miss = drp_spec_miss_bit();
   int pass = 0;
   bool seg_done = false;
   if ((h[1] & drp_spec_retry_mask()) == miss) {
+    // the next pass verifies the dirty list the last one wrote (k: its index), or every tile
+    uint32_t k = 0;
+    bool full = h[10] != 0 || h[8] > NT;
     for (; pass < kSpecRepairPasses && (h[1] & miss); pass++) {
       if (pass >= kSegRepairAfter && !seg_done) {
         // the misses keep coming one tile per pass (wrong predictions that agree with each
@@ -503,15 +512,32 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
                   (unsigned long long)fm[s], (unsigned long long)tp[s + 1]);
             CHK(drp_launch_seg_repair(&P, s, fm[s], tp[s + 1], c->scratch.at<uint64_t>(L.segw), st));
             c->timing.seg_repairs++;
+            full = true;  // (claims rewritten over a range)
           }
       }
       CHK(hipMemsetAsync(P.incl_e, 0, NT * 8, st));
       CHK(hipMemsetAsync(P.overflow, 0, 4, st));
       CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
       CHK(hipMemsetAsync(P.vlist_n, 0, 4, st));
-      CHK(drp_launch_spec_verify(&P, NT, ns, tstream, st));
-      CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
+      const uint32_t kn = k ^ 1u;  // this pass's dirty list
+      CHK(hipMemsetAsync(ctrl + 8 + kn, 0, 4, st));
+      CHK(hipMemsetAsync(ctrl + 10 + kn, 0, 4, st));
+      DecodeParams V = P;
+      V.dlist = dl[kn];
+      V.dlist_n = ctrl + 8 + kn;
+      if (full) {
+        CHK(drp_launch_spec_verify(&V, NT, ns, tstream, st));
+      } else {
+        V.vlist = dl[k];
+        V.vlist_n = ctrl + 8 + k;
+        CHK(drp_launch_spec_verify_list(&V, h[8 + k], ns, tstream, st));
+      }
+      CHK(hipMemcpyAsync(h, ctrl, 64, hipMemcpyDeviceToHost, st));
       CHK(hipStreamSynchronize(st));
+      TRACE("decode_spec: pass %d over %s (%u tiles), %u listed next", pass + 1, full ? "every tile" : "the dirty list",
+            full ? (unsigned)NT : h[8 + k], h[8 + kn]);
+      k = kn;
+      full = h[10 + k] != 0 || h[8 + k] > NT;
       if (trace_on()) {
         uint64_t f0 = 0;
         CHK(hipMemcpy(&f0, P.first_miss, 8, hipMemcpyDeviceToHost));

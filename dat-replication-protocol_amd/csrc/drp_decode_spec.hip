@@ -1571,6 +1571,19 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
       // so a miss-free pass saw a constant claim array and its proof holds).
       P.claim[t] = inside ? exit_t : C_ID;
       if (P.first_miss) atomicMin((unsigned long long *)&P.first_miss[G.s], (unsigned long long)t);
+      if (P.dlist) {
+        // the tiles whose entry this repair changes: t + 1 and, through identity claims, up to
+        // the first later tile with a claim of its own (a longer run: the next pass is a full one)
+        const uint64_t tend = P.tile_prefix[G.s + 1];
+        uint64_t j = t + 1;
+        uint32_t r = 0;
+        for (; j < tend && r < 64u; j++, r++) {
+          const uint32_t q = atomicAdd(P.dlist_n, 1u);
+          if (q < P.dlist_cap) P.dlist[q] = (uint32_t)j;
+          if (P.claim[j] != C_ID) break;
+        }
+        if (r == 64u) atomicOr(P.dlist_n + 2, 1u);  // (the list's overflow word)
+      }
       if (P.stats) {  // debug capture (DRP_STATS=1): the first misses
         const unsigned long long q = atomicAdd(&P.stats[0], 1ull);
         if (q < 5) {
@@ -2168,6 +2181,17 @@ extern "C" hipError_t drp_launch_spec_verify(const DecodeParams *P, uint64_t nt_
   } else {
     hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
   }
+  return hipGetLastError();
+}
+
+// A repair pass over the tiles the previous pass listed (P->vlist / P->vlist_n: its dirty list,
+// n entries), appending to P->dlist.
+extern "C" hipError_t drp_launch_spec_verify_list(const DecodeParams *P, uint64_t n, uint64_t nstreams,
+                                                  uint32_t *tile_stream, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  DecodeParams Q = *P;
+  Q.tile_stream = nstreams > 1 ? tile_stream : nullptr;
+  hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)(n < 16384 ? n : 16384)), dim3(spec::NT), 0, st, Q);
   return hipGetLastError();
 }
 

@@ -57,6 +57,11 @@ struct DecodeParams {
   uint32_t *vlist, *vlist_n;
   uint8_t *tile_k;
   uint64_t *first_miss;  // per stream: the first tile a verify pass repaired (~0: none)
+  // verify_counts appends the tiles whose entry a repair changed (the next repair pass verifies
+  // only those); a count past dlist_cap or a nonzero dlist_n[2] means the next pass must be a
+  // full one
+  uint32_t *dlist, *dlist_n;
+  uint64_t dlist_cap;
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
   unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
 };
@@ -89,6 +94,8 @@ hipError_t drp_launch_seg_repair(const drp::DecodeParams *P, uint64_t s, uint64_
                                  hipStream_t st);
 hipError_t drp_launch_spec_verify(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                   uint32_t *tile_stream, hipStream_t st);
+hipError_t drp_launch_spec_verify_list(const drp::DecodeParams *P, uint64_t n, uint64_t nstreams,
+                                       uint32_t *tile_stream, hipStream_t st);
 hipError_t drp_launch_spec_tail(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                 uint32_t *tile_stream, uint64_t *scan_tmp, hipStream_t st);
 // exclusive scan of a per-tile u64 array over all tiles; flags capacity overflow of the total
