@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/drp.h"
@@ -397,6 +398,7 @@ int run_decode_exact(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const ui
 // The default decode: speculate-and-verify kernel (drp_decode_spec.hip). Returns DRP_E_RETRY
 // when a prediction failed (or a bounded wait expired): the caller then runs the exact kernel.
 constexpr int kSpecRepairPasses = 16;
+constexpr int kChain = 3;  // dirty-list repair passes queued per host read
 constexpr int kSegRepairAfter = 3;  // verify passes before the segmented repair of the streams still missing  // one verify pass each (0.7 ms on C5), vs ~1.5 s for an exact re-run there
 
 int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
@@ -470,6 +472,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.dlist = dl[0];
   P.dlist_n = ctrl + 8;
   P.dlist_cap = NT;
+  if (const char *e = getenv("DRP_DIRTY_CAP")) P.dlist_cap = std::min<uint64_t>(NT, strtoull(e, nullptr, 10));  // (tests)
   CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
   unsigned long long *dstats = nullptr;
   if (getenv("DRP_STATS")) {
@@ -495,7 +498,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   if ((h[1] & drp_spec_retry_mask()) == miss) {
     // the next pass verifies the dirty list the last one wrote (k: its index), or every tile
     uint32_t k = 0;
-    bool full = h[10] != 0 || h[8] > NT;
+    bool full = h[10] != 0 || h[8] > P.dlist_cap;
     for (; pass < kSpecRepairPasses && (h[1] & miss); pass++) {
       if (pass >= kSegRepairAfter && !seg_done) {
         // the misses keep coming one tile per pass (wrong predictions that agree with each
@@ -515,29 +518,36 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
             full = true;  // (claims rewritten over a range)
           }
       }
-      CHK(hipMemsetAsync(P.incl_e, 0, NT * 8, st));
-      CHK(hipMemsetAsync(P.overflow, 0, 4, st));
-      CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
-      CHK(hipMemsetAsync(P.vlist_n, 0, 4, st));
-      const uint32_t kn = k ^ 1u;  // this pass's dirty list
-      CHK(hipMemsetAsync(ctrl + 8 + kn, 0, 4, st));
-      CHK(hipMemsetAsync(ctrl + 10 + kn, 0, 4, st));
-      DecodeParams V = P;
-      V.dlist = dl[kn];
-      V.dlist_n = ctrl + 8 + kn;
-      if (full) {
-        CHK(drp_launch_spec_verify(&V, NT, ns, tstream, st));
-      } else {
-        V.vlist = dl[k];
-        V.vlist_n = ctrl + 8 + k;
-        CHK(drp_launch_spec_verify_list(&V, h[8 + k], ns, tstream, st));
+      // a full pass alone; dirty-list passes kChain at a time with one host read at the end
+      // (a pass whose input list is empty launches nothing but the memsets)
+      const int chain = full ? 1 : std::min(kChain, kSpecRepairPasses - pass);
+      for (int cp = 0; cp < chain; cp++) {
+        CHK(hipMemsetAsync(P.incl_e, 0, NT * 8, st));
+        CHK(hipMemsetAsync(P.overflow, 0, 4, st));
+        CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
+        CHK(hipMemsetAsync(P.vlist_n, 0, 4, st));
+        const uint32_t kn = k ^ 1u;  // this pass's dirty list
+        CHK(hipMemsetAsync(ctrl + 8 + kn, 0, 4, st));
+        CHK(hipMemsetAsync(ctrl + 10 + kn, 0, 4, st));
+        DecodeParams V = P;
+        V.dlist = dl[kn];
+        V.dlist_n = ctrl + 8 + kn;
+        if (full) {
+          CHK(drp_launch_spec_verify(&V, NT, ns, tstream, st));
+        } else {
+          V.vlist = dl[k];
+          V.vlist_n = ctrl + 8 + k;
+          V.vlist_ovf = ctrl + 10 + k;
+          CHK(drp_launch_spec_verify_list(&V, cp == 0 ? h[8 + k] : ~0ull, ns, tstream, st));
+        }
+        k = kn;
       }
       CHK(hipMemcpyAsync(h, ctrl, 64, hipMemcpyDeviceToHost, st));
       CHK(hipStreamSynchronize(st));
-      TRACE("decode_spec: pass %d over %s (%u tiles), %u listed next", pass + 1, full ? "every tile" : "the dirty list",
-            full ? (unsigned)NT : h[8 + k], h[8 + kn]);
-      k = kn;
-      full = h[10 + k] != 0 || h[8 + k] > NT;
+      TRACE("decode_spec: passes %d-%d over %s, %u listed next", pass + 1, pass + chain,
+            full ? "every tile" : "dirty lists", h[8 + k]);
+      pass += chain - 1;
+      full = h[10 + k] != 0 || h[8 + k] > P.dlist_cap;
       if (trace_on()) {
         uint64_t f0 = 0;
         CHK(hipMemcpy(&f0, P.first_miss, 8, hipMemcpyDeviceToHost));

@@ -1435,6 +1435,13 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   // every tile (one per workgroup), or the tiles verify_lite listed (a few per workgroup)
   const uint32_t nwork = P.vlist ? *P.vlist_n : 0u;
+  if (P.vlist_ovf && (*P.vlist_ovf || nwork > P.dlist_cap)) {  // an incomplete dirty list: the host
+    if (blockIdx.x == 0 && tid == 0) {                          // runs a full pass next
+      atomicOr(P.dlist_n + 2, 1u);
+      atomicOr(P.overflow, F_MISS);
+    }
+    return;
+  }
   for (uint32_t wi = blockIdx.x; P.vlist ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
   const uint64_t t = P.vlist ? P.vlist[wi] : wi;
   bsync();  // the previous tile's LDS reads are done
@@ -2188,10 +2195,11 @@ extern "C" hipError_t drp_launch_spec_verify(const DecodeParams *P, uint64_t nt_
 // n entries), appending to P->dlist.
 extern "C" hipError_t drp_launch_spec_verify_list(const DecodeParams *P, uint64_t n, uint64_t nstreams,
                                                   uint32_t *tile_stream, hipStream_t st) {
-  if (n == 0) return hipSuccess;
+  if (n == 0) return hipSuccess;  // (n = ~0: the count is on the device only)
   DecodeParams Q = *P;
   Q.tile_stream = nstreams > 1 ? tile_stream : nullptr;
-  hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)(n < 16384 ? n : 16384)), dim3(spec::NT), 0, st, Q);
+  const uint64_t g = n == ~0ull ? 1024 : (n < 16384 ? n : 16384);
+  hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)g), dim3(spec::NT), 0, st, Q);
   return hipGetLastError();
 }
 

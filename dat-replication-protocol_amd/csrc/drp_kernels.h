@@ -62,6 +62,7 @@ struct DecodeParams {
   // full one
   uint32_t *dlist, *dlist_n;
   uint64_t dlist_cap;
+  uint32_t *vlist_ovf;  // vlist is a dirty list: its overflow word (set: pass the overflow on, verify nothing)
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
   unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
 };

@@ -37,6 +37,26 @@ def test_cascade_parity(ctx, period, at, small, chg):
     assert t.strict_reruns == 0, "fell back to the exact kernel"
 
 
+@pytest.mark.parametrize("cap", ["1", "0"])
+def test_dirty_list_overflow_full_pass(ctx, monkeypatch, cap):
+    """Repair passes verify only the tiles a repair changed (dirty lists, drp_api.hip); a list
+    past its capacity (forced here with DRP_DIRTY_CAP) must fall back to a full verify pass with
+    the same results. A 600 KB blob after the shadow's start also gives a miss whose successors
+    run through identity claims (the run cap of 64 tiles)."""
+    from _gpu import assert_same
+    monkeypatch.setenv("DRP_DIRTY_CAP", cap)
+    for period, at, small, chg in CASCADES[:3]:
+        wire = S.shadow_stream(int(8 * 2**20 / period), period=period, shadow_at=at, small=small, change_every=chg)
+        g = ctx.decode_batch(wire)
+        assert_same(g, O.decode_batch(wire), f"shadow {period}/{at}/{small}/{chg} cap {cap}")
+        assert ctx.timing().strict_reruns == 0, "fell back to the exact kernel"
+    rng = random.Random(7)
+    parts = [S.frame(S.change_payload(b"k%06d" % i, i + 1, i, i + 1, rng.randbytes(4096))) for i in range(300)]
+    parts.insert(150, S.frame(b"\x01\x02" * 300_000, 2))
+    wire = b"".join(parts)
+    assert_same(ctx.decode_batch(wire), O.decode_batch(wire), f"blob run cap {cap}")
+
+
 def _c5_with_error(nframes, at, seed=5):
     rng = random.Random(seed)
     parts = [S.frame(S.change_payload(b"k%06d" % i, i + 1, i, i + 1, rng.randbytes(4096))) for i in range(nframes)]
