@@ -472,6 +472,10 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.dlist = dl[0];
   P.dlist_n = ctrl + 8;
   P.dlist_cap = NT;
+  P.dstamp = reinterpret_cast<uint32_t *>(rec + 4 * NT);  // (after the dirty lists)
+  P.pass_id = 1;
+  if (const char *e = getenv("DRP_KSTRONG_HBM")) P.kstrong_hbm = atoi(e);  // (tests: weaker predictions)
+  CHK(hipMemsetAsync(P.dstamp, 0, NT * 4, st));
   if (const char *e = getenv("DRP_DIRTY_CAP")) P.dlist_cap = std::min<uint64_t>(NT, strtoull(e, nullptr, 10));  // (tests)
   CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
   unsigned long long *dstats = nullptr;
@@ -532,6 +536,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
         DecodeParams V = P;
         V.dlist = dl[kn];
         V.dlist_n = ctrl + 8 + kn;
+        V.pass_id = (uint32_t)(pass + cp + 2);
         if (full) {
           CHK(drp_launch_spec_verify(&V, NT, ns, tstream, st));
         } else {

@@ -231,12 +231,13 @@ enum : uint32_t { S_DEAD = 0, S_OK = 1, S_HBM = 2 };
 #endif
 template <bool LOCAL>
 __device__ __forceinline__ uint32_t strong(const Img &m, uint64_t c, uint64_t s1, uint64_t &R, uint32_t &n,
-                                           bool &far) {
+                                           bool &far, int khbm = 0) {
   uint64_t p = c;
   n = 0;
   R = NONE;
   far = false;
-  constexpr int K = LOCAL ? KSTRONG : DRP_KSTRONG_HBM;  // frames a deferred candidate survives in HBM
+  // frames a deferred candidate survives in HBM (khbm: a weaker test prediction, DecodeParams)
+  const int K = LOCAL ? KSTRONG : (khbm ? khbm : DRP_KSTRONG_HBM);
 #pragma unroll 1
   for (int k = 0; k < K; k++) {
     if (p >= m.se) break;  // reached the stream end: survived
@@ -748,7 +749,7 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
         uint64_t r;
         uint32_t k;
         bool f;
-        if (strong<false>(m, lb + o, s1, r, k, f) == S_OK) {
+        if (strong<false>(m, lb + o, s1, r, k, f, P.kstrong_hbm) == S_OK) {
           g = lb + o;
           E = g;
           R = r;
@@ -1254,7 +1255,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
         uint64_t r;
         uint32_t k;
         bool f;
-        if (strong<false>(m, G.A + lb + o, G.A + s1r, r, k, f) == S_OK) {
+        if (strong<false>(m, G.A + lb + o, G.A + s1r, r, k, f, P.kstrong_hbm) == S_OK) {
           g = (off + (uint32_t)__builtin_popcountll(live & ((1ull << o) - 1ull))) | ((lb + o) << 16);
           E = g;
           R = fwalk(lnd, g, s1r, n);
@@ -1424,6 +1425,9 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
   P.tile_k[t] = (uint8_t)k;
 }
 
+#ifndef DRP_DIRTY_DEDUPE
+#define DRP_DIRTY_DEDUPE 1  // 0: no per-pass stamps (A/B of the duplicate-entry race the tests pin)
+#endif
 __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint64_t xr[NT / WAVE];
@@ -1585,8 +1589,12 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
         uint64_t j = t + 1;
         uint32_t r = 0;
         for (; j < tend && r < 64u; j++, r++) {
-          const uint32_t q = atomicAdd(P.dlist_n, 1u);
-          if (q < P.dlist_cap) P.dlist[q] = (uint32_t)j;
+          // once per tile per list: two workgroups verifying one tile in the same pass would race
+          // on its records (the slow path rewrites them while the other reads them)
+          if (!DRP_DIRTY_DEDUPE || atomicMax(&P.dstamp[j], P.pass_id) < P.pass_id) {
+            const uint32_t q = atomicAdd(P.dlist_n, 1u);
+            if (q < P.dlist_cap) P.dlist[q] = (uint32_t)j;
+          }
           if (P.claim[j] != C_ID) break;
         }
         if (r == 64u) atomicOr(P.dlist_n + 2, 1u);  // (the list's overflow word)

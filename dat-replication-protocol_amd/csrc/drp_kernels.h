@@ -63,6 +63,9 @@ struct DecodeParams {
   uint32_t *dlist, *dlist_n;
   uint64_t dlist_cap;
   uint32_t *vlist_ovf;  // vlist is a dirty list: its overflow word (set: pass the overflow on, verify nothing)
+  uint32_t *dstamp;     // per tile: the last pass id whose dirty list holds it (one entry per tile per list)
+  uint32_t pass_id;     // this verify pass (1: the head's; zeroed stamps before it)
+  int kstrong_hbm;      // 0: DRP_KSTRONG_HBM; else frames a deferred candidate must survive (tests)
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
   unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
 };
