@@ -412,18 +412,26 @@ __device__ __forceinline__ uint64_t lane_min64(uint64_t v) {
   } while (0)
 
 // Tile geometry shared by both kernels.
+// A load through the constant address space: a scalar load (s_load, no vmcnt) for a uniform
+// address. Only for arrays no kernel that uses it writes (the stream and tile geometry, and the
+// output bases in emit_tiles).
+template <class T>
+__device__ __forceinline__ T ldc(const T *p) {
+  return *reinterpret_cast<const __attribute__((address_space(4))) T *>(reinterpret_cast<uintptr_t>(p));
+}
+
 struct TileGeo {
   uint64_t s, tf, so, se, A, e0;
 };
 __device__ __forceinline__ TileGeo tile_geo(const DecodeParams &P, uint64_t t) {
   TileGeo G;
-  G.s = P.tile_stream ? P.tile_stream[t] : 0;
+  G.s = P.tile_stream ? ldc(P.tile_stream + t) : 0;
   if (G.s >= P.nstreams) G.s = P.nstreams - 1;  // (t past the last tile: read before the exit check)
-  G.tf = P.tile_prefix[G.s];
-  G.so = P.stream_off[G.s];
-  G.se = P.stream_off[G.s + 1];
+  G.tf = ldc(P.tile_prefix + G.s);
+  G.so = ldc(P.stream_off + G.s);
+  G.se = ldc(P.stream_off + G.s + 1);
   G.A = (G.so & ~(uint64_t)(TILE - 1)) + (t - G.tf) * TILE;
-  G.e0 = G.so + (P.entry ? P.entry[G.s] : 0ull);
+  G.e0 = G.so + (P.entry ? ldc(P.entry + G.s) : 0ull);
   return G;
 }
 
@@ -1821,7 +1829,7 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
   if (t >= ntiles) continue;  // (whole workgroup)
   const uint64_t se = G.se, A = G.A;
   // the records load with the tile bytes, not after them
-  const uint64_t base = P.tile_base[t];
+  const uint64_t base = ldc(P.tile_base + t);
   const uint32_t k0 = P.tile_k ? P.tile_k[t] : 0u;  // threads before e_t's (verify_lite)
   const uint8_t eb = tid < k0 ? (uint8_t)0xFF : P.ent[t * NT + tid];  // exact entry of this thread's bytes
   const uint8_t en = P.ent_n[t * NT + tid];   // exact frames from it (kernel 2)
