@@ -1805,6 +1805,9 @@ __device__ __forceinline__ bool emit_frame_fast(const DecodeParams &P, const Img
 #ifndef DRP_EMIT_FAST_WAVES
 #define DRP_EMIT_FAST_WAVES 6  // the fast emit kernel holds no general Change decoder: 6 waves/SIMD, no spills
 #endif
+#ifndef DRP_EMIT_XCD
+#define DRP_EMIT_XCD 1  // fast emit: XCD-contiguous tile order
+#endif
 #ifndef DRP_EMIT_SPLIT
 #define DRP_EMIT_SPLIT 1  // 0: one emit kernel with the general decoder inline (5 waves/SIMD)
 #endif
@@ -1823,7 +1826,11 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   const uint32_t nwork = (!FAST && P.vlist) ? *P.vlist_n : 0u;
   for (uint32_t wi = blockIdx.x; (!FAST && P.vlist) ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
-  const uint64_t t = (!FAST && P.vlist) ? P.vlist[wi] : wi;
+  uint64_t t = (!FAST && P.vlist) ? P.vlist[wi] : wi;
+  if (FAST && DRP_EMIT_XCD) {  // workgroups go to the 8 XCDs round-robin: give each XCD one
+    const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = wi % 8u;  // contiguous eighth, so
+    t = (uint64_t)x * q + min(x, r) + wi / 8u;  // neighbouring tiles share an L2 (column lines)
+  }
   if (!FAST) bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
   if (t >= ntiles) continue;  // (whole workgroup)
