@@ -70,6 +70,12 @@ bool is_device_ptr(const void *p) {
 
 size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
+double now_ms() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+
 }  // namespace
 
 struct drp_ctx {
@@ -79,11 +85,12 @@ struct drp_ctx {
   uint32_t B = 128;
   int strict = 0;
   int exact = 0;  // 1: always the exact kernel (decode_tiles), never the speculative one
-  int key_post = 0;  // drp_decode_stage computes key hashes / key flags
+  int key_post = 0;  // DRP_KEY_POST_*: key hashes and/or key flags on every decode
   int cus = 256;
   uint32_t waves_per_cu = 16;
   DevBuf scratch, in_stage, out_stage, aux;
   DevBuf dec_cols;  // device columns of the staged host-batch decode (drp_decode_stage)
+  double frames_per_byte = 0;  // density of the last staged batch (sizes the next one's columns)
   drp_timing timing = {};
   std::vector<uint64_t> host_tmp;
   // the staged host-batch decode: row 0 is a host-built blob continuation when nf0 == 1; GPU
@@ -110,6 +117,18 @@ struct drp_ctx {
 extern "C" {
 
 int drp_abi_version(void) { return DRP_ABI_VERSION; }
+
+int drp_device_count(int *n) {
+  if (!n) return DRP_E_INVAL;
+  *n = 0;
+  int k = 0;
+  if (hipGetDeviceCount(&k) != hipSuccess) {
+    (void)hipGetLastError();
+    return DRP_OK;  // no runtime / no device: zero devices
+  }
+  *n = k;
+  return DRP_OK;
+}
 
 int drp_open(int device, drp_ctx **out) {
   if (!out) return DRP_E_INVAL;
@@ -183,9 +202,9 @@ int drp_set_exact(drp_ctx *c, int exact) {
   return DRP_OK;
 }
 
-int drp_set_key_post(drp_ctx *c, int on) {
-  if (!c) return DRP_E_INVAL;
-  c->key_post = on ? 1 : 0;
+int drp_set_key_post(drp_ctx *c, int mode) {
+  if (!c || mode < DRP_KEY_POST_OFF || mode > DRP_KEY_POST_FLAGS) return DRP_E_INVAL;
+  c->key_post = mode;
   return DRP_OK;
 }
 
@@ -198,7 +217,7 @@ int drp_set_strict(drp_ctx *c, int strict) {
 // scratch layout for a decode of `nbytes` over `ns` streams
 struct DecLayout {
   uint64_t ntiles_max;
-  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, tstream, ent, tk, fmiss, segw, scan_tmp, total;
+  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, tstream, ent, tk, tsp, fmiss, segw, scan_tmp, total;
   uint64_t nsg;
 };
 static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
@@ -217,6 +236,7 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.tstream = o; o += al(L.ntiles_max * 4);    // tile -> stream (speculative kernel)
   L.ent = o; o += al(L.ntiles_max * 128 * 3);  // per-thread entries + counts (speculative kernel)
   L.tk = o; o += al(L.ntiles_max);             // first entry thread per tile (verify_lite)
+  L.tsp = o; o += al(L.ntiles_max);            // sparse-tile marks (verify_lite -> emit_sparse)
   L.fmiss = o; o += al(ns * 8);                  // first missed tile per stream (verify)
   L.segw = o; o += al((2 * 64 * 1024 + 1025) * 8);  // segmented repair: candidates + entries
   L.scan_tmp = o; o += al((L.ntiles_max / 4096 + 2) * 8);  // tile scans: block sums
@@ -333,7 +353,8 @@ int run_decode_exact_once(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, con
   CHK(hipEventRecord(c->ev[2], st));
   CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
                           scount, fr->type, co->flags, cap, res, st));
-  CHK(drp_launch_key_post(bytes, tile_prefix, ns, P.tile_base, P.tile_count, cap, fr, co, st));
+  CHK(drp_launch_key_post(bytes, tile_prefix, ns, P.tile_base, P.tile_count, cap, fr, co,
+                          c->key_post == DRP_KEY_POST_FLAGS, st));
   CHK(hipEventRecord(c->ev[3], st));
   uint32_t h[2];
   CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
@@ -399,6 +420,8 @@ int run_decode_exact(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const ui
 // when a prediction failed (or a bounded wait expired): the caller then runs the exact kernel.
 constexpr int kSpecRepairPasses = 16;
 constexpr int kChain = 3;  // dirty-list repair passes queued per host read
+constexpr uint64_t kSegFramesMax = 4096;      // frames per segment past which the exact kernel is cheaper
+constexpr uint64_t kSegDenseMinTiles = 8192;  // (ranges under 64 MiB always take the segmented repair)
 constexpr int kSegRepairAfter = 3;  // verify passes before the segmented repair of the streams still missing  // one verify pass each (0.7 ms on C5), vs ~1.5 s for an exact re-run there
 
 int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
@@ -465,6 +488,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.vlist = reinterpret_cast<uint32_t *>(rec + 2 * NT) + NT;  // (after the dense work list)
   P.vlist_n = ctrl + 5;
   P.tile_k = c->scratch.at<uint8_t>(L.tk);
+  P.tile_sparse = c->scratch.at<uint8_t>(L.tsp);
   P.first_miss = c->scratch.at<uint64_t>(L.fmiss);
   // dirty lists (ping-pong, after the work list and vlist in rec): the tiles each verify pass's
   // repairs handed to the next pass; counts at ctrl[8 + k], overflow words at ctrl[10 + k]
@@ -513,6 +537,30 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
         CHK(hipMemcpyAsync(fm.data(), P.first_miss, ns * 8, hipMemcpyDeviceToHost, st));
         CHK(hipMemcpyAsync(tp.data(), tile_prefix, (ns + 1) * 8, hipMemcpyDeviceToHost, st));
         CHK(hipStreamSynchronize(st));
+        // The segmented repair walks up to 64 candidate chains per segment (<= 1024 segments)
+        // frame by frame, one lane each: its cost grows with the frames per segment, while the
+        // exact kernel's grows with the bytes (and is slow only on long random-payload frames).
+        // A range whose chains hold more than kSegFramesMax frames per segment (dense small
+        // frames: ~13 ms per 1.7 GB, against ~5 ms exact) goes to the exact kernel instead.
+        bool dense = false;
+        uint64_t *fsum = c->scratch.at<uint64_t>(L.segw);
+        for (uint64_t s = 0; s < ns && !dense; s++) {
+          if (fm[s] == ~0ull || tp[s + 1] - fm[s] < kSegDenseMinTiles) continue;
+          CHK(hipMemsetAsync(fsum, 0, 8, st));
+          CHK(drp_launch_range_sum(P.tile_count, fm[s], tp[s + 1], fsum, st));
+          uint64_t f = 0;
+          CHK(hipMemcpyAsync(&f, fsum, 8, hipMemcpyDeviceToHost, st));
+          CHK(hipStreamSynchronize(st));
+          const uint64_t nseg = std::min<uint64_t>(tp[s + 1] - fm[s], 1024);
+          dense = f / nseg > kSegFramesMax;
+          TRACE("decode_spec: stream %llu range %llu tiles, %llu frames on the predicted chains%s",
+                (unsigned long long)s, (unsigned long long)(tp[s + 1] - fm[s]), (unsigned long long)f,
+                dense ? ": dense, exact kernel" : "");
+        }
+        if (dense) {
+          h[1] = miss;  // (reported as a failed prediction: the caller runs the exact kernel)
+          break;
+        }
         for (uint64_t s = 0; s < ns; s++)
           if (fm[s] != ~0ull) {
             TRACE("decode_spec: segmented repair of stream %llu from tile %llu to %llu", (unsigned long long)s,
@@ -567,7 +615,8 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     CHK(hipEventRecord(c->ev[2], st));
     CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
                             scount, fr->type, co->flags, cap, res, st));
-    CHK(drp_launch_key_post(bytes, tile_prefix, ns, P.tile_base, P.tile_count, cap, fr, co, st));
+    CHK(drp_launch_key_post(bytes, tile_prefix, ns, P.tile_base, P.tile_count, cap, fr, co,
+                          c->key_post == DRP_KEY_POST_FLAGS, st));
   } else {
     CHK(hipEventRecord(c->ev[2], st));
   }
@@ -809,9 +858,15 @@ static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry 
   // the continuation's payload bytes are pass-through: only [a, n) goes to the device
   const uint64_t a = brem & ~15ull, m = n - a;
   const uint8_t *dbytes = bytes + a;
+  float h2d_ms = 0;
   if (!is_device_ptr(bytes) || ((uintptr_t)bytes & 15)) {
     if (!c->in_stage.ensure(m + 64)) return DRP_E_NOMEM;
-    if (m) CHK(hipMemcpyAsync(c->in_stage.p, bytes + a, m, hipMemcpyDefault, st));
+    const double t0 = now_ms();
+    if (m) {
+      CHK(hipMemcpyAsync(c->in_stage.p, bytes + a, m, hipMemcpyDefault, st));
+      CHK(hipStreamSynchronize(st));
+    }
+    h2d_ms = (float)(now_ms() - t0);
     dbytes = (const uint8_t *)c->in_stage.p;
   }
   const size_t stage_meta = 256;
@@ -822,24 +877,37 @@ static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry 
   uint64_t hv[3] = {0, m, brem - a};
   CHK(hipMemcpyAsync(soff, hv, 16, hipMemcpyHostToDevice, st));
   CHK(hipMemcpyAsync(ent, hv + 2, 8, hipMemcpyHostToDevice, st));
-  uint64_t cap = m / 32 + 1024;  // frames; grown below when the stream is denser
+  // frames: sized from the density of the ctx's previous batch (a stream's batches are alike),
+  // 1/32 per byte at first; grown below to the exact count when the stream is denser
+  const double dens = c->frames_per_byte > 0 ? c->frames_per_byte * 1.25 : 1.0 / 32;
+  uint64_t cap = (uint64_t)((double)m * dens) + 1024;
   drp_stream_result r;
   int rc = DRP_OK;
   for (int attempt = 0; attempt < 2; attempt++) {
     if (!c->dec_cols.ensure(carve_bytes(cap))) return DRP_E_NOMEM;
     carve(c->dec_cols, cap, S.fr, S.co);
-    if (!c->key_post) S.co.key_hash = nullptr;
+    if (c->key_post != DRP_KEY_POST_HASH) S.co.key_hash = nullptr;
     S.cap = cap;
     rc = run_decode(c, dbytes, m, soff, ent, 1, &S.fr, &S.co, cap, dres);
     if (rc != DRP_OK && rc != DRP_E_CAPACITY) return rc;
     CHK(hipMemcpyAsync(&r, dres, sizeof(r), hipMemcpyDeviceToHost, st));
     CHK(hipStreamSynchronize(st));
     if (rc == DRP_OK) break;
-    // the chain held more frames than the guess (frames past a malformed Change count too):
-    // retry at the bound, every delivered frame being at least 2 bytes
-    cap = m / 2 + 2;
+    // The chain held more frames than the guess. Rows needed: the delivered frames plus a
+    // malformed Change. When they fit, the result is complete (a malformed Change inside the
+    // capacity was seen, so nothing before it was missed; the frames after it are not
+    // delivered). Otherwise r.frames is the exact chain count or a malformed Change past the
+    // capacity ends the stream earlier: retry at that bound.
+    const uint64_t need = r.frames + ((r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0);
+    if (need <= cap) {
+      rc = DRP_OK;
+      break;
+    }
+    cap = need + 1;
   }
   if (rc != DRP_OK) return rc;
+  c->timing.h2d_ms = h2d_ms;
+  c->frames_per_byte = m ? (double)r.frames / (double)m : 0.0;
   const uint64_t bad = (r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0;
   S.shift = a;
   S.rows = S.nf0 + r.frames + bad;
@@ -872,6 +940,7 @@ static int fetch_staged(drp_ctx *c, const drp_frames *frames, const drp_changes 
   }
   const uint64_t g0 = first + dst - S.nf0;  // first GPU row
   const uint64_t ng = rows - dst;
+  const double t0 = now_ms();
   if (ng) {
     auto cp = [&](void *d, const void *s_, size_t w) {
       return hipMemcpyAsync(static_cast<char *>(d) + dst * w, static_cast<const char *>(s_) + g0 * w, ng * w,
@@ -898,6 +967,7 @@ static int fetch_staged(drp_ctx *c, const drp_frames *frames, const drp_changes 
     if (S.shift)
       for (uint64_t i = 0; i < ng; i++) frames->payload_off[dst + i] += S.shift;
   }
+  c->timing.d2h_ms = (float)(now_ms() - t0);
   return DRP_OK;
 }
 
@@ -924,7 +994,8 @@ int drp_decode_batch(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *ca
   if (is_device_ptr(frames->payload_off)) return decode_batch_device_out(c, bytes, n, carry, frames, cols, cap,
                                                                          n_frames, err_frame, err_code, err_detail);
   const int key_post = c->key_post;
-  c->key_post = cols->key_hash != nullptr;  // key hashes when the caller asks for them
+  if (cols->key_hash) c->key_post = DRP_KEY_POST_HASH;  // key hashes when the caller asks for them
+  else if (key_post == DRP_KEY_POST_HASH) c->key_post = DRP_KEY_POST_OFF;
   int rc = stage_decode(c, bytes, n, carry, n_frames, err_frame, err_code, err_detail);
   c->key_post = key_post;
   if (rc != DRP_OK) return rc;

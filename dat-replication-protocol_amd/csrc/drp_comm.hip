@@ -155,4 +155,39 @@ int drp_index_allgather_multi(drp_ctx **ctxs, drp_comm **comms, int ngpu, const 
   return DRP_OK;
 }
 
+int drp_index_allgather_host(drp_ctx **ctxs, drp_comm **comms, int ngpu, const drp_stream_stats *const *local,
+                             uint64_t per_gpu, drp_stream_stats *global, uint64_t *base) {
+  if (!ctxs || !comms || ngpu < 1 || ngpu > 64 || (per_gpu && (!local || !global || !base))) return DRP_E_INVAL;
+  if (!per_gpu) return DRP_OK;
+  const size_t lb = per_gpu * sizeof(drp_stream_stats), gb = lb * (size_t)ngpu, bb = per_gpu * (size_t)ngpu * 8;
+  void *dl[64] = {}, *dg[64] = {}, *db[64] = {};
+  int rc = DRP_OK;
+  for (int g = 0; g < ngpu && rc == DRP_OK; g++) {
+    if (!ctxs[g] || !local[g] || hipSetDevice(drp_device(ctxs[g])) != hipSuccess) {
+      rc = !ctxs[g] || !local[g] ? DRP_E_INVAL : DRP_E_HIP;
+      break;
+    }
+    if (hipMalloc(&dl[g], lb) != hipSuccess || hipMalloc(&dg[g], gb) != hipSuccess || hipMalloc(&db[g], bb) != hipSuccess)
+      rc = DRP_E_NOMEM;
+    else if (hipMemcpyAsync(dl[g], local[g], lb, hipMemcpyHostToDevice, (hipStream_t)drp_stream(ctxs[g])) != hipSuccess)
+      rc = DRP_E_HIP;
+  }
+  if (rc == DRP_OK)
+    rc = drp_index_allgather_multi(ctxs, comms, ngpu, (const drp_stream_stats *const *)dl, per_gpu,
+                                   (drp_stream_stats *const *)dg, (uint64_t *const *)db);
+  if (rc == DRP_OK && hipSetDevice(drp_device(ctxs[0])) == hipSuccess) {
+    if (hipMemcpy(global, dg[0], gb, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(base, db[0], bb, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = DRP_E_HIP;
+  }
+  for (int g = 0; g < ngpu; g++) {
+    if (!ctxs[g]) continue;
+    (void)hipSetDevice(drp_device(ctxs[g]));
+    if (dl[g]) (void)hipFree(dl[g]);
+    if (dg[g]) (void)hipFree(dg[g]);
+    if (db[g]) (void)hipFree(db[g]);
+  }
+  return rc;
+}
+
 }  // extern "C"

@@ -1361,6 +1361,10 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
 // verify_counts then takes, so results are verify_counts' in every case. Threads before k are
 // left to emit_tiles through tile_k (the records stay as kernel 1 wrote them).
 constexpr uint32_t VL_BLK = 256, VL_G = 8;
+#ifndef DRP_SP_FRAMES
+#define DRP_SP_FRAMES 8  // frames of a sparse tile (0: no sparse emission)
+#endif
+constexpr uint32_t SP_FRAMES = DRP_SP_FRAMES;
 __device__ __forceinline__ uint32_t bytes_from(uint32_t s, uint32_t d) {  // byte mask of dword d: index >= s
   return s <= 4u * d ? 0xFFFFFFFFu : (s >= 4u * d + 4u ? 0u : 0xFFFFFFFFu << (8u * (s - 4u * d)));
 }
@@ -1398,7 +1402,7 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
   const uint32_t k = inside ? (uint32_t)((et - G.A) / SEGB) : NT;
   const uint32_t kr = k / 16u, ki = k % 16u;
   const uint32_t ew[4] = {e4.x, e4.y, e4.z, e4.w}, nw[4] = {n4.x, n4.y, n4.z, n4.w}, cw[4] = {c4.x, c4.y, c4.z, c4.w};
-  uint32_t bad = 0, sf = 0, sc = 0, rsm = 0;
+  uint32_t bad = 0, sf = 0, sc = 0, rsm = 0, multi = 0;
   const uint32_t s = r > kr ? 0u : (r == kr ? ki : 16u);  // this lane's threads from k on
 #pragma unroll
   for (uint32_t d = 0; d < 4; d++) {
@@ -1406,6 +1410,7 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
     sf = __builtin_amdgcn_udot4(nw[d] & m, 0x01010101u, sf, false);
     sc = __builtin_amdgcn_udot4(cw[d] & m, 0x01010101u, sc, false);
     rsm |= restart_bytes(ew[d]) << (4u * d);
+    multi |= nw[d] & m & 0xFEFEFEFEu;  // a thread from k on with more than one frame
   }
   if (inside) {
     if (r == kr) {
@@ -1420,6 +1425,7 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
     sf += shfl_xor32(sf, d);
     sc += shfl_xor32(sc, d);
     bad |= shfl_xor32(bad, d);
+    multi |= shfl_xor32(multi, d);
   }
   const bool miss = !inside && !bogus && claim != C_ID && claim != et;
   if (r != 0) return;
@@ -1431,6 +1437,7 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
   P.tile_count[t] = sf;
   P.tile_nch[t] = sc;
   P.tile_k[t] = (uint8_t)k;
+  if (P.tile_sparse) P.tile_sparse[t] = (!multi && sf <= SP_FRAMES) ? 1 : 0;
 }
 
 #ifndef DRP_DIRTY_DEDUPE
@@ -1621,6 +1628,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     P.tile_count[t] = count_t;
     P.tile_nch[t] = nch_t;
     if (P.tile_k) P.tile_k[t] = 0;  // (this kernel rewrote the records of the threads before e_t)
+    if (P.tile_sparse) P.tile_sparse[t] = 0;  // (its records may be the slow path's: emit_tiles takes it)
   }
   }
 }
@@ -1802,6 +1810,279 @@ __device__ __forceinline__ bool emit_frame_fast(const DecodeParams &P, const Img
   return true;
 }
 
+// ---- the fast emit in 32-bit tile-relative form ----------------------------------------------
+// Every position is an offset into the tile's LDS image (< IMG), every output store is a uniform
+// column pointer at the tile's first row plus a 32-bit row index (SGPR base + VGPR offset
+// addressing), and varints of up to 4 bytes are assembled in 32 bits: the same columns as
+// emit_frame_fast, with far fewer vector instructions per frame.
+struct RowCols {
+  uint64_t *poff;
+  uint32_t *plen;
+  uint8_t *type;
+  uint32_t *ko, *kl, *so, *sl, *vo, *vl;
+  uint64_t *ch, *fr, *to;
+  uint8_t *fl;
+  uint32_t lim;  // rows the tile may write (the capacity left)
+};
+__device__ __forceinline__ RowCols row_cols(const DecodeParams &P, uint64_t base) {
+  RowCols r;
+  r.poff = P.payload_off + base;
+  r.plen = P.payload_len + base;
+  r.type = P.type + base;
+  r.ko = P.key_off + base;
+  r.kl = P.key_len + base;
+  r.so = P.subset_off + base;
+  r.sl = P.subset_len + base;
+  r.vo = P.value_off + base;
+  r.vl = P.value_len + base;
+  r.ch = P.change + base;
+  r.fr = P.from + base;
+  r.to = P.to + base;
+  r.fl = P.flags + base;
+  r.lim = base >= P.cap ? 0u : (uint32_t)umin64(P.cap - base, 0xFFFFFFFFull);
+  return r;
+}
+
+// bytes o..o+3 and o+4..o+7 of the LDS image
+__device__ __forceinline__ void lds8(const uint8_t *lds, uint32_t o, uint32_t &w, uint32_t &wn) {
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(lds) + (o >> 2);
+  const uint32_t sh = (o & 3u) * 8u, a0 = q[0], a1 = q[1], a2 = q[2];
+  w = __builtin_amdgcn_alignbit(a1, a0, sh);
+  wn = __builtin_amdgcn_alignbit(a2, a1, sh);
+}
+
+// decode_change_fast over the LDS image: payload at image offset po, pl bytes, bytes [0, lim) of
+// the image valid. true with decode_change's columns; false for any other shape (or a field that
+// leaves the image): the tile then goes to the general kernel, as with decode_change_fast.
+__device__ __forceinline__ bool change_fast32(const uint8_t *lds, uint32_t po, uint32_t pl, uint32_t lim,
+                                              ChangeCols &c) {
+  c.key_off = c.key_len = c.subset_off = c.subset_len = c.value_off = c.value_len = 0;
+  c.change = c.from = c.to = 0;
+  c.flags = 0;
+  c.err = 0;
+  uint32_t found = 0, off = 0;
+  while (off < pl) {
+    const uint32_t q = po + off;
+    if (pl - off < 2u || q + 2u > lim) return false;
+    uint32_t w, wn;
+    lds8(lds, q, w, wn);
+    const uint32_t b0 = w & 0xFFu, tag = b0 >> 3;
+    if (b0 >= 0x80u || tag - 1u > 5u) return false;
+    const uint32_t x = __builtin_amdgcn_alignbit(wn, w, 8);  // bytes 1..4
+    const uint32_t tm = ~x & 0x80808080u;
+    uint32_t k2;
+    uint64_t v;
+    const uint32_t v28 = (x & 0x7Fu) | ((x >> 1) & 0x3F80u) | ((x >> 2) & 0x1FC000u) | ((x >> 3) & 0xFE00000u);
+    if (tm) {
+      k2 = ((uint32_t)__builtin_ctz(tm) >> 3) + 1u;
+      v = v28 & ((1u << (7u * k2)) - 1u);  // (k2 = 4: 2^28 - 1, no overflow)
+    } else {  // a 5-byte varint: byte 5 must end it
+      const uint32_t b5 = (wn >> 8) & 0xFFu;
+      if (b5 & 0x80u) return false;
+      k2 = 5u;
+      v = (uint64_t)v28 | ((uint64_t)b5 << 28);
+    }
+    if (k2 > pl - off - 1u || q + 1u + k2 > lim) return false;
+    if (tag - 3u <= 2u) {
+      if (tag == 3u) {
+        c.change = v;
+        found |= 2;
+      } else if (tag == 4u) {
+        c.from = v;
+        found |= 4;
+      } else {
+        c.to = v;
+        found |= 8;
+      }
+      off += 1u + k2;
+    } else {
+      const uint32_t o2 = off + 1u + k2;
+      if (v > (uint64_t)(pl - o2)) return false;
+      const uint32_t v32 = (uint32_t)v;
+      if (tag == 1u) {
+        c.subset_off = o2;
+        c.subset_len = v32;
+        c.flags |= DRP_F_SUBSET;
+      } else if (tag == 2u) {
+        c.key_off = o2;
+        c.key_len = v32;
+        found |= 1;
+      } else {
+        c.value_off = o2;
+        c.value_len = v32;
+        c.flags |= DRP_F_VALUE;
+      }
+      off = o2 + v32;
+    }
+  }
+  if (found != 15) {
+    c.err = DRP_ERR_REQUIRED;
+    c.flags |= DRP_F_BAD;
+  }
+  return true;
+}
+
+// The delivered frame at image offset o, row i of the tile: false when its header or payload is
+// not in the fast shapes (the tile goes to the general kernel). Headers of 1..3-byte varints
+// whose 16 bytes lie inside the image and the stream (se_rel) are parsed here; others take the
+// 64-bit path (emit_frame_fast).
+__device__ __forceinline__ bool emit_frame32(const DecodeParams &P, const Img &m, const RowCols &C, uint32_t o,
+                                             uint32_t i, uint32_t se_rel, uint64_t base, uint64_t &badf) {
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(m.lds) + (o >> 2);
+  const uint32_t w = __builtin_amdgcn_alignbit(q[1], q[0], (o & 3u) * 8u);
+  const uint32_t tm = ~w & 0x808080u;
+  if (!tm || o + 16u > IMG || o + 16u > se_rel) return emit_frame_fast(P, m, m.A + o, base + i, badf);
+  if (i >= C.lim) return true;
+  const uint32_t k = ((uint32_t)__builtin_ctz(tm) >> 3) + 1u;
+  const uint32_t L = ((w & 0x7Fu) | ((w >> 1) & 0x3F80u) | ((w >> 2) & 0x1FC000u)) & ((1u << (7u * k)) - 1u);
+  const uint32_t id = (w >> (8u * k)) & 0xFFu;
+  const uint32_t po = o + k + 1u, pl = L - 1u;
+  const bool partial = id == 2u && L > se_rel - o - k;  // a blob cut by the stream end (H_TAIL_BLOB)
+  C.poff[i] = m.A + po;
+  C.plen[i] = pl;
+  C.type[i] = (uint8_t)(id | (partial ? DRP_FRAME_PARTIAL : 0u));
+  if (id != 1u) return true;
+  ChangeCols c;
+  if (!change_fast32(m.lds, po, pl, se_rel < IMG ? se_rel : IMG, c)) return false;
+  C.ko[i] = c.key_off;
+  C.kl[i] = c.key_len;
+  C.so[i] = c.subset_off;
+  C.sl[i] = c.subset_len;
+  C.vo[i] = c.value_off;
+  C.vl[i] = c.value_len;
+  C.ch[i] = c.change;
+  C.fr[i] = c.from;
+  C.to[i] = c.to;
+  uint32_t fl = c.flags;
+  if (c.err == DRP_ERR_REQUIRED) fl |= DRP_F_MISSING;
+  C.fl[i] = (uint8_t)fl;
+  if (c.err) badf = base + i < badf ? base + i : badf;
+  return true;
+}
+
+// ---- sparse tiles: frames decoded from HBM, no staging ---------------------------------------
+// A tile whose threads from tile_k on each deliver at most one frame (at the thread's entry, from
+// verification's records) and at most SP_FRAMES in all (long frames: C5's 4 KB Changes, blob
+// payloads) needs no walk and no LDS image: its frame starts are the entries themselves. Eight
+// lanes read a tile's records (16 threads each), the frames go to an LDS list, and every thread
+// then decodes one frame through 16-byte windows of the batch (header, then the Change field
+// headers: string and bytes contents are skipped, so a 4 KB value costs nothing). The columns
+// are decode_change's. A frame whose entry is not a delivered header (an id-0 header before it)
+// clears the tile's mark and emit_tiles takes the whole tile as before.
+struct GlobalWinReader {
+  static constexpr bool kFast = true;
+  const uint8_t *g;
+  uint64_t lim;  // the stream end
+  __device__ __forceinline__ bool ok(uint64_t p, uint64_t n) const { return p + n <= lim; }
+  __device__ __forceinline__ void win(uint64_t p, uint64_t &w0, uint64_t &w1) const {
+    const uint64_t a = p & ~15ull;
+    const uint4 u = ld16(g, a, lim), v = ld16(g, a + 16, lim);
+    const uint64_t q0 = ((uint64_t)u.y << 32) | u.x, q1 = ((uint64_t)u.w << 32) | u.z;
+    const uint64_t q2 = ((uint64_t)v.y << 32) | v.x, q3 = ((uint64_t)v.w << 32) | v.z;
+    const uint32_t o = (uint32_t)(p & 15);
+    if (o < 8) {
+      w0 = funnel(q0, q1, 8 * o);
+      w1 = funnel(q1, q2, 8 * o);
+    } else {
+      w0 = funnel(q1, q2, 8 * (o - 8));
+      w1 = funnel(q2, q3, 8 * (o - 8));
+    }
+  }
+  __device__ __forceinline__ void win8(uint64_t p, uint32_t &w, uint32_t &wn) const {
+    uint64_t w0, w1;
+    win(p, w0, w1);
+    w = (uint32_t)w0;
+    wn = (uint32_t)(w0 >> 32);
+  }
+};
+
+constexpr uint32_t SP_TPB = 64;  // tiles per workgroup
+__global__ __launch_bounds__(256) void emit_sparse(DecodeParams P) {
+  __shared__ uint32_t lst[SP_TPB * SP_FRAMES];  // tile (in the workgroup) << 16 | thread << 8 | rank
+  __shared__ uint32_t nl;
+  __shared__ uint32_t fail[SP_TPB];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * SP_TPB;
+  const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  if (tid == 0) nl = 0;
+  if (tid < SP_TPB) fail[tid] = 0;
+  __syncthreads();
+  // records: 8 lanes per tile (16 threads each), 32 tiles per pass
+  for (uint32_t pass = 0; pass < SP_TPB / 32; pass++) {
+    const uint32_t j = pass * 32u + tid / VL_G, r = tid % VL_G;
+    const uint64_t t = t0 + j;
+    const bool sp = t < ntiles && P.tile_sparse[t];
+    uint32_t fm = 0;  // this lane's threads that deliver a frame at their entry
+    if (sp) {
+      const uint32_t k0 = P.tile_k[t];
+      const uint4 e4 = *reinterpret_cast<const uint4 *>(P.ent + t * NT + 16u * r);
+      const uint4 n4 = *reinterpret_cast<const uint4 *>(P.ent_n + t * NT + 16u * r);
+      const uint32_t ew[4] = {e4.x, e4.y, e4.z, e4.w}, nw[4] = {n4.x, n4.y, n4.z, n4.w};
+#pragma unroll
+      for (uint32_t b = 0; b < 16; b++) {
+        const uint32_t e = (ew[b >> 2] >> (8u * (b & 3u))) & 0xFFu, n = (nw[b >> 2] >> (8u * (b & 3u))) & 0xFFu;
+        if (16u * r + b >= k0 && e < 0x80u && n == 1u) fm |= 1u << b;
+      }
+    }
+    const uint32_t c = (uint32_t)__builtin_popcount(fm);
+    uint32_t pre = c;  // inclusive prefix over the tile's 8 lanes
+#pragma unroll
+    for (uint32_t d = 1; d < VL_G; d <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)pre, d, VL_G);
+      if (r >= d) pre += y;
+    }
+    uint32_t rank = pre - c;
+    if (c) {
+      uint32_t q = atomicAdd(&nl, c);
+      for (uint32_t bits = fm; bits; bits &= bits - 1, q++, rank++)
+        if (q < SP_TPB * SP_FRAMES) lst[q] = (j << 16) | ((16u * r + (uint32_t)__builtin_ctz(bits)) << 8) | rank;
+    }
+  }
+  __syncthreads();
+  const uint32_t n = min(nl, SP_TPB * SP_FRAMES);  // (<= SP_FRAMES per tile: never cut)
+  for (uint32_t i = tid; i < n; i += 256) {
+    const uint32_t e = lst[i], j = e >> 16, th = (e >> 8) & 0xFFu, rank = e & 0xFFu;
+    const uint64_t t = t0 + j;
+    const TileGeo G = tile_geo(P, t);
+    const uint64_t p = G.A + (uint64_t)th * SEGB + (P.ent[t * NT + th] & 63u);
+    const GlobalWinReader rd{P.bytes, G.se};
+    uint64_t w0, w1;
+    rd.win(p, w0, w1);
+    const Hdr h = parse_win(w0, w1, p, G.se);
+    if (!((h.kind == H_VALID && h.id != 0) || h.kind == H_TAIL_BLOB)) {
+      fail[j] = 1;  // (an id-0 header at the entry: the delivered frame is further on)
+      continue;
+    }
+    const uint64_t f = P.tile_base[t] + rank;
+    if (f >= P.cap) continue;
+    const uint64_t po = p + h.vlen + 1, pl = h.L - 1;
+    P.payload_off[f] = po;
+    P.payload_len[f] = pl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pl;
+    P.type[f] = (uint8_t)(h.id | (h.kind == H_TAIL_BLOB ? DRP_FRAME_PARTIAL : 0u));
+    if (h.id != 1) continue;
+    const ChangeCols cc = decode_change(rd, po, pl);
+    P.key_off[f] = cc.key_off;
+    P.key_len[f] = cc.key_len;
+    P.subset_off[f] = cc.subset_off;
+    P.subset_len[f] = cc.subset_len;
+    P.value_off[f] = cc.value_off;
+    P.value_len[f] = cc.value_len;
+    P.change[f] = cc.change;
+    P.from[f] = cc.from;
+    P.to[f] = cc.to;
+    uint32_t fl = cc.flags;
+    if (cc.err == DRP_ERR_REQUIRED) fl |= DRP_F_MISSING;
+    P.flags[f] = (uint8_t)fl;
+    if (cc.err) atomicMin((unsigned long long *)&P.payload_err[G.s], (unsigned long long)f);
+  }
+  __syncthreads();
+  if (tid < SP_TPB && fail[tid]) P.tile_sparse[t0 + tid] = 0;
+}
+
+#ifndef DRP_EMIT32
+#define DRP_EMIT32 1  // 0: the 64-bit fast emit (A/B)
+#endif
+
 #ifndef DRP_EMIT_FAST_WAVES
 #define DRP_EMIT_FAST_WAVES 6  // the fast emit kernel holds no general Change decoder: 6 waves/SIMD, no spills
 #endif
@@ -1834,6 +2115,7 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
   if (!FAST) bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
   if (t >= ntiles) continue;  // (whole workgroup)
+  if (FAST && P.tile_sparse && P.tile_sparse[t]) continue;  // emit_sparse wrote it
   const uint64_t se = G.se, A = G.A;
   // the records load with the tile bytes, not after them
   const uint64_t base = ldc(P.tile_base + t);
@@ -1884,7 +2166,13 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
     bsync();
     if constexpr (FAST) {
       bool ok = true;
-      for (uint32_t i = tid; i < count_t; i += NT) ok &= emit_frame_fast(P, m, A + lst[i], base + i, badf);
+      if (DRP_EMIT32) {
+        const RowCols C = row_cols(P, base);
+        const uint32_t se_rel = (uint32_t)umin64(se - A, 0x7FFFFFFFull);
+        for (uint32_t i = tid; i < count_t; i += NT) ok &= emit_frame32(P, m, C, lst[i], i, se_rel, base, badf);
+      } else {
+        for (uint32_t i = tid; i < count_t; i += NT) ok &= emit_frame_fast(P, m, A + lst[i], base + i, badf);
+      }
       if (!ok) defer = 1;
       bsync();
       if (defer) {  // the general kernel re-emits the whole tile (its payload errors too)
@@ -1924,6 +2212,7 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
 constexpr uint32_t SEG_CAND = 64, SEG_GMAX = 1024;
 struct SegRange {
   uint64_t s, t0, tl, G, nseg;  // stream, tiles [t0, tl), tiles per segment, segments
+  uint64_t tend;                // the stream's tile end (tl < tend: the range was clamped)
   uint64_t *cand;               // per segment: 64 starts, then 64 exits
   uint64_t *seg_entry;          // [nseg + 1] exact entry of each segment (and the final exit)
 };
@@ -1960,8 +2249,8 @@ __device__ __forceinline__ uint64_t seg_tile_a(const TileGeo &G, uint64_t u) {
 }
 // the segment's end: the next segment's first tile, or the stream end
 __device__ __forceinline__ uint64_t seg_end(const TileGeo &G, const SegRange &R, uint64_t seg) {
-  const uint64_t tb = R.t0 + (seg + 1) * R.G;
-  return tb >= R.tl ? G.se : seg_tile_a(G, tb);
+  const uint64_t tb = umin64(R.t0 + (seg + 1) * R.G, R.tl);
+  return tb >= R.tend ? G.se : seg_tile_a(G, tb);
 }
 // chain step inside the staged tile: advance p while it starts a frame before lim (the tile end,
 // or the segment end); a header that ends the chain returns MARK_TERM (| M_ERR) | p
@@ -2102,6 +2391,14 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
   for (uint64_t i = tid; i < tb - ta; i += NT) P.claim[ta + i] = lcl[i];
 }
 
+// sum of a per-tile column over a tile range (the segmented repair's cost estimate)
+__global__ __launch_bounds__(256) void range_sum_kernel(const uint64_t *v, uint64_t t0, uint64_t t1, uint64_t *out) {
+  uint64_t acc = 0;
+  for (uint64_t t = t0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; t < t1; t += (uint64_t)gridDim.x * 256) acc += v[t];
+  acc = wave_sum64(acc);
+  if ((threadIdx.x & 63u) == 0 && acc) atomicAdd((unsigned long long *)out, (unsigned long long)acc);
+}
+
 // per-stream change / blob counts (one thread per stream)
 __global__ void stream_counts_kernel(const uint64_t *tile_prefix, uint64_t nstreams, const uint64_t *count,
                                      const uint64_t *base, const uint64_t *nch, const uint64_t *nch_base,
@@ -2238,6 +2535,12 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
   if (DRP_EMIT_SPLIT && Q.vlist) {  // the fast kernel, then the general one on the tiles it lists
     e = hipMemsetAsync(Q.vlist_n, 0, 4, st);
     if (e != hipSuccess) return e;
+    if (spec::SP_FRAMES && Q.tile_sparse) {  // sparse tiles first (no staging), then every other tile
+      hipLaunchKernelGGL(spec::emit_sparse, dim3((uint32_t)((nt_max + spec::SP_TPB - 1) / spec::SP_TPB)), dim3(256),
+                         0, st, Q);
+    } else {
+      Q.tile_sparse = nullptr;
+    }
     hipLaunchKernelGGL(spec::emit_tiles<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
     hipLaunchKernelGGL(spec::emit_tiles<false>, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0,
                        st, Q);
@@ -2251,6 +2554,14 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
                                   Q.scount, st);
 }
 
+extern "C" hipError_t drp_launch_range_sum(const uint64_t *v, uint64_t t0, uint64_t t1, uint64_t *out,
+                                           hipStream_t st) {
+  if (t1 <= t0) return hipSuccess;
+  const uint64_t nb = (t1 - t0 + 255) / 256;
+  hipLaunchKernelGGL(spec::range_sum_kernel, dim3((uint32_t)(nb < 1024 ? nb : 1024)), dim3(256), 0, st, v, t0, t1, out);
+  return hipGetLastError();
+}
+
 // Segmented repair of stream s from tile t0 (its first missed tile) to its end (the caller then
 // runs a verify pass). scratch: 2 * 64 * 1024 + 1025 words.
 extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, uint64_t t0, uint64_t tl,
@@ -2259,10 +2570,12 @@ extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, u
   spec::SegRange R;
   R.s = s;
   R.t0 = t0;
-  R.tl = tl;
-  const uint64_t n = tl - t0;
+  R.tend = tl;
+  // at most 1024 segments of SEG_GMAX tiles (8 GiB of 8 KiB tiles): a longer range is repaired up
+  // to there; the verify passes that follow prove the claims past it as before (or fall back)
+  const uint64_t n = tl - t0 < 1024ull * spec::SEG_GMAX ? tl - t0 : 1024ull * spec::SEG_GMAX;
+  R.tl = t0 + n;
   R.G = (n + 1023) / 1024;
-  if (R.G > spec::SEG_GMAX) return hipErrorInvalidValue;
   R.nseg = (n + R.G - 1) / R.G;
   R.cand = scratch;
   R.seg_entry = scratch + 2 * spec::SEG_CAND * 1024;

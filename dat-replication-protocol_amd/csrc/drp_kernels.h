@@ -56,6 +56,10 @@ struct DecodeParams {
   // the threads before it); null: verify_counts verifies every tile
   uint32_t *vlist, *vlist_n;
   uint8_t *tile_k;
+  // per tile: 1 when the tile is sparse (every thread from tile_k on delivers at most one frame,
+  // at its entry; a few frames in all): emit_sparse decodes its frames from HBM without staging
+  // the tile, and emit_tiles skips it (emit_sparse clears the mark of a tile it cannot take)
+  uint8_t *tile_sparse;
   uint64_t *first_miss;  // per stream: the first tile a verify pass repaired (~0: none)
   // verify_counts appends the tiles whose entry a repair changed (the next repair pass verifies
   // only those); a count past dlist_cap or a nonzero dlist_n[2] means the next pass must be a
@@ -94,6 +98,10 @@ uint32_t drp_spec_retry_mask(void);
 uint32_t drp_spec_miss_bit(void);
 hipError_t drp_launch_spec_head(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                 uint32_t *tile_stream, hipStream_t st);
+// out[0] += sum of v[t0, t1) (out zeroed by the caller)
+hipError_t drp_launch_range_sum(const uint64_t *v, uint64_t t0, uint64_t t1, uint64_t *out, hipStream_t st);
+// emit_sparse over every tile (before emit_tiles): the tiles verification marked sparse
+hipError_t drp_launch_emit_sparse(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t st);
 hipError_t drp_launch_seg_repair(const drp::DecodeParams *P, uint64_t s, uint64_t t0, uint64_t tl, uint64_t *scratch,
                                  hipStream_t st);
 hipError_t drp_launch_spec_verify(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
@@ -119,7 +127,7 @@ hipError_t drp_launch_encode(const drp::EncodeParams *P, hipStream_t st);
 // key hash + key flags for every change frame written (no-op when co->key_hash is NULL)
 hipError_t drp_launch_key_post(const uint8_t *bytes, const uint64_t *tile_prefix, uint64_t nstreams,
                                const uint64_t *tile_base, const uint64_t *tile_count, uint64_t cap,
-                               const drp_frames *fr, const drp_changes *co, hipStream_t st);
+                               const drp_frames *fr, const drp_changes *co, int flags_only, hipStream_t st);
 hipError_t drp_launch_index_scan(const drp_stream_stats *stats, uint64_t count, uint64_t *base,
                                  hipStream_t st);
 hipError_t drp_launch_stats_from_results(const drp_stream_result *res, const uint64_t *stream_off,

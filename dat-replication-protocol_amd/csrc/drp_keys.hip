@@ -6,7 +6,7 @@
 // a consumer that only needs key bytes or a hash (dat storage) skips that, and the JS layer
 // takes the cheaper latin1 path for ASCII keys (same string).
 //
-// One thread per frame, grid-stride; runs after emission over the frames the decode wrote
+// The hash column is optional (DRP_KEY_POST_FLAGS: flags only). One thread per frame, grid-stride; runs after emission over the frames the decode wrote
 // (their count is the last tile's base + count), reading the key bytes from the batch in HBM.
 #include "drp_device.h"
 #include "drp_kernels.h"
@@ -128,12 +128,12 @@ __global__ __launch_bounds__(256) void key_post_kernel(const uint8_t *bytes, con
     if ((type[f] & 0x3Fu) != DRP_TYPE_CHANGE) continue;
     const uint32_t fl = flags[f];
     if (fl & DRP_F_BAD) {
-      key_hash[f] = 0;
+      if (key_hash) key_hash[f] = 0;
       continue;
     }
     const uint8_t *k = bytes + payload_off[f] + key_off[f];
     const uint32_t n = key_len[f];
-    key_hash[f] = xxh64(k, n);
+    if (key_hash) key_hash[f] = xxh64(k, n);
     flags[f] = (uint8_t)(fl | key_class(k, n));
   }
 }
@@ -143,8 +143,10 @@ __global__ __launch_bounds__(256) void key_post_kernel(const uint8_t *bytes, con
 
 extern "C" hipError_t drp_launch_key_post(const uint8_t *bytes, const uint64_t *tile_prefix, uint64_t nstreams,
                                           const uint64_t *tile_base, const uint64_t *tile_count, uint64_t cap,
-                                          const drp_frames *fr, const drp_changes *co, hipStream_t st) {
-  if (!co->key_hash || cap == 0) return hipSuccess;
+                                          const drp_frames *fr, const drp_changes *co, int flags_only,
+                                          hipStream_t st) {
+  // the hash when the caller gave a column for it; the key flags also without one (flags_only)
+  if ((!co->key_hash && !flags_only) || cap == 0) return hipSuccess;
   uint64_t blocks = (cap + 255) / 256;
   if (blocks > 65536) blocks = 65536;  // grid-stride beyond
   hipLaunchKernelGGL(drp::keys::key_post_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, bytes, tile_prefix,

@@ -22,6 +22,9 @@
  *                                                   of each key) and the key flags 0x10 / 0x20
  *   decodeSync(ctx, buf, blobRemaining[, keyPost]) -> the same object (blocks the JS thread)
  *   encode(ctx, heap, n, 10 column arrays, cb)   -> cb(err, Buffer of wire bytes)
+ *   deviceCount()                                -> HIP devices visible to the process
+ *   indexAllgather(ctxs[], stats[])              -> {table, base}: the global frame index of
+ *                                                   streams sharded over this process's devices
  *
  * Host columns are sized from the decoded frame count (drp_decode_stage, then
  * drp_decode_fetch), and handed to JS as external ArrayBuffers (no second copy).
@@ -32,6 +35,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/drp.h"
 
@@ -117,8 +121,9 @@ typedef struct {
   uint32_t ec, ed;
   drp_carry carry;
   void *col[NCOL];
-  int key_post;   /* also the key hash column + key flags (drp_set_key_post) */
+  int key_post;   /* also the key hash column (drp_set_key_post; the key flags are always on) */
   void *khash;
+  double t_h2d, t_gpu, t_d2h, t_convert; /* ms: batch to HBM, decode kernels, columns back, u64 -> Number */
 } dec_job;
 
 static void free_cols(dec_job *j) {
@@ -131,9 +136,17 @@ static void free_cols(dec_job *j) {
 }
 
 /* the GPU part: decode, size the host columns from the frame count, fetch (worker thread) */
+static double now_ms(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+
 static void dec_run(dec_job *j) {
   pthread_mutex_lock(&j->box->mu);
-  drp_set_key_post(j->box->c, j->key_post);
+  /* the key flags always (the JS layer cuts ASCII keys from one latin1 string of the batch),
+     the key hash column when asked */
+  drp_set_key_post(j->box->c, j->key_post ? DRP_KEY_POST_HASH : DRP_KEY_POST_FLAGS);
   j->rc = drp_decode_stage(j->box->c, j->bytes, j->n, &j->carry, &j->nf, &j->ef, &j->ec, &j->ed);
   if (j->rc == DRP_OK) {
     /* rows to expose: delivered frames plus a malformed Change (its flags say why) */
@@ -150,18 +163,26 @@ static void dec_run(dec_job *j) {
       j->rc = drp_decode_fetch(j->box->c, &fr, &co, 0, j->rows);
     }
   }
+  drp_timing tm;
+  if (drp_last_timing(j->box->c, &tm) == DRP_OK) {
+    j->t_h2d = tm.h2d_ms;
+    j->t_gpu = tm.total_ms;
+    j->t_d2h = tm.d2h_ms;
+  }
   pthread_mutex_unlock(&j->box->mu);
   if (j->rc != DRP_OK) {
     free_cols(j);
     return;
   }
   /* u64 -> JS Number, in place (varint.decode yields Numbers) */
+  const double t0 = now_ms();
   const int conv[] = {C_OFF, C_CH, C_FR, C_TO};
   for (size_t k = 0; k < sizeof conv / sizeof conv[0]; k++) {
     uint64_t *u = (uint64_t *)j->col[conv[k]];
     double *d = (double *)j->col[conv[k]];
     for (uint64_t r = 0; r < j->rows; r++) d[r] = (double)u[r];
   }
+  j->t_convert = now_ms() - t0;
 }
 
 static void free_finalizer(napi_env env, void *data, void *hint) {
@@ -188,6 +209,16 @@ static napi_value dec_result(napi_env env, dec_job *j) {
   set_num(env, res, "tailKind", j->carry.tail_kind);
   set_num(env, res, "blobRemaining", (double)j->carry.blob_remaining);
   set_num(env, res, "frameBytes", (double)j->carry.frame_bytes);
+  napi_value yes, t;
+  napi_get_boolean(env, true, &yes);
+  napi_set_named_property(env, res, "asciiKeys", yes); /* flags carry DRP_F_KEY_ASCII */
+  if (napi_create_object(env, &t) == napi_ok) {
+    set_num(env, t, "h2d", j->t_h2d);
+    set_num(env, t, "gpu", j->t_gpu);
+    set_num(env, t, "d2h", j->t_d2h);
+    set_num(env, t, "convert", j->t_convert);
+    napi_set_named_property(env, res, "t", t);
+  }
   for (int i = 0; i < NCOL; i++) {
     napi_value ab, ta;
     if (napi_create_external_arraybuffer(env, j->col[i], j->rows * COL_W[i] + 8, free_finalizer, NULL, &ab) !=
@@ -412,12 +443,119 @@ static napi_value js_encode(napi_env env, napi_callback_info info) {
   return NULL;
 }
 
+/* ---- devices and the multi-GPU global index ---------------------------------------------- */
+
+static napi_value js_device_count(napi_env env, napi_callback_info info) {
+  (void)info;
+  int n = 0;
+  drp_device_count(&n);
+  napi_value v;
+  NAPI_CALL(env, napi_create_int32(env, n, &v));
+  return v;
+}
+
+/* indexAllgather(ctxs: [ctx per device], stats: [Float64Array(perGpu * 4) per device])
+ *   -> {table: Float64Array(ngpu * perGpu * 4), base: Float64Array(ngpu * perGpu)}
+ * The per-stream (frames, changes, blobs, wireBytes) records of every device, all-gathered over
+ * RCCL (drp_comm_init_all + drp_index_allgather_host: one communicator per device of this
+ * process) and scanned into the global index of each stream's first frame. Synchronous. */
+static napi_value js_index_allgather(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  uint32_t ng = 0, ns = 0;
+  bool a0 = false, a1 = false;
+  if (argc < 2 || napi_is_array(env, argv[0], &a0) != napi_ok || napi_is_array(env, argv[1], &a1) != napi_ok || !a0 ||
+      !a1 || napi_get_array_length(env, argv[0], &ng) != napi_ok || napi_get_array_length(env, argv[1], &ns) != napi_ok ||
+      ng < 1 || ng > 64 || ns != ng) {
+    napi_throw_type_error(env, NULL, "indexAllgather(ctxs[], stats[]): one ctx and one Float64Array per device");
+    return NULL;
+  }
+  drp_ctx *ctxs[64];
+  drp_comm *comms[64] = {0};
+  drp_stream_stats *local[64] = {0};
+  size_t per = 0;
+  int rc = DRP_OK;
+  for (uint32_t g = 0; g < ng && rc == DRP_OK; g++) {
+    napi_value e, st;
+    ctx_box *b = NULL;
+    napi_typedarray_type ty;
+    size_t len = 0, boff = 0;
+    void *data = NULL;
+    napi_value ab;
+    if (napi_get_element(env, argv[0], g, &e) != napi_ok || napi_get_value_external(env, e, (void **)&b) != napi_ok ||
+        napi_get_element(env, argv[1], g, &st) != napi_ok ||
+        napi_get_typedarray_info(env, st, &ty, &len, &data, &ab, &boff) != napi_ok || ty != napi_float64_array ||
+        len % 4 || (g && len / 4 != per)) {
+      rc = DRP_E_INVAL;
+      break;
+    }
+    per = len / 4;
+    ctxs[g] = b->c;
+    local[g] = (drp_stream_stats *)malloc(per * sizeof(drp_stream_stats) + 8);
+    if (!local[g]) {
+      rc = DRP_E_NOMEM;
+      break;
+    }
+    const double *d = (const double *)data;
+    for (size_t i = 0; i < per; i++) {
+      local[g][i].frames = (uint64_t)d[4 * i];
+      local[g][i].changes = (uint64_t)d[4 * i + 1];
+      local[g][i].blobs = (uint64_t)d[4 * i + 2];
+      local[g][i].wire_bytes = (uint64_t)d[4 * i + 3];
+    }
+  }
+  drp_stream_stats *global = NULL;
+  uint64_t *base = NULL;
+  if (rc == DRP_OK) {
+    global = (drp_stream_stats *)malloc(ng * per * sizeof(drp_stream_stats) + 8);
+    base = (uint64_t *)malloc(ng * per * 8 + 8);
+    if (!global || !base) rc = DRP_E_NOMEM;
+  }
+  if (rc == DRP_OK) rc = drp_comm_init_all(ctxs, (int)ng, comms);
+  if (rc == DRP_OK)
+    rc = drp_index_allgather_host(ctxs, comms, (int)ng, (const drp_stream_stats *const *)local, per, global, base);
+  for (uint32_t g = 0; g < ng; g++) {
+    drp_comm_destroy(comms[g]);
+    free(local[g]);
+  }
+  napi_value out = NULL;
+  if (rc == DRP_OK) {
+    napi_value tab_ab, base_ab, tab, bs;
+    double *td = NULL, *bd = NULL;
+    if (napi_create_object(env, &out) != napi_ok ||
+        napi_create_arraybuffer(env, ng * per * 32, (void **)&td, &tab_ab) != napi_ok ||
+        napi_create_arraybuffer(env, ng * per * 8, (void **)&bd, &base_ab) != napi_ok ||
+        napi_create_typedarray(env, napi_float64_array, ng * per * 4, tab_ab, 0, &tab) != napi_ok ||
+        napi_create_typedarray(env, napi_float64_array, ng * per, base_ab, 0, &bs) != napi_ok) {
+      out = NULL;
+      rc = DRP_E_NOMEM;
+    } else {
+      for (size_t i = 0; i < ng * per; i++) {
+        td[4 * i] = (double)global[i].frames;
+        td[4 * i + 1] = (double)global[i].changes;
+        td[4 * i + 2] = (double)global[i].blobs;
+        td[4 * i + 3] = (double)global[i].wire_bytes;
+        bd[i] = (double)base[i];
+      }
+      napi_set_named_property(env, out, "table", tab);
+      napi_set_named_property(env, out, "base", bs);
+    }
+  }
+  free(global);
+  free(base);
+  if (rc != DRP_OK) return throw_rc(env, "indexAllgather", rc);
+  return out;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"open", NULL, js_open, NULL, NULL, NULL, napi_enumerable, NULL},
       {"decode", NULL, js_decode, NULL, NULL, NULL, napi_enumerable, NULL},
       {"decodeSync", NULL, js_decode_sync, NULL, NULL, NULL, napi_enumerable, NULL},
       {"encode", NULL, js_encode, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"indexAllgather", NULL, js_index_allgather, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   napi_value v;

@@ -24,6 +24,10 @@ var FLUSH = Buffer.from([0]) // identity-compared end sentinel (decode.js:6, :12
 var MAX_BATCH = Number(process.env.DRP_MAX_BATCH) || 64 * 1024 * 1024
 var MAX_FRAME = require('buffer').constants.MAX_LENGTH
 
+// a batch whose frames average at most TEXT_PER_FRAME bytes is turned into one latin1 string
+// for its ASCII keys (cheaper than a string per key); larger frames keep one string per key
+var TEXT_PER_FRAME = 512
+var TEXT_MAX = 256 * 1024 * 1024 // (below V8's string length limit)
 var TYPE_MASK = 0x3f
 var CONT = 0x40
 var PARTIAL = 0x80
@@ -80,8 +84,9 @@ var ERRORS = {
 
 // opts (not in the reference, whose constructor takes none):
 //   keyHash: true  - every change object also carries keyHash, the XXH64 of its key bytes as
-//                    a BigInt, computed on the GPU (drp_keys.hip); ASCII keys then become
-//                    strings through the latin1 decoder (the same string, without UTF-8 work)
+//                    a BigInt, computed on the GPU (drp_keys.hip)
+//   device: k      - the GPU this stream decodes on (default: DRP_DEVICE or 0); independent
+//                    streams are spread over a node's GPUs this way (index.js: shard)
 function Decoder (opts) {
   if (!(this instanceof Decoder)) return new Decoder(opts)
   stream.Writable.call(this)
@@ -99,12 +104,14 @@ function Decoder (opts) {
   this._onblob = drainBlob
   this._onfinalize = noopFinalize
 
-  this._ctx = native.context()
+  this._ctx = native.context(opts && opts.device)
   this._queue = []        // written chunks not yet handed to the GPU
   this._queued = 0
   this._scheduled = false
-  this._busy = false      // a batch is being decoded or replayed
-  this._held = null       // write callback held back until its batch is delivered
+  this._inflight = false  // a batch is on the GPU (worker thread)
+  this._ready = null      // a decoded batch waiting for the one being replayed
+  this._halt = false      // a batch ended in an error: nothing after it is decoded
+  this._held = null       // write callback held back until its batch is on the GPU
   this._final = null      // end(): finalize once everything before it is delivered
   this._carry = null      // an incomplete frame header (<= 10 bytes)
   this._partial = null    // an incomplete Change frame of known size: {buf, filled}
@@ -112,8 +119,10 @@ function Decoder (opts) {
   this._blob = null       // the open BlobStream
   this._res = null        // decoded batch being replayed
   this._buf = null        // its bytes
+  this._text = null       // its bytes as one latin1 string (ASCII keys are cut from it)
+  this._tooBig = 0        // its carried Change frame was larger than a Buffer can hold
   this._next = 0          // next frame to deliver
-  this._tooBig = 0        // a carried Change frame larger than a Buffer can hold
+  this.timing = { batches: 0, h2d: 0, gpu: 0, d2h: 0, convert: 0, replay: 0 } // ms, summed
 
   var self = this
   this._up = function () {
@@ -171,14 +180,16 @@ Decoder.prototype.end = function (data, enc, cb) {
   stream.Writable.prototype.end.call(this, cb)
 }
 
-// Hand the queued bytes to the GPU (one batch), or finish when nothing is left.
+// Hand the queued bytes to the GPU (one batch), or finish when nothing is left. At most one
+// batch is on the GPU and one waits decoded while another is replayed: batch k + 1 is split and
+// decoded on the worker thread while batch k's callbacks run here.
 Decoder.prototype._kick = function () {
-  if (this._busy || this.destroyed) return
+  if (this._inflight || this._ready || this._halt || this.destroyed) return
   if (!this._queued) {
     var held = this._held
     this._held = null
     if (held) held()
-    if (this._final && !this._queued && !this._busy) {
+    if (this._final && !this._queued && !this._res && !this._inflight) {
       var fin = this._final
       this._final = null
       this._onfinalize(fin) // decode.js:125-128
@@ -208,23 +219,29 @@ Decoder.prototype._kick = function () {
     this._carry = null
   }
   var batch = chunks.length === 1 ? chunks[0] : Buffer.concat(chunks)
-  this._busy = true
+  this._inflight = true
+  var held = this._held // its bytes are in this batch now
+  this._held = null
   var self = this
   native.decode(this._ctx, batch, this._blobLeft, function (err, res) {
     self._ondecoded(err, res, batch)
   }, this._keyPost)
+  if (held) held()
 }
 
 Decoder.prototype._ondecoded = function (err, res, batch) {
+  this._inflight = false
   if (this.destroyed) return
   if (err) return this.destroy(err)
+  // the carry into the next batch (decode.js:75-81) is known now, before the replay
+  var tooBig = 0
   if (!res.errCode) {
     var rest = batch.length - res.consumed
     if (res.tailKind === TAIL_HEADER) {
       this._carry = Buffer.from(batch.slice(res.consumed)) // copied, as into _header
     } else if (res.tailKind === TAIL_CHANGE) {
       if (res.frameBytes > MAX_FRAME) {
-        this._tooBig = res.frameBytes // reported after the frames before it (the reference throws)
+        tooBig = res.frameBytes // reported after the frames before it (the reference throws)
       } else {
         var buf = Buffer.allocUnsafe(res.frameBytes) // decode.js:227 allocates _buffer the same way
         batch.copy(buf, 0, res.consumed)
@@ -233,18 +250,85 @@ Decoder.prototype._ondecoded = function (err, res, batch) {
     }
   }
   this._blobLeft = res.blobRemaining
+  if (res.errCode || tooBig) this._halt = true
+  var t = res.t
+  if (t) {
+    var tm = this.timing
+    tm.batches++
+    tm.h2d += t.h2d
+    tm.gpu += t.gpu
+    tm.d2h += t.d2h
+    tm.convert += t.convert
+  }
+  var entry = { res: res, buf: batch, tooBig: tooBig }
+  if (this._res) {
+    this._ready = entry
+    return
+  }
+  this._play(entry)
+}
+
+Decoder.prototype._play = function (e) {
+  var res = e.res
+  var batch = e.buf
   this._res = res
   this._buf = batch
+  this._tooBig = e.tooBig
+  this._text = res.asciiKeys && batch.length <= TEXT_MAX && batch.length <= TEXT_PER_FRAME * res.n
+    ? batch.toString('latin1') : null
   this._next = 0
+  this._kick() // the next batch goes to the GPU before this one's callbacks run
   this._replay()
 }
 
 // Deliver decoded frames in order while no callback is outstanding (decode.js:144-169).
+// Change frames are built inline (the hot loop: one object, one key string, one value slice per
+// frame); keys the GPU flagged ASCII are cut from one latin1 string of the batch (the same string
+// buf.toString('utf8', ...) would give, without a UTF-8 decode per key).
 Decoder.prototype._replay = function () {
   var res = this._res
-  while (this._next < res.n && this._pending <= 0 && !this.destroyed) {
-    this._deliver(this._next++)
+  var buf = this._buf
+  var n = res.n
+  var type = res.type
+  var off = res.off
+  var flags = res.flags
+  var ko = res.ko
+  var kl = res.kl
+  var keyHash = res.keyHash
+  var text = this._text
+  var down = this._down
+  var i = this._next
+  var t0 = process.hrtime()
+  // (no callback can re-enter this loop: _down only resumes a paused replay)
+  while (i < n && this._pending <= 0 && !this.destroyed) {
+    if ((type[i] & TYPE_MASK) !== 1) {
+      this._deliverBlob(i)
+      i++
+      continue
+    }
+    // messages.Change.decode result shape: {subset, key, change, from, to, value}
+    var o = off[i]
+    var f = flags[i]
+    var k0 = o + ko[i]
+    var k1 = k0 + kl[i]
+    var vo = o + res.vo[i]
+    var change = {
+      subset: (f & 1) ? buf.toString('utf8', o + res.so[i], o + res.so[i] + res.sl[i]) : '',
+      key: (text !== null && (f & KEY_ASCII)) ? text.substring(k0, k1) : buf.toString('utf8', k0, k1),
+      change: res.change[i],
+      from: res.from[i],
+      to: res.to[i],
+      value: (f & 2) ? buf.slice(vo, vo + res.vl[i]) : null
+    }
+    if (keyHash) change.keyHash = keyHash[i]
+    this.changes++
+    this._pending++ // released by the handler's cb (_up, decode.js:89-93)
+    this._onchange(change, down)
+    i++
   }
+  this._next = i
+  var dt = process.hrtime(t0)
+  this.timing.replay += dt[0] * 1e3 + dt[1] * 1e-6
   if (this.destroyed) return
   if (this._pending > 0) {
     this._paused = true // resumed by _down
@@ -256,33 +340,19 @@ Decoder.prototype._replay = function () {
   }
   this._res = null
   this._buf = null
-  this._busy = false
-  this._kick()
+  this._text = null
+  var next = this._ready
+  this._ready = null
+  if (next) this._play(next)
+  else this._kick()
 }
 
-Decoder.prototype._deliver = function (i) {
+// blob frame (or the continuation of one opened in an earlier batch)
+Decoder.prototype._deliverBlob = function (i) {
   var res = this._res
   var buf = this._buf
   var type = res.type[i]
   var off = res.off[i]
-  if ((type & TYPE_MASK) === 1) {
-    // messages.Change.decode result shape: {subset, key, change, from, to, value}
-    var flags = res.flags[i]
-    var ko = off + res.ko[i]
-    var change = {
-      subset: (flags & 1) ? buf.toString('utf8', off + res.so[i], off + res.so[i] + res.sl[i]) : '',
-      key: buf.toString((flags & KEY_ASCII) ? 'latin1' : 'utf8', ko, ko + res.kl[i]),
-      change: res.change[i],
-      from: res.from[i],
-      to: res.to[i],
-      value: (flags & 2) ? buf.slice(off + res.vo[i], off + res.vo[i] + res.vl[i]) : null
-    }
-    if (res.keyHash) change.keyHash = res.keyHash[i]
-    this.changes++
-    this._onchange(change, this._up())
-    return
-  }
-  // blob frame (or the continuation of one opened in an earlier batch)
   if (!(type & CONT)) {
     this.blobs++
     this._blob = new BlobStream(this)

@@ -77,8 +77,10 @@ function uint (obj, k) {
   return v
 }
 
-function Encoder () {
-  if (!(this instanceof Encoder)) return new Encoder()
+// opts (not in the reference, whose constructor takes none): device: the GPU this stream
+// encodes on (default: DRP_DEVICE or 0)
+function Encoder (opts) {
+  if (!(this instanceof Encoder)) return new Encoder(opts)
   stream.Readable.call(this)
 
   this.destroyed = false
@@ -92,7 +94,7 @@ function Encoder () {
   this._scheduled = false
   this._ondrain = null
   this._out = []       // ordered output: {data, cb} (data null until its encode completes), or EOF
-  this._ctx = native.context()
+  this._ctx = native.context(opts && opts.device)
 }
 util.inherits(Encoder, stream.Readable)
 

@@ -27,8 +27,9 @@ EXPORTS = [
     "drp_encode_size", "drp_encode_device",
     "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results", "drp_device",
     "drp_comm_id", "drp_comm_init_rank", "drp_comm_init_all", "drp_comm_destroy",
-    "drp_index_allgather", "drp_index_allgather_multi",
+    "drp_index_allgather", "drp_index_allgather_multi", "drp_index_allgather_host", "drp_device_count",
 ]
+KEY_POST_OFF, KEY_POST_HASH, KEY_POST_FLAGS = 0, 1, 2
 DRP_E_COMM = -7
 COMM_ID_BYTES = 128
 
@@ -68,7 +69,7 @@ class StreamStats(C.Structure):
 class Timing(C.Structure):
     _fields_ = [("decode_ms", C.c_float), ("finalize_ms", C.c_float), ("total_ms", C.c_float),
                 ("strict_reruns", U32), ("spec_repairs", U32), ("exact_retries", U32), ("verify_relisted", U32),
-                ("seg_repairs", U32), ("reserved", U32)]
+                ("seg_repairs", U32), ("reserved", U32), ("h2d_ms", C.c_float), ("d2h_ms", C.c_float)]
 
 
 _lib = None
@@ -118,12 +119,15 @@ def lib():
         L.drp_index_allgather.argtypes = [P, P, P, U64, P, P]
         L.drp_index_allgather_multi.argtypes = [C.POINTER(P), C.POINTER(P), C.c_int, C.POINTER(P), U64,
                                                 C.POINTER(P), C.POINTER(P)]
+        L.drp_index_allgather_host.argtypes = [C.POINTER(P), C.POINTER(P), C.c_int, C.POINTER(P), U64, P, P]
+        L.drp_device_count.argtypes = [C.POINTER(C.c_int)]
         for f in ["drp_open", "drp_synchronize", "drp_last_timing", "drp_set_tile",
                   "drp_set_strict", "drp_set_exact", "drp_set_key_post", "drp_decode_device", "drp_decode_batch",
                   "drp_decode_stage", "drp_decode_fetch", "drp_encode_size",
                   "drp_encode_device", "drp_encode_batch", "drp_index_scan",
                   "drp_stream_stats_from_results", "drp_device", "drp_comm_id", "drp_comm_init_rank",
-                  "drp_comm_init_all", "drp_index_allgather", "drp_index_allgather_multi"]:
+                  "drp_comm_init_all", "drp_index_allgather", "drp_index_allgather_multi",
+                  "drp_index_allgather_host", "drp_device_count"]:
             getattr(L, f).restype = C.c_int
         _lib = L
     return _lib
@@ -262,7 +266,7 @@ class Ctx:
         carry = Carry(blob_remaining, 0, 0, 0, 0)
         nf, ef, ec, ed = U64(), U64(), U32(), U32()
         buf = w if n else np.zeros(16, np.uint8)
-        _chk("drp_set_key_post", self.L.drp_set_key_post(self.h, 1 if key_hash else 0))
+        _chk("drp_set_key_post", self.L.drp_set_key_post(self.h, KEY_POST_HASH if key_hash else KEY_POST_OFF))
         _chk("drp_decode_stage", self.L.drp_decode_stage(self.h, _p(buf), n, C.byref(carry), C.byref(nf),
                                                          C.byref(ef), C.byref(ec), C.byref(ed)))
         rows = int(nf.value) + (1 if ec.value in (ERR_CHANGE, ERR_REQUIRED) else 0)

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DRP_ABI_VERSION 2
+#define DRP_ABI_VERSION 3
 
 /* ---- return codes -------------------------------------------------------- */
 #define DRP_OK 0
@@ -156,10 +156,15 @@ typedef struct drp_timing {
   uint32_t verify_relisted; /* tiles verify_lite handed to verify_counts (a re-walk or a longer look-back) */
   uint32_t seg_repairs;     /* streams whose claims the segmented repair recomputed (miss cascades) */
   uint32_t reserved;
+  /* host-batch calls (drp_decode_stage / drp_decode_fetch / drp_decode_batch), wall clock: */
+  float h2d_ms;   /* staging the batch into HBM */
+  float d2h_ms;   /* copying the columns back (drp_decode_fetch) */
 } drp_timing;
 
 /* ---- context ------------------------------------------------------------- */
 int drp_abi_version(void);
+/* Number of HIP devices visible to the process (0 when none; gfx950 is checked by drp_open). */
+int drp_device_count(int *n);
 int drp_open(int device, drp_ctx **out);
 void drp_close(drp_ctx *ctx);
 /* The hipStream_t (as void*) all kernels of this ctx are launched on. */
@@ -174,9 +179,15 @@ int drp_set_tile(drp_ctx *ctx, uint32_t tile_bytes);
  * speculate-and-verify kernel and fall back to the exact one when a prediction fails.
  * Results are identical either way; drp_timing.strict_reruns reports a fallback. */
 int drp_set_exact(drp_ctx *ctx, int exact);
-/* 1: drp_decode_stage also computes the key hash / key flags (fetched when the caller's
- * drp_changes.key_hash is non-NULL); 0 (default): it does not. */
-int drp_set_key_post(drp_ctx *ctx, int on);
+/* Key post-processing on every decode of the ctx (drp_keys.hip):
+ * DRP_KEY_POST_HASH (1): the key hash column (drp_decode_stage: fetched when the caller's
+ *   drp_changes.key_hash is non-NULL) and the key flags DRP_F_KEY_ASCII / DRP_F_KEY_UTF8;
+ * DRP_KEY_POST_FLAGS (2): the key flags only (no hash column);
+ * DRP_KEY_POST_OFF (0, default): neither. */
+#define DRP_KEY_POST_OFF 0
+#define DRP_KEY_POST_HASH 1
+#define DRP_KEY_POST_FLAGS 2
+int drp_set_key_post(drp_ctx *ctx, int mode);
 /* Look-back composes exact inclusive exits only, never the per-tile maps agg_t. Test hook. */
 int drp_set_strict(drp_ctx *ctx, int strict);
 /* Device scratch bytes needed to decode `n` bytes split into `nstreams` streams. */
@@ -266,6 +277,12 @@ int drp_index_allgather(drp_ctx *ctx, drp_comm *comm, const drp_stream_stats *lo
 /* The same for ngpu contexts in one process (one grouped all-gather). */
 int drp_index_allgather_multi(drp_ctx **ctxs, drp_comm **comms, int ngpu, const drp_stream_stats *const *local,
                               uint64_t per_gpu, drp_stream_stats *const *global, uint64_t *const *base);
+/* drp_index_allgather_multi from HOST arrays (a host that keeps its per-stream counters on the
+ * CPU, e.g. the N-API addon): local[g][per_gpu] are staged to device g, all-gathered over RCCL,
+ * scanned on every device, and device 0's table and bases are copied to global[ngpu * per_gpu]
+ * and base[ngpu * per_gpu]. Returns after completion. */
+int drp_index_allgather_host(drp_ctx **ctxs, drp_comm **comms, int ngpu, const drp_stream_stats *const *local,
+                             uint64_t per_gpu, drp_stream_stats *global, uint64_t *base);
 
 #ifdef __cplusplus
 }

@@ -12,12 +12,17 @@ var write = Number(process.argv[3])
 var reps = Number(process.argv[4] || 3)
 var frames = 0
 var times = []
+var breakdown = []
 
 function once (done) {
   var d = protocol.decode()
   d.change(function (c, cb) { frames++; cb() })
   var t0 = process.hrtime.bigint()
-  d.on('finish', function () { times.push(Number(process.hrtime.bigint() - t0) / 1e9); done() })
+  d.on('finish', function () {
+    times.push(Number(process.hrtime.bigint() - t0) / 1e9)
+    breakdown.push(d.timing)
+    done()
+  })
   var pos = 0
   ;(function pump () {
     while (pos < wire.length) {
@@ -34,10 +39,19 @@ function once (done) {
     var t = times.slice(1) // the first pass warms up (device context, allocations)
     var best = Math.min.apply(null, t)
     var mean = t.reduce(function (a, b) { return a + b }, 0) / t.length
+    // per pass, ms, mean over the timed passes: H2D (staging into HBM), the decode kernels, the
+    // D2H of the columns and their u64 -> Number conversion run on the addon's worker thread,
+    // overlapped with the JS replay of the previous batch (building the change objects and
+    // running the callbacks) on the main thread
+    var b = breakdown.slice(1)
+    var ms = {}
+    ;['h2d', 'gpu', 'd2h', 'convert', 'replay', 'batches'].forEach(function (k) {
+      ms[k] = b.reduce(function (a, x) { return a + x[k] }, 0) / b.length
+    })
     process.stdout.write(JSON.stringify({ write_bytes: write, max_batch: Number(process.env.DRP_MAX_BATCH || 0) ||
       64 * 1024 * 1024, wire_bytes: wire.length, frames_per_pass: frames / (reps + 1), seconds_mean: mean,
       seconds_best: best, frames_per_s: frames / (reps + 1) / mean, wire_GBps: wire.length / mean / 1e9,
-      node: process.version }) + '\n')
+      breakdown_ms_per_pass: ms, wall_ms_per_pass: mean * 1e3, node: process.version }) + '\n')
     return
   }
   once(function () { next(i + 1) })

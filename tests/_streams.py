@@ -174,3 +174,18 @@ def shadow_stream(nframes, period=8192, shadow_at=100, small=10, seed=7, change_
         out[s:s + len(sh_small)] = sh_small
         out[s + small:s + small + len(sh_big)] = sh_big
     return bytes(out)
+
+
+def shadow_stream_np(nframes, period, shadow_at, small, seed=7):
+    """shadow_stream for blob frames only, vectorised (GB-sized inputs): every period-byte row
+    holds the real blob header at 0 and the shadow chain's two headers at shadow_at and
+    shadow_at + small over random payload bytes."""
+    a = np.random.default_rng(seed).integers(0, 256, size=(nframes, period), dtype=np.uint8)
+    kr = len(varint(period - 2))
+    hdr = varint(period - kr) + b"\x02"
+    sh_small = varint(small - 1) + b"\x02"
+    sh_big_len = period - small
+    sh_big = varint(sh_big_len - len(varint(sh_big_len))) + b"\x02"
+    for off, h in [(0, hdr), (shadow_at, sh_small), (shadow_at + small, sh_big)]:
+        a[:, off:off + len(h)] = np.frombuffer(h, np.uint8)
+    return a.reshape(-1)

@@ -5,17 +5,23 @@
 //   mode "destroy": async acks, and decoder.destroy() inside the n-th change callback
 //   mode "digest": events carry sha256 of keys/values/blob data instead of hex
 //   mode "keyhash": decode({keyHash: true}); change events also carry keyHash (decimal)
+//   mode "ticks": one write per event-loop turn (synchronous acks)
+// DRP_MAX_BATCH in the environment sets the decoder's batch threshold
 'use strict'
 var fs = require('fs')
 var path = require('path')
 var crypto = require('crypto')
-var protocol = require(path.join(__dirname, '..', '..', 'dat-replication-protocol_amd'))
+var pkg = path.join(__dirname, '..', '..', 'dat-replication-protocol_amd')
+// DRP_MOCK_NATIVE=1: the CPU stand-in for the addon (tests/js/mock_native.js; CPU tests of the JS layer)
+if (process.env.DRP_MOCK_NATIVE === '1') require('./mock_native').install(pkg)
+var protocol = require(pkg)
 
 var wire = fs.readFileSync(process.argv[2])
 var sizes = (process.argv[3] || '65536').split(',').map(Number)
 var mode = process.argv[4] || ''
 var nth = Number(process.argv[5] || 0)
 var asyncAck = mode === 'async' || mode === 'destroy'
+var ticks = mode === 'ticks'
 var digest = mode === 'digest'
 function enc (b) {
   return digest ? crypto.createHash('sha256').update(b).digest('hex').slice(0, 16) : b.toString('hex')
@@ -55,10 +61,21 @@ function done () {
 }
 var pos = 0
 var k = 0
-while (pos < wire.length) {
-  var n = sizes[k++ % sizes.length]
-  d.write(wire.slice(pos, pos + n))
-  pos += n
+if (ticks) {
+  // one write per event-loop turn: each turn's bytes become a batch of their own
+  ;(function next () {
+    if (pos >= wire.length) return d.end()
+    var n = sizes[k++ % sizes.length]
+    d.write(wire.slice(pos, pos + n))
+    pos += n
+    setImmediate(next)
+  })()
+} else {
+  while (pos < wire.length) {
+    var n = sizes[k++ % sizes.length]
+    d.write(wire.slice(pos, pos + n))
+    pos += n
+  }
+  d.end()
 }
-d.end()
 setTimeout(function () { process.stderr.write('decode_events: timeout\n'); done(); process.exit(3) }, 100000).unref()

@@ -114,6 +114,49 @@ def test_cascade_512mb_under_50ms(ctx):
     assert best <= 0.050, f"{best * 1e3:.1f} ms"
 
 
+def test_dense_cascade_1_7gb(ctx):
+    """A 1.7 GB two-framing stream of dense small frames (200 B blobs whose payloads hold a
+    denser shadow chain, tests/_streams.shadow_stream_np): the prediction follows the shadow in
+    every tile. The segmented repair would walk ~16K frames per chain per segment (~13 ms); the
+    decode must see the range is dense and take the exact kernel, bit-exact with the generator's
+    frame table, and finish within the bound printed and asserted here."""
+    import ctypes as C
+
+    import torch
+
+    import bench
+    from _gpu import drp_amd
+    period = 200
+    n = int(1.7e9) // period
+    wire = S.shadow_stream_np(n, period=period, shadow_at=20, small=4)
+    dev = torch.device("cuda", 0)
+    w = torch.from_numpy(wire).to(dev)
+    del wire
+    so = torch.tensor([0, w.numel()], dtype=torch.int64, device=dev)
+    cap = n + 64
+    outs = bench.alloc_outputs(cap, dev)
+    res = torch.zeros(C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+    best = 1e9
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.decode_device(w, so, None, outs, cap, res)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    t = ctx.timing()
+    print(f"1.7 GB dense shadow stream: {best * 1e3:.1f} ms, repair passes {t.spec_repairs}, "
+          f"segmented repairs {t.seg_repairs}, exact re-runs {t.strict_reruns}")
+    hdr = len(S.varint(period - 2)) + 1
+    i = torch.arange(n, device=dev, dtype=torch.int64)
+    assert torch.equal(outs["payload_off"][:n], i * period + hdr)
+    assert bool((outs["payload_len"][:n] == period - hdr).all()) and bool((outs["type"][:n] == 2).all())
+    r = drp_amd.StreamResult.from_buffer_copy(res.cpu().numpy().tobytes())
+    assert (r.frames, r.blobs, r.err_code, r.tail_kind) == (n, n, 0, 0)
+    assert best <= 0.060, f"{best * 1e3:.1f} ms"
+    del w, outs
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("khbm", ["2", "3"])
 def test_weak_prediction_c5_round_trip(ctx, monkeypatch, khbm):
     """DRP_KSTRONG_HBM weakens claims_fast's check of deferred candidates (frames that leave the

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_oracle_under_asan_ubsan():
     # one test builds once and runs every seed (parallel workers must not relink the binary
     # while another one executes it)
-    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "fuzz"])
+    subprocess.check_call(["make", "-s", "-B", "-C", os.path.join(ROOT, "oracle"), "fuzz"])
     exe = os.path.join(ROOT, "oracle", "_build", "sanitize_fuzz")
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
     for seed in (1, 2, 3):
