@@ -358,11 +358,14 @@ def verify_c5(cols, heap, wire, o, res, n, dev, samples=256):
             assert torch.equal(wire[po + off_w:po + off_w + ln], heap[off_h:off_h + ln]), i
 
 
-def main_c5(args, dev):
+def main_c5(args, dev, rank=0, world=1):
     """--workload c5: batched encode -> decode round trip of 1M Changes with 4 KB values per
-    step on one GPU (BASELINE configs[4]); value = Changes round-tripped per second."""
+    step per GPU (BASELINE configs[4]: 8 x MI355X); each rank round-trips its own rows (weak
+    scaling), then the 32 B per-stream stats are all-gathered (drp_index_allgather over RCCL; gloo
+    only to rehearse ranks on one GPU). value = Changes round-tripped per second, whole job."""
+    dist = world > 1
     n = args.c5_changes
-    cols, heap, frame = c5_on_device(n, seed=55, dev=dev)
+    cols, heap, frame = c5_on_device(n, seed=55 + rank, dev=dev)
     W = int(frame.sum())
     out = torch.empty(W + 64, dtype=torch.uint8, device=dev)
     foff = torch.empty(n + 1, dtype=torch.int64, device=dev)
@@ -375,6 +378,7 @@ def main_c5(args, dev):
     ext = torch.cuda.ExternalStream(ctx.stream, device=dev)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     enc_ms, dec_ms = [], []
+    state = {"base": None}
 
     def step(timed):
         evs[0].record(ext)
@@ -382,6 +386,12 @@ def main_c5(args, dev):
         evs[1].record(ext)
         ctx.decode_device(wire, stream_off, None, outs, cap, res)
         evs[2].record(ext)
+        if dist:  # the only collective: one 32-byte stats record per rank's stream
+            stats = drp_dist.local_stats_device(ctx, res, stream_off)
+            if args.backend == "nccl":
+                _, state["base"] = drp_dist.global_index_rccl(ctx, stats, world)
+            else:
+                state["base"] = drp_dist.global_index_device(ctx, drp_dist.gather_stats(stats, world))
         if timed:
             torch.cuda.synchronize(dev)
             enc_ms.append(evs[0].elapsed_time(evs[1]))
@@ -393,36 +403,55 @@ def main_c5(args, dev):
     assert int(foff[n]) == W, (int(foff[n]), W)
     assert torch.equal(foff[1:] - foff[:-1], frame), "frame sizes differ from the encode.js layout"
     verify_c5(cols, heap, wire, outs, res, n, dev)
+    if dist:  # every rank's stream holds n frames: the global index of rank r's stream is r * n
+        assert torch.equal(state["base"].cpu(), torch.arange(world, dtype=torch.int64) * n), state["base"]
+        torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize(dev)
+    if dist:
+        torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    if dist:
+        cdev = dev if args.backend == "nccl" else torch.device("cpu")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(tt.item())
     H = int(heap.numel())
     e, d = float(np.mean(enc_ms)) / 1e3, float(np.mean(dec_ms)) / 1e3
     b_enc, b_dec = 49 * n + H + W, W + 13 * n + 49 * n
+    t = ctx.timing()
+    gather = ("drp_index_allgather (RCCL) of the 32 B stream stats + index scan" if args.backend == "nccl" else
+              "gloo all-gather of the 32 B stream stats + index scan") if dist else "no collective (1 GPU)"
     out_line = {
-        "metric": "round-tripped Change frames/sec (batched encode + decode), 1 MI355X",
-        "value": n * args.steps / elapsed, "unit": "frames/s", "n_gpus": 1, "steps": args.steps,
+        "metric": f"round-tripped Change frames/sec (batched encode + decode), {world} MI355X",
+        "value": n * world * args.steps / elapsed, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic: C5 columns + heap generated on device (seeded), resident in HBM",
-        "config": {"workload": f"C5: {n} Changes, 4096 B values, key U[1,256], change/from/to U[0,2^32)",
-                   "wire_bytes": W, "heap_bytes": H},
-        "wire_GBps": 2 * W * args.steps / elapsed / 1e9,
+        "data": "synthetic: C5 columns + heap generated on device (seeded per rank), resident in HBM",
+        "config": {"workload": f"C5: {n} Changes per GPU, 4096 B values, key U[1,256], change/from/to U[0,2^32)",
+                   "wire_bytes_per_gpu": W, "heap_bytes_per_gpu": H,
+                   "parallelism": f"one stream per GPU, {world} GPU(s); {gather}"},
+        "wire_GBps": 2 * W * world * args.steps / elapsed / 1e9,
         "roofline": {"bound": "hbm", "achieved": (b_enc + b_dec) / (e + d) / 1e9, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": (b_enc + b_dec) / (e + d) / 1e9 / HBM_PEAK_GBPS,
                      "traffic": None, "kernel": "encode (enc_size, enc_scan, enc_write) + speculative decode",
-                     "bytes_model": "encode 49*C + H + W, decode W + 13*F + 49*C"},
+                     "bytes_model": "encode 49*C + H + W, decode W + 13*F + 49*C (rank 0)"},
         "encode": {"ms": e * 1e3, "GBps": b_enc / e / 1e9, "frac": b_enc / e / 1e9 / HBM_PEAK_GBPS},
         "decode": {"ms": d * 1e3, "GBps": b_dec / d / 1e9, "frac": b_dec / d / 1e9 / HBM_PEAK_GBPS,
-                   "exact_fallbacks": ctx.timing().strict_reruns, "repair_passes": ctx.timing().spec_repairs},
+                   "exact_fallbacks": t.strict_reruns, "repair_passes": t.spec_repairs,
+                   "segmented_repairs": t.seg_repairs},
     }
-    if not args.no_cpu:
-        out_line["cpu_baseline"] = cpu_baseline_c5()
-    print(json.dumps(out_line), flush=True)
+    if rank == 0:
+        if world == 1 and not args.no_cpu:
+            out_line["cpu_baseline"] = cpu_baseline_c5()
+        print(json.dumps(out_line), flush=True)
+    drp_dist.close_comms()
     ctx.close()
+    if dist:
+        torch.distributed.destroy_process_group()
 
 
 def main():
@@ -467,8 +496,7 @@ def main():
     torch.cuda.set_device(dev)
 
     if args.workload == "c5":
-        assert not dist, "c5 is a one-GPU round-trip workload"
-        return main_c5(args, dev)
+        return main_c5(args, dev, rank, world)
     if args.workload == "c2":
         nframes = args.frames
         wire = c2_on_device(nframes, seed=1234 + rank, dev=dev)
@@ -578,6 +606,9 @@ def main():
             "wire_GBps": wire_total / elapsed / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profile(kname, nframes),
+                         "traffic_source": "not measured in this run: profiles/pmc_decode.json (rocprofv3 "
+                                           "FETCH_SIZE x2 + WRITE_SIZE per frame, separate --pmc passes of "
+                                           "scripts/gpu_pmc.sh on a 20M-frame C2 launch) x this launch's frames",
                          "kernel": kname, "kernel_ms": dec_avg_s * 1e3,
                          "exact_fallbacks": fallbacks, "repair_passes": repairs,
                          "verify_relisted_tiles": relisted // max(1, args.steps),

@@ -566,7 +566,8 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
   // With a work list (the fast kernel ran first): the edge and dense tiles it listed, a few per
   // workgroup; without one: every tile, one per workgroup.
   const uint32_t nwork = P.work ? *P.work_n : 0u;
-  for (uint32_t wi = blockIdx.x; P.work ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
+  const uint32_t wfrom = (P.work && P.work_from) ? *P.work_from : 0u;  // (chunked: this chunk's entries)
+  for (uint32_t wi = wfrom + blockIdx.x; P.work ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
   const uint64_t t = P.work ? P.work[wi] : wi;
   bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
@@ -872,6 +873,55 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
   return v;
 }
 
+// A Change frame that leaves the listed positions (long frames: C5's 4 KB values) cannot have its
+// chain followed in the image. It is strong when its payload parses as a Change in the schema's
+// own shape: one-byte tags of the schema with their wire types (length-delimited subset, key and
+// value; varint change, from and to of <= 5 bytes), every field header inside the image, the
+// required fields present, and the last field ending exactly at the payload end (the value's
+// bytes are not read). Random bytes essentially never pass; a real frame in another shape is left
+// undecided as before. Prediction only: verification is exact.
+#ifndef DRP_CHANGE_FILLS
+#define DRP_CHANGE_FILLS 1
+#endif
+__device__ __forceinline__ bool change_fills(const uint32_t *w32, uint32_t po, uint32_t pl) {
+  uint32_t off = 0, found = 0;
+#pragma unroll 1
+  for (uint32_t f = 0; f < 8u && off < pl; f++) {
+    const uint32_t q = po + off;
+    if (q + 12u > IMG) return false;
+    const uint32_t d = q >> 2, sh = (q & 3u) * 8u;
+    const uint32_t a0 = w32[d], a1 = w32[d + 1], a2 = w32[d + 2];
+    const uint32_t w = __builtin_amdgcn_alignbit(a1, a0, sh), wn = __builtin_amdgcn_alignbit(a2, a1, sh);
+    const uint32_t b0 = w & 0xFFu, tag = b0 >> 3;
+    const bool num = tag - 3u <= 2u;  // change / from / to: varints; subset / key / value: lengths
+    if (b0 >= 0x80u || tag - 1u > 5u || (b0 & 7u) != (num ? 0u : 2u)) return false;
+    const uint32_t x = __builtin_amdgcn_alignbit(wn, w, 8);  // bytes 1..4
+    const uint32_t tm = ~x & 0x80808080u;
+    uint32_t k2;
+    uint64_t v = (x & 0x7Fu) | ((x >> 1) & 0x3F80u) | ((x >> 2) & 0x1FC000u) | ((x >> 3) & 0xFE00000u);
+    if (tm) {
+      k2 = ((uint32_t)__builtin_ctz(tm) >> 3) + 1u;
+      v &= (1u << (7u * k2)) - 1u;
+    } else {
+      const uint32_t b5 = (wn >> 8) & 0xFFu;
+      if (b5 & 0x80u) return false;
+      k2 = 5u;
+      v |= (uint64_t)b5 << 28;
+    }
+    if (k2 + 1u > pl - off) return false;
+    if (num) {
+      found |= 1u << (tag - 2u);
+      off += 1u + k2;
+    } else {
+      const uint32_t o2 = off + 1u + k2;
+      if (v > (uint64_t)(pl - o2)) return false;
+      if (tag == 2u) found |= 1u;
+      off = o2 + (uint32_t)v;
+    }
+  }
+  return off == pl && found == 15u;
+}
+
 // Node word: successor code (node index or NX_*) | min(successor offset, 0x3FFF) << 16 | id << 30
 // (id 3: the node's own header is invalid).
 // Walk from node exit x (offset < s1r) through the thread's bytes: returns the exit (a node whose
@@ -986,6 +1036,9 @@ struct FastLds {
   uint32_t xw[8];
   uint32_t xf[2 * NT / WAVE], wl[NT / WAVE], fl[NT / WAVE];
   uint64_t xm[4];  // candidate masks (two waves): [w] strong, [2 + w] strong and far
+#ifdef DRP_K1_PAD
+  uint8_t pad[DRP_K1_PAD];  // (A/B only: caps the workgroups per CU through LDS)
+#endif
 };
 enum : uint32_t { FC_OK = 0, FC_DENSE = 1, FC_ABLATE = 2 };
 
@@ -1143,8 +1196,9 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
         c = NX_NEAR;  // ends at the stream end: survived
         a = 1;
       } else if (succ >= (DRP_HALO_NODES ? IMG - 16 : TILE)) {
-        c = NX_FAR;   // past the listed positions: undecided (a restart that needs it checks in HBM)
-        a = 2;
+        c = NX_FAR;   // past the listed positions: undecided (a restart that needs it checks in HBM),
+        a = 2;        // unless it is a Change frame whose fields fill it exactly (strong by structure)
+        if (DRP_CHANGE_FILLS && id == 1u && change_fills(w32, o + k + 1u, L - 1u)) a = 1;
       } else {
         const uint32_t th = succ / SEGB, b = succ % SEGB;
         const uint64_t lw = lmw[th];
@@ -1336,7 +1390,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
 
 __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) {
   __shared__ FastLds S;
-  const uint64_t t = blockIdx.x;
+  const uint64_t t = P.tile0 + blockIdx.x;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   const TileGeo G = tile_geo(P, t);
   if (t >= ntiles) return;  // (whole workgroup)
@@ -1360,7 +1414,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
 // that does not pass (a re-walk is needed, a miss, a longer identity run) goes to a list that
 // verify_counts then takes, so results are verify_counts' in every case. Threads before k are
 // left to emit_tiles through tile_k (the records stay as kernel 1 wrote them).
-constexpr uint32_t VL_BLK = 256, VL_G = 8;
+constexpr uint32_t VL_BLK = 256, VL_G = NT / 16;  // lanes per tile (16 threads' records each)
 #ifndef DRP_SP_FRAMES
 #define DRP_SP_FRAMES 8  // frames of a sparse tile (0: no sparse emission)
 #endif
@@ -1374,7 +1428,7 @@ __device__ __forceinline__ uint32_t restart_bytes(uint32_t x) {  // 4-bit mask: 
 }
 __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
   const uint32_t tid = threadIdx.x, r = tid & (VL_G - 1u), gb = (tid & 63u) & ~(VL_G - 1u);
-  const uint64_t t = ((uint64_t)blockIdx.x * VL_BLK + tid) / VL_G;
+  const uint64_t t = P.tile0 + ((uint64_t)blockIdx.x * VL_BLK + tid) / VL_G;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   if (t >= ntiles) return;  // (whole 8-lane group: no barriers or cross-group exchanges below)
   const TileGeo G = tile_geo(P, t);
@@ -1389,7 +1443,7 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
     const int64_t j = (int64_t)t - 1 - (int64_t)(VL_G * step + r);
     const bool virt = j < (int64_t)G.tf;
     const uint64_t c = virt ? G.e0 : P.claim[j];
-    const uint32_t gm = (uint32_t)(__ballot(virt || c != C_ID) >> gb) & 0xFFu;
+    const uint32_t gm = (uint32_t)(__ballot(virt || c != C_ID) >> gb) & ((1u << VL_G) - 1u);
     if (gm) {
       const uint32_t src = gb + (uint32_t)__builtin_ctz(gm);
       et = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(c >> 32), (int)src, WAVE) << 32) |
@@ -2002,14 +2056,15 @@ __global__ __launch_bounds__(256) void emit_sparse(DecodeParams P) {
   __shared__ uint32_t nl;
   __shared__ uint32_t fail[SP_TPB];
   const uint32_t tid = threadIdx.x;
-  const uint64_t t0 = (uint64_t)blockIdx.x * SP_TPB;
+  const uint64_t t0 = P.tile0 + (uint64_t)blockIdx.x * SP_TPB;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   if (tid == 0) nl = 0;
   if (tid < SP_TPB) fail[tid] = 0;
   __syncthreads();
-  // records: 8 lanes per tile (16 threads each), 32 tiles per pass
-  for (uint32_t pass = 0; pass < SP_TPB / 32; pass++) {
-    const uint32_t j = pass * 32u + tid / VL_G, r = tid % VL_G;
+  // records: VL_G lanes per tile (16 threads each), 256 / VL_G tiles per pass
+  constexpr uint32_t PER = 256 / VL_G;
+  for (uint32_t pass = 0; pass < SP_TPB / PER; pass++) {
+    const uint32_t j = pass * PER + tid / VL_G, r = tid % VL_G;
     const uint64_t t = t0 + j;
     const bool sp = t < ntiles && P.tile_sparse[t];
     uint32_t fm = 0;  // this lane's threads that deliver a frame at their entry
@@ -2076,7 +2131,7 @@ __global__ __launch_bounds__(256) void emit_sparse(DecodeParams P) {
     if (cc.err) atomicMin((unsigned long long *)&P.payload_err[G.s], (unsigned long long)f);
   }
   __syncthreads();
-  if (tid < SP_TPB && fail[tid]) P.tile_sparse[t0 + tid] = 0;
+  if (tid < SP_TPB && fail[tid]) P.tile_sparse[t0 + tid] = 0;  // ((t0 + tid < ntiles: fail is only set for tiles)
 }
 
 #ifndef DRP_EMIT32
@@ -2112,6 +2167,7 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
     const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = wi % 8u;  // contiguous eighth, so
     t = (uint64_t)x * q + min(x, r) + wi / 8u;  // neighbouring tiles share an L2 (column lines)
   }
+  if (FAST) t += P.tile0;
   if (!FAST) bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
   if (t >= ntiles) continue;  // (whole workgroup)
@@ -2399,6 +2455,37 @@ __global__ __launch_bounds__(256) void range_sum_kernel(const uint64_t *v, uint6
   if ((threadIdx.x & 63u) == 0 && acc) atomicAdd((unsigned long long *)out, (unsigned long long)acc);
 }
 
+__global__ __launch_bounds__(SCAN_BLK) void chunk_scan_kernel(const uint64_t *cnt, uint64_t *base, uint64_t t0,
+                                                              uint64_t t1, const uint64_t *tile_prefix, uint64_t nstreams,
+                                                              uint64_t *carry, uint64_t cap, uint32_t *overflow) {
+  __shared__ uint64_t sw[SCAN_BLK / WAVE];
+  const uint64_t nt = tile_prefix[nstreams];
+  if (t1 > nt) t1 = nt;
+  uint64_t c = *carry;
+  for (uint64_t a = t0; a < t1; a += SCAN_SPAN) {
+    const uint64_t i0 = a + threadIdx.x * SCAN_PER;
+    uint64_t v[SCAN_PER], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++) {
+      v[k] = i0 + k < t1 ? cnt[i0 + k] : 0;
+      sum += v[k];
+    }
+    uint64_t total;
+    uint64_t o = c + block_excl_scan64(sum, sw, total);
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_PER; k++) {
+      if (i0 + k < t1) {
+        base[i0 + k] = o;
+        if (i0 + k == nt - 1 && o + v[k] > cap) atomicOr(overflow, 1u);
+      }
+      o += v[k];
+    }
+    c += total;
+  }
+  __syncthreads();  // (every thread read *carry before it is written)
+  if (threadIdx.x == 0) *carry = c;
+}
+
 // per-stream change / blob counts (one thread per stream)
 __global__ void stream_counts_kernel(const uint64_t *tile_prefix, uint64_t nstreams, const uint64_t *count,
                                      const uint64_t *base, const uint64_t *nch, const uint64_t *nch_base,
@@ -2559,6 +2646,42 @@ extern "C" hipError_t drp_launch_range_sum(const uint64_t *v, uint64_t t0, uint6
   if (t1 <= t0) return hipSuccess;
   const uint64_t nb = (t1 - t0 + 255) / 256;
   hipLaunchKernelGGL(spec::range_sum_kernel, dim3((uint32_t)(nb < 1024 ? nb : 1024)), dim3(256), 0, st, v, t0, t1, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t drp_launch_chunk_scan(const uint64_t *cnt, uint64_t *base, uint64_t t0, uint64_t t1,
+                                            const uint64_t *tile_prefix, uint64_t nstreams, uint64_t *carry,
+                                            uint64_t cap, uint32_t *overflow, hipStream_t st) {
+  if (t1 <= t0) return hipSuccess;
+  hipLaunchKernelGGL(spec::chunk_scan_kernel, dim3(1), dim3(spec::SCAN_BLK), 0, st, cnt, base, t0, t1, tile_prefix,
+                     nstreams, carry, cap, overflow);
+  return hipGetLastError();
+}
+
+// Pipelined decode, one chunk of ntc tiles from P->tile0 (single stream; drp_api.hip): claims (the
+// general kernel takes the chunk's work-list entries from *P->work_from on), ...
+extern "C" hipError_t drp_launch_chunk_claims(const DecodeParams *P, uint64_t ntc, hipStream_t st) {
+  if (ntc == 0) return hipSuccess;
+  hipLaunchKernelGGL(spec::claims_fast, dim3((uint32_t)ntc), dim3(spec::NT), 0, st, *P);
+  hipLaunchKernelGGL(spec::spec_claims, dim3(64), dim3(spec::NT), 0, st, *P);
+  return hipGetLastError();
+}
+// ... verification (records-only, then verify_counts on the tiles it lists; caller zeroes vlist_n),
+extern "C" hipError_t drp_launch_chunk_verify(const DecodeParams *P, uint64_t ntc, hipStream_t st) {
+  if (ntc == 0) return hipSuccess;
+  const uint64_t nb = (ntc * spec::VL_G + spec::VL_BLK - 1) / spec::VL_BLK;
+  hipLaunchKernelGGL(spec::verify_lite, dim3((uint32_t)nb), dim3(spec::VL_BLK), 0, st, *P);
+  hipLaunchKernelGGL(spec::verify_counts, dim3(1024), dim3(spec::NT), 0, st, *P);
+  return hipGetLastError();
+}
+// ... and emission (sparse tiles, the fast kernel, the general one on its list; caller zeroes vlist_n)
+extern "C" hipError_t drp_launch_chunk_emit(const DecodeParams *P, uint64_t ntc, hipStream_t st) {
+  if (ntc == 0) return hipSuccess;
+  if (spec::SP_FRAMES && P->tile_sparse)
+    hipLaunchKernelGGL(spec::emit_sparse, dim3((uint32_t)((ntc + spec::SP_TPB - 1) / spec::SP_TPB)), dim3(256), 0, st,
+                       *P);
+  hipLaunchKernelGGL(spec::emit_tiles<true>, dim3((uint32_t)ntc), dim3(spec::NT), 0, st, *P);
+  hipLaunchKernelGGL(spec::emit_tiles<false>, dim3(1024), dim3(spec::NT), 0, st, *P);
   return hipGetLastError();
 }
 

@@ -112,6 +112,45 @@ __device__ __forceinline__ uint64_t enc_funnel(uint64_t lo, uint64_t hi, uint32_
   return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
 }
 
+#ifndef DRP_ENC_UNROLL
+#define DRP_ENC_UNROLL 1  // 16-byte blocks per lane in flight in the bulk copy
+#endif
+#ifndef DRP_ENC_NT
+#define DRP_ENC_NT 0  // 1: non-temporal heap loads and wire stores in the bulk copy (A/B)
+#endif
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 enc_ld(const uint4 *p) {
+#if DRP_ENC_NT
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void enc_st(uint4 *p, uint4 v) {
+#if DRP_ENC_NT
+  u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p));
+#else
+  *p = v;
+#endif
+}
+// 16 bytes starting `sh` bytes into lo (the next bytes from hi)
+__device__ __forceinline__ uint4 enc_shift(uint4 lo, uint4 hi, uint32_t sh) {
+  if (sh == 0) return lo;
+  const uint64_t q0 = ((uint64_t)lo.y << 32) | lo.x, q1 = ((uint64_t)lo.w << 32) | lo.z;
+  const uint64_t q2 = ((uint64_t)hi.y << 32) | hi.x, q3 = ((uint64_t)hi.w << 32) | hi.z;
+  uint64_t w0, w1;
+  if (sh < 8) {
+    w0 = enc_funnel(q0, q1, 8 * sh);
+    w1 = enc_funnel(q1, q2, 8 * sh);
+  } else {
+    w0 = enc_funnel(q1, q2, 8 * (sh - 8));
+    w1 = enc_funnel(q2, q3, 8 * (sh - 8));
+  }
+  return make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+}
+
 // Wave copy of n bytes: byte head up to 16-byte alignment of dst, then one aligned 16-byte
 // store per lane per step whose bytes come from the two aligned 16-byte source blocks that
 // cover them (funnel shift by the wave-uniform source misalignment), then a byte tail. The
@@ -131,26 +170,23 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
   const uint32_t sh = (uint32_t)((uintptr_t)src & 15);
   const uint4 *sa = reinterpret_cast<const uint4 *>(src - sh);
   uint4 *da = reinterpret_cast<uint4 *>(dst);
-  for (uint64_t b = lane; b < nb; b += 64) {
-    const uint4 lo = sa[b];
-    uint4 out;
-    if (sh == 0) {
-      out = lo;
-    } else {
-      const uint4 hi = sa[b + 1];
-      const uint64_t q0 = ((uint64_t)lo.y << 32) | lo.x, q1 = ((uint64_t)lo.w << 32) | lo.z;
-      const uint64_t q2 = ((uint64_t)hi.y << 32) | hi.x, q3 = ((uint64_t)hi.w << 32) | hi.z;
-      uint64_t w0, w1;
-      if (sh < 8) {
-        w0 = enc_funnel(q0, q1, 8 * sh);
-        w1 = enc_funnel(q1, q2, 8 * sh);
-      } else {
-        w0 = enc_funnel(q1, q2, 8 * (sh - 8));
-        w1 = enc_funnel(q2, q3, 8 * (sh - 8));
-      }
-      out = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+  uint64_t b = lane;
+#if DRP_ENC_UNROLL > 1
+  // DRP_ENC_UNROLL blocks per lane in flight: every load of a step is issued before its stores
+  for (; b + 64 * (DRP_ENC_UNROLL - 1) < nb; b += 64 * DRP_ENC_UNROLL) {
+    uint4 lo[DRP_ENC_UNROLL], hi[DRP_ENC_UNROLL];
+#pragma unroll
+    for (int u = 0; u < DRP_ENC_UNROLL; u++) {
+      lo[u] = enc_ld(sa + b + 64 * u);
+      hi[u] = sh ? enc_ld(sa + b + 64 * u + 1) : lo[u];
     }
-    da[b] = out;
+#pragma unroll
+    for (int u = 0; u < DRP_ENC_UNROLL; u++) enc_st(da + b + 64 * u, enc_shift(lo[u], hi[u], sh));
+  }
+#endif
+  for (; b < nb; b += 64) {
+    const uint4 lo = enc_ld(sa + b);
+    enc_st(da + b, sh == 0 ? lo : enc_shift(lo, enc_ld(sa + b + 1), sh));
   }
   const uint32_t tail = (uint32_t)(n & 15);
   if (lane < tail) dst[(nb << 4) + lane] = src[(nb << 4) + lane];

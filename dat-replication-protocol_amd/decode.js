@@ -22,6 +22,7 @@ var native = require('./native')
 
 var FLUSH = Buffer.from([0]) // identity-compared end sentinel (decode.js:6, :125)
 var MAX_BATCH = Number(process.env.DRP_MAX_BATCH) || 64 * 1024 * 1024
+var PIECE = Number(process.env.DRP_PIECE) || 16 * 1024 * 1024 // bytes per GPU call
 var MAX_FRAME = require('buffer').constants.MAX_LENGTH
 
 // a batch whose frames average at most TEXT_PER_FRAME bytes is turned into one latin1 string
@@ -196,9 +197,26 @@ Decoder.prototype._kick = function () {
     }
     return
   }
+  // at most PIECE bytes go to the GPU at a time (a big write is cut into pieces, so the decode of
+  // piece k + 1 overlaps the replay of piece k); the rest stays queued
   var chunks = this._queue
-  this._queue = []
-  this._queued = 0
+  if (this._queued <= PIECE) {
+    this._queue = []
+    this._queued = 0
+  } else {
+    var took = 0
+    var k = 0
+    while (took < PIECE) took += chunks[k++].length
+    var last = chunks[k - 1]
+    var over = took - PIECE
+    this._queue = chunks.slice(k)
+    if (over > 0) { // (slices share the write's memory: no copy)
+      chunks[k - 1] = last.slice(0, last.length - over)
+      this._queue.unshift(last.slice(last.length - over))
+    }
+    chunks = chunks.slice(0, k)
+    this._queued -= PIECE
+  }
   var p = this._partial
   if (p) {
     // collect the rest of a Change frame of known size: each byte is copied once
@@ -211,7 +229,7 @@ Decoder.prototype._kick = function () {
       if (take < c.length) chunks[k] = c.slice(take)
       else k++
     }
-    if (p.filled < p.buf.length) return this._kick() // nothing else to decode yet
+    if (p.filled < p.buf.length) return this._kick() // nothing else to decode yet (or the rest of the queue)
     this._partial = null
     chunks = [p.buf].concat(chunks.slice(k))
   } else if (this._carry) {
@@ -220,8 +238,8 @@ Decoder.prototype._kick = function () {
   }
   var batch = chunks.length === 1 ? chunks[0] : Buffer.concat(chunks)
   this._inflight = true
-  var held = this._held // its bytes are in this batch now
-  this._held = null
+  var held = this._queued ? null : this._held // all of its bytes are on their way to the GPU now
+  if (held) this._held = null
   var self = this
   native.decode(this._ctx, batch, this._blobLeft, function (err, res) {
     self._ondecoded(err, res, batch)

@@ -17,6 +17,8 @@ timeout -k 10 300 python -u bench.py > gpurun_out/bench_$TAG.log 2>&1
 echo bench done
 timeout -k 10 200 python -u bench.py --workload c5 --steps 5 --warmup 2 --no-cpu > gpurun_out/bench_c5_$TAG.log 2>&1
 echo c5 done
+timeout -k 10 200 python -u bench.py --workload c4 --steps 5 --warmup 2 --no-cpu > gpurun_out/bench_c4_$TAG.log 2>&1
+echo c4 done
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG -o run -- \
   python3 -u $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu > $GRAFT_REPO_ROOT/gpurun_out/bench_prof_$TAG.log 2>&1)
 echo prof done

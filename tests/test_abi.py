@@ -52,3 +52,15 @@ def test_open_without_gpu_fails_cleanly():
     with pytest.raises(drp_amd.DrpError) as e:
         drp_amd.Ctx(0)
     assert e.value.rc == drp_amd.DRP_E_NODEV
+
+
+def test_device_count_without_gpu():
+    """drp_device_count is callable anywhere (0 devices here, the box's count there)."""
+    import sys
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "dat-replication-protocol_amd", "python"))
+    import drp_amd
+    n = ctypes.c_int(-1)
+    assert drp_amd.lib().drp_device_count(ctypes.byref(n)) == 0
+    assert n.value == (torch.cuda.device_count() if torch.cuda.is_available() else 0)
+    assert drp_amd.lib().drp_device_count(None) == drp_amd.DRP_E_INVAL

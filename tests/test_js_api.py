@@ -264,6 +264,51 @@ def test_decoder_key_hash_option():
 
 @pytest.mark.gpu
 @needs_node
+def test_global_index_over_devices():
+    """Streams sharded over the process's devices (index.js shard: contiguous blocks, as
+    bench.py's C4 shards) each decode on their device ({device: k}); globalIndex() all-gathers
+    the per-stream counters through libdrp's RCCL communicators (drp_index_allgather_host, one
+    per device of this process) into every stream's global first-frame index. On a one-GPU box
+    all shards land on device 0; the frame counts must equal the oracle's and the bases their
+    prefix sums."""
+    rng = random.Random(41)
+    wires = [S.random_stream(rng, n, blob_p=0.05, blob_max=2000) for n in (300, 0, 1200, 57, 800)]
+    code = r"""
+var fs = require('fs'), p = require(%r)
+var wires = JSON.parse(fs.readFileSync(process.argv[1])).map(function (h) { return Buffer.from(h, 'hex') })
+var ndev = Math.max(1, p.devices())
+var devs = p.shard(wires.length, ndev)
+var decs = wires.map(function (w, i) { return p.decode({device: devs[i]}) })
+var left = decs.length
+decs.forEach(function (d, i) {
+  d.on('finish', function () { if (--left === 0) done() })
+  d.end(wires[i])
+})
+function done () {
+  var g = p.globalIndex(decs, ndev)
+  console.log(JSON.stringify({ndev: ndev, devs: devs, base: g.base, frames: g.frames,
+    counts: decs.map(function (d) { return [d.changes, d.blobs] })}))
+  process.exit(0)
+}
+""" % os.path.join(ROOT, "dat-replication-protocol_amd")
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump([w.hex() for w in wires], f)
+        path = f.name
+    try:
+        out = json.loads(subprocess.check_output([NODE, "-e", code, path], text=True, timeout=120))
+    finally:
+        os.unlink(path)
+    frames = []
+    for w, (ch, bl) in zip(wires, out["counts"]):
+        r = O.decode_batch(w)
+        assert (ch, bl) == (r["changes"], r["blobs"])
+        frames.append(r["nframes"])
+    assert out["frames"] == frames
+    assert out["base"] == [sum(frames[:i]) for i in range(len(frames))]
+
+
+@pytest.mark.gpu
+@needs_node
 def test_encoder_input_policy():
     """Encoder.change validates synchronously, as messages.Change.encode throws inside change()
     (encode.js:102-117): key must be a string, change/from/to unsigned integers <= 2^53 - 1
