@@ -251,7 +251,7 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.tk = o; o += al(L.ntiles_max);             // first entry thread per tile (verify_lite)
   L.tsp = o; o += al(L.ntiles_max);            // sparse-tile marks (verify_lite -> emit_sparse)
   L.fmiss = o; o += al(ns * 8);                  // first missed tile per stream (verify)
-  L.segw = o; o += al((2 * 64 * 1024 + 1025) * 8);  // segmented repair: candidates + entries
+  L.segw = o; o += al((2 * 64 * 8192 + 8193) * 8);  // segmented repair: candidates + entries (SEG_NMAX)
   L.scan_tmp = o; o += al((L.ntiles_max / 4096 + 2) * 8);  // tile scans: block sums
   L.total = o;
   return L;
@@ -433,8 +433,6 @@ int run_decode_exact(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const ui
 // when a prediction failed (or a bounded wait expired): the caller then runs the exact kernel.
 constexpr int kSpecRepairPasses = 16;
 constexpr int kChain = 3;  // dirty-list repair passes queued per host read
-constexpr uint64_t kSegFramesMax = 4096;      // frames per segment past which the exact kernel is cheaper
-constexpr uint64_t kSegDenseMinTiles = 8192;  // (ranges under 64 MiB always take the segmented repair)
 constexpr int kSegRepairAfter = 3;  // verify passes before the segmented repair of the streams still missing  // one verify pass each (0.7 ms on C5), vs ~1.5 s for an exact re-run there
 
 int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
@@ -564,30 +562,6 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
         CHK(hipMemcpyAsync(fm.data(), P.first_miss, ns * 8, hipMemcpyDeviceToHost, st));
         CHK(hipMemcpyAsync(tp.data(), tile_prefix, (ns + 1) * 8, hipMemcpyDeviceToHost, st));
         CHK(hipStreamSynchronize(st));
-        // The segmented repair walks up to 64 candidate chains per segment (<= 1024 segments)
-        // frame by frame, one lane each: its cost grows with the frames per segment, while the
-        // exact kernel's grows with the bytes (and is slow only on long random-payload frames).
-        // A range whose chains hold more than kSegFramesMax frames per segment (dense small
-        // frames: ~13 ms per 1.7 GB, against ~5 ms exact) goes to the exact kernel instead.
-        bool dense = false;
-        uint64_t *fsum = c->scratch.at<uint64_t>(L.segw);
-        for (uint64_t s = 0; s < ns && !dense; s++) {
-          if (fm[s] == ~0ull || tp[s + 1] - fm[s] < kSegDenseMinTiles) continue;
-          CHK(hipMemsetAsync(fsum, 0, 8, st));
-          CHK(drp_launch_range_sum(P.tile_count, fm[s], tp[s + 1], fsum, st));
-          uint64_t f = 0;
-          CHK(hipMemcpyAsync(&f, fsum, 8, hipMemcpyDeviceToHost, st));
-          CHK(hipStreamSynchronize(st));
-          const uint64_t nseg = std::min<uint64_t>(tp[s + 1] - fm[s], 1024);
-          dense = f / nseg > kSegFramesMax;
-          TRACE("decode_spec: stream %llu range %llu tiles, %llu frames on the predicted chains%s",
-                (unsigned long long)s, (unsigned long long)(tp[s + 1] - fm[s]), (unsigned long long)f,
-                dense ? ": dense, exact kernel" : "");
-        }
-        if (dense) {
-          h[1] = miss;  // (reported as a failed prediction: the caller runs the exact kernel)
-          break;
-        }
         for (uint64_t s = 0; s < ns; s++)
           if (fm[s] != ~0ull) {
             TRACE("decode_spec: segmented repair of stream %llu from tile %llu to %llu", (unsigned long long)s,

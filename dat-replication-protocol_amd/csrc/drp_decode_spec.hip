@@ -2265,7 +2265,9 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
 //                  chain position past it, the chain's end, or identity).
 // A verify pass then proves the new claims as usual. Cost: two streaming passes over the range
 // spread over the CUs plus a short serial stitch, however the predictions failed.
-constexpr uint32_t SEG_CAND = 64, SEG_GMAX = 1024;
+constexpr uint32_t SEG_CAND = 64, SEG_GMAX = 1024;  // candidates per segment, tiles per segment (max)
+constexpr uint64_t SEG_NMAX = 8192;  // segments per repair (max)
+constexpr uint64_t SEG_GMIN = 4;     // tiles per segment (min)
 struct SegRange {
   uint64_t s, t0, tl, G, nseg;  // stream, tiles [t0, tl), tiles per segment, segments
   uint64_t tend;                // the stream's tile end (tl < tend: the range was clamped)
@@ -2387,34 +2389,56 @@ __global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
   }
 }
 
-__global__ __launch_bounds__(WAVE) void seg_stitch(DecodeParams P, SegRange R) {
-  const uint32_t lane = threadIdx.x;
+// The candidate tables of SEG_SB segments at a time are staged in LDS by the whole workgroup
+// (double-buffered: the next block loads while wave 0 follows the chain through this one), so
+// the serial part is a ballot per segment on LDS data.
+constexpr uint32_t SEG_SB = 32, SEG_STB = 1024;  // segments per staged block, threads
+__global__ __launch_bounds__(SEG_STB) void seg_stitch(DecodeParams P, SegRange R) {
+  __shared__ uint64_t tab[2][SEG_SB][2 * SEG_CAND];  // 2 x 32 KB
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const TileGeo G = seg_geo(P, R.s);
+  constexpr uint32_t W = SEG_SB * 2 * SEG_CAND;  // words per block
+  auto load = [&](uint64_t blk, uint32_t buf) {
+    const uint64_t w0 = blk * W, wn = umin64(R.nseg * 2 * SEG_CAND, w0 + W);
+    for (uint64_t w = w0 + tid; w < wn; w += SEG_STB) (&tab[buf][0][0])[w - w0] = R.cand[w];
+  };
+  const uint64_t nblk = (R.nseg + SEG_SB - 1) / SEG_SB;
+  load(0, 0);
+  __syncthreads();
   uint64_t e = R.seg_entry[0];
-  for (uint64_t seg = 0; seg < R.nseg; seg++) {
-    const uint64_t send = seg_end(G, R, seg);
-    if (lane == 0) R.seg_entry[seg] = e;
-    if (!is_pos(e) || e >= send) continue;  // the chain ended, or jumps over the segment
-    const uint64_t st = R.cand[seg * 2 * SEG_CAND + lane];
-    const uint64_t hit = __ballot(st == e);
-    if (hit) {
-      e = readlane64(R.cand[seg * 2 * SEG_CAND + SEG_CAND + lane], (uint32_t)__builtin_ctzll(hit));
-      continue;
-    }
-    uint64_t p = e;  // not a candidate: walk it (one lane, headers from HBM)
-    if (lane == 0) {
-      while (p < send && p < G.se) {
-        const Hdr h = hdr_global(P.bytes, p, G.se);
-        if (h.kind != H_VALID) {
-          p = term_of(h, p);
-          break;
+  for (uint64_t blk = 0; blk < nblk; blk++) {
+    const uint32_t cur = (uint32_t)(blk & 1);
+    if (tid >= WAVE) {
+      if (blk + 1 < nblk) load(blk + 1, cur ^ 1u);  // (the other waves: the next block)
+    } else {
+      for (uint32_t k = 0; k < SEG_SB; k++) {
+        const uint64_t seg = blk * SEG_SB + k;
+        if (seg >= R.nseg) break;
+        const uint64_t send = seg_end(G, R, seg);
+        if (lane == 0) R.seg_entry[seg] = e;
+        if (!is_pos(e) || e >= send) continue;  // the chain ended, or jumps over the segment
+        const uint64_t hit = __ballot(tab[cur][k][lane] == e);
+        if (hit) {
+          e = tab[cur][k][SEG_CAND + (uint32_t)__builtin_ctzll(hit)];
+          continue;
         }
-        p = h.succ;
+        uint64_t p = e;  // not a candidate: walk it (one lane, headers from HBM)
+        if (lane == 0) {
+          while (p < send && p < G.se) {
+            const Hdr h = hdr_global(P.bytes, p, G.se);
+            if (h.kind != H_VALID) {
+              p = term_of(h, p);
+              break;
+            }
+            p = h.succ;
+          }
+        }
+        e = readlane64(p, 0);
       }
     }
-    e = readlane64(p, 0);
+    __syncthreads();  // (the next block is staged; this one's reads are done)
   }
-  if (lane == 0) R.seg_entry[R.nseg] = e;
+  if (tid == 0) R.seg_entry[R.nseg] = e;
 }
 
 __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
@@ -2445,14 +2469,6 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
     bsync();
   }
   for (uint64_t i = tid; i < tb - ta; i += NT) P.claim[ta + i] = lcl[i];
-}
-
-// sum of a per-tile column over a tile range (the segmented repair's cost estimate)
-__global__ __launch_bounds__(256) void range_sum_kernel(const uint64_t *v, uint64_t t0, uint64_t t1, uint64_t *out) {
-  uint64_t acc = 0;
-  for (uint64_t t = t0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; t < t1; t += (uint64_t)gridDim.x * 256) acc += v[t];
-  acc = wave_sum64(acc);
-  if ((threadIdx.x & 63u) == 0 && acc) atomicAdd((unsigned long long *)out, (unsigned long long)acc);
 }
 
 __global__ __launch_bounds__(SCAN_BLK) void chunk_scan_kernel(const uint64_t *cnt, uint64_t *base, uint64_t t0,
@@ -2641,14 +2657,6 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
                                   Q.scount, st);
 }
 
-extern "C" hipError_t drp_launch_range_sum(const uint64_t *v, uint64_t t0, uint64_t t1, uint64_t *out,
-                                           hipStream_t st) {
-  if (t1 <= t0) return hipSuccess;
-  const uint64_t nb = (t1 - t0 + 255) / 256;
-  hipLaunchKernelGGL(spec::range_sum_kernel, dim3((uint32_t)(nb < 1024 ? nb : 1024)), dim3(256), 0, st, v, t0, t1, out);
-  return hipGetLastError();
-}
-
 extern "C" hipError_t drp_launch_chunk_scan(const uint64_t *cnt, uint64_t *base, uint64_t t0, uint64_t t1,
                                             const uint64_t *tile_prefix, uint64_t nstreams, uint64_t *carry,
                                             uint64_t cap, uint32_t *overflow, hipStream_t st) {
@@ -2686,7 +2694,7 @@ extern "C" hipError_t drp_launch_chunk_emit(const DecodeParams *P, uint64_t ntc,
 }
 
 // Segmented repair of stream s from tile t0 (its first missed tile) to its end (the caller then
-// runs a verify pass). scratch: 2 * 64 * 1024 + 1025 words.
+// runs a verify pass). scratch: 2 * 64 * SEG_NMAX + SEG_NMAX + 1 words.
 extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, uint64_t t0, uint64_t tl,
                                             uint64_t *scratch, hipStream_t st) {
   if (tl <= t0) return hipSuccess;
@@ -2694,17 +2702,20 @@ extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, u
   R.s = s;
   R.t0 = t0;
   R.tend = tl;
-  // at most 1024 segments of SEG_GMAX tiles (8 GiB of 8 KiB tiles): a longer range is repaired up
-  // to there; the verify passes that follow prove the claims past it as before (or fall back)
-  const uint64_t n = tl - t0 < 1024ull * spec::SEG_GMAX ? tl - t0 : 1024ull * spec::SEG_GMAX;
+  // at most SEG_NMAX segments of SEG_GMAX tiles (64 GiB of 8 KiB tiles): a longer range is repaired
+  // up to there; the verify passes that follow prove the claims past it as before (or fall back).
+  // Short segments: a candidate chain walks only its segment (the SIMD's cost is its densest
+  // chain), and the segments fill the CUs several workgroups deep.
+  const uint64_t n = tl - t0 < spec::SEG_NMAX * spec::SEG_GMAX ? tl - t0 : spec::SEG_NMAX * spec::SEG_GMAX;
   R.tl = t0 + n;
-  R.G = (n + 1023) / 1024;
+  const uint64_t g = (n + spec::SEG_NMAX - 1) / spec::SEG_NMAX;
+  R.G = g > spec::SEG_GMIN ? g : spec::SEG_GMIN;
   R.nseg = (n + R.G - 1) / R.G;
   R.cand = scratch;
-  R.seg_entry = scratch + 2 * spec::SEG_CAND * 1024;
+  R.seg_entry = scratch + 2 * spec::SEG_CAND * spec::SEG_NMAX;
   DecodeParams Q = *P;
   hipLaunchKernelGGL(spec::seg_walk, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);
-  hipLaunchKernelGGL(spec::seg_stitch, dim3(1), dim3(WAVE), 0, st, Q, R);
+  hipLaunchKernelGGL(spec::seg_stitch, dim3(1), dim3(spec::SEG_STB), 0, st, Q, R);
   hipLaunchKernelGGL(spec::seg_claims, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);
   return hipGetLastError();
 }

@@ -192,6 +192,64 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
   if (lane < tail) dst[(nb << 4) + lane] = src[(nb << 4) + lane];
 }
 
+#ifndef DRP_ENC_COPY2
+#define DRP_ENC_COPY2 1  // 0: wave_copy (one source block pair per lane per step)
+#endif
+#ifndef DRP_ENC_BATCH
+#define DRP_ENC_BATCH 8  // 16-byte blocks per lane loaded before any is stored (wave_copy2)
+#endif
+// wave_copy2: the same aligned-store copy with up to DRP_ENC_BATCH blocks per lane loaded before
+// any is stored (a 4 KB value is one batch: every load of the copy is in flight at once), and
+// each source block loaded once: the second block a lane's funnel shift needs is the next lane's
+// first (a lane permute), lane 63 taking the first block of the next column. Copies under 64
+// bytes are one byte per lane.
+__device__ __forceinline__ void wave_copy2(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint64_t n,
+                                           uint32_t lane) {
+  if (n < 64) {
+    if (lane < n) dst[lane] = src[lane];
+    return;
+  }
+  const uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15);
+  if (lane < head) dst[lane] = src[lane];
+  dst += head;
+  src += head;
+  n -= head;
+  const uint64_t nb = n >> 4;
+  const uint32_t tail = (uint32_t)(n & 15);
+  const uint32_t sh = (uint32_t)((uintptr_t)src & 15);
+  const uint4 *sa = reinterpret_cast<const uint4 *>(src - sh);
+  uint4 *da = reinterpret_cast<uint4 *>(dst);
+  // source blocks needed: [0, nb) and, when shifted, block nb (it holds source bytes: the last
+  // byte is past 16 nb - sh + 15 whenever sh > 0 and the copy is not empty)
+  const uint64_t ns = nb + (sh ? 1 : 0);
+  const int nxt = (int)(((lane + 1) & 63u) << 2);
+  for (uint64_t b0 = 0; b0 < nb; b0 += 64 * DRP_ENC_BATCH) {
+    uint4 v[DRP_ENC_BATCH + 1];
+#pragma unroll
+    for (int u = 0; u <= DRP_ENC_BATCH; u++) {
+      const uint64_t b = b0 + 64u * u + lane;
+      v[u] = (u < DRP_ENC_BATCH || lane == 0) && b < ns ? enc_ld(sa + b) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < DRP_ENC_BATCH; u++) {
+      const uint64_t b = b0 + 64u * u + lane;
+      if (b0 + 64u * u >= nb) break;
+      uint4 w = v[u];
+      if (sh) {
+        const uint4 src_hi = lane == 63 ? v[u + 1] : v[u];
+        uint4 hi;
+        hi.x = (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)src_hi.x);
+        hi.y = (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)src_hi.y);
+        hi.z = (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)src_hi.z);
+        hi.w = (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)src_hi.w);
+        w = enc_shift(w, hi, sh);
+      }
+      if (b < nb) enc_st(da + b, w);
+    }
+  }
+  if (lane < tail) dst[(nb << 4) + lane] = src[(nb << 4) + lane];
+}
+
 #ifndef DRP_ENC_WAVES
 #define DRP_ENC_WAVES 65536  // waves of the write kernel (grid-stride over frames)
 #endif
@@ -232,6 +290,11 @@ __device__ __forceinline__ uint32_t put_segs(uint8_t *o, uint32_t lane, const VS
   return tot;
 }
 
+#if DRP_ENC_COPY2
+#define WAVE_COPY wave_copy2
+#else
+#define WAVE_COPY wave_copy
+#endif
 // one wave per frame (grid-stride over frames)
 __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
   const uint32_t lane = lane_id();
@@ -252,13 +315,13 @@ __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
       off = put_segs(o, lane, g);
     }
     if (sub) {
-      wave_copy(o + off, P.heap + s.subset_off[i], s.subset_len[i], lane);
+      WAVE_COPY(o + off, P.heap + s.subset_off[i], s.subset_len[i], lane);
       off += s.subset_len[i];
     }
     {
       const VSeg g[2] = {vbyte1(0x12), vseg(s.key_len[i])};
       off += put_segs(o + off, lane, g);
-      wave_copy(o + off, P.heap + s.key_off[i], s.key_len[i], lane);
+      WAVE_COPY(o + off, P.heap + s.key_off[i], s.key_len[i], lane);
       off += s.key_len[i];
     }
     {
@@ -266,7 +329,7 @@ __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
                          vbyte1(0x32, val), val ? vseg(s.value_len[i]) : VSeg{0ull, 0u, 0u}};
       off += put_segs(o + off, lane, g);
     }
-    if (val) wave_copy(o + off, P.heap + s.value_off[i], s.value_len[i], lane);
+    if (val) WAVE_COPY(o + off, P.heap + s.value_off[i], s.value_len[i], lane);
 #else
     // header + subset prefix
     uint8_t pre[32];

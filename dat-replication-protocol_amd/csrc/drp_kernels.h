@@ -103,7 +103,6 @@ uint32_t drp_spec_miss_bit(void);
 hipError_t drp_launch_spec_head(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                 uint32_t *tile_stream, hipStream_t st);
 // out[0] += sum of v[t0, t1) (out zeroed by the caller)
-hipError_t drp_launch_range_sum(const uint64_t *v, uint64_t t0, uint64_t t1, uint64_t *out, hipStream_t st);
 // tile_base over tiles [t0, t1) = *carry + exclusive prefix of cnt; *carry += their total (one
 // workgroup; the chunks of the pipelined decode run in order on one stream)
 hipError_t drp_launch_chunk_scan(const uint64_t *cnt, uint64_t *base, uint64_t t0, uint64_t t1,

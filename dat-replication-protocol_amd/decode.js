@@ -312,16 +312,24 @@ Decoder.prototype._replay = function () {
   var flags = res.flags
   var ko = res.ko
   var kl = res.kl
+  var so = res.so
+  var sl = res.sl
+  var vcol = res.vo
+  var vl = res.vl
+  var cc = res.change
+  var cf = res.from
+  var ct = res.to
   var keyHash = res.keyHash
   var text = this._text
   var down = this._down
   var i = this._next
   var t0 = process.hrtime()
   // (no callback can re-enter this loop: _down only resumes a paused replay)
-  while (i < n && this._pending <= 0 && !this.destroyed) {
+  while (i < n && this._pending <= 0) {
     if ((type[i] & TYPE_MASK) !== 1) {
       this._deliverBlob(i)
       i++
+      if (this.destroyed) break
       continue
     }
     // messages.Change.decode result shape: {subset, key, change, from, to, value}
@@ -329,20 +337,21 @@ Decoder.prototype._replay = function () {
     var f = flags[i]
     var k0 = o + ko[i]
     var k1 = k0 + kl[i]
-    var vo = o + res.vo[i]
+    var vo = o + vcol[i]
     var change = {
-      subset: (f & 1) ? buf.toString('utf8', o + res.so[i], o + res.so[i] + res.sl[i]) : '',
+      subset: (f & 1) ? buf.toString('utf8', o + so[i], o + so[i] + sl[i]) : '',
       key: (text !== null && (f & KEY_ASCII)) ? text.substring(k0, k1) : buf.toString('utf8', k0, k1),
-      change: res.change[i],
-      from: res.from[i],
-      to: res.to[i],
-      value: (f & 2) ? buf.slice(vo, vo + res.vl[i]) : null
+      change: cc[i],
+      from: cf[i],
+      to: ct[i],
+      value: (f & 2) ? buf.slice(vo, vo + vl[i]) : null
     }
     if (keyHash) change.keyHash = keyHash[i]
     this.changes++
     this._pending++ // released by the handler's cb (_up, decode.js:89-93)
     this._onchange(change, down)
     i++
+    if (this.destroyed) break
   }
   this._next = i
   var dt = process.hrtime(t0)
