@@ -94,12 +94,17 @@ struct drp_ctx {
   DevBuf scratch, in_stage, out_stage, aux;
   DevBuf dec_cols;  // device columns of the staged host-batch decode (drp_decode_stage)
   double frames_per_byte = 0;  // density of the last staged batch (sizes the next one's columns)
+  int blob_skip = DRP_BLOB_SKIP_AUTO;
+  bool blob_heavy = false;     // the last host batch was mostly blob payload (AUTO: stage in pieces)
+  uint64_t blob_run = 0;       // bytes from a piece's start to the next blob header, last seen
   drp_timing timing = {};
   std::vector<uint64_t> host_tmp;
   // the staged host-batch decode: row 0 is a host-built blob continuation when nf0 == 1; GPU
-  // rows follow, their payload_off relative to batch offset `shift` (where staging started)
+  // rows follow, each piece's payload_off relative to the batch offset where that piece was
+  // staged (pieces: {first GPU row, batch offset}; one piece unless blobs were skipped)
   struct Staged {
-    uint64_t rows = 0, nf0 = 0, shift = 0, cap = 0;
+    uint64_t rows = 0, nf0 = 0, cap = 0;
+    std::vector<std::pair<uint64_t, uint64_t>> pieces;
     uint64_t off0 = 0;
     uint32_t len0 = 0;
     uint8_t ty0 = 0;
@@ -224,6 +229,12 @@ int drp_set_key_post(drp_ctx *c, int mode) {
 int drp_set_strict(drp_ctx *c, int strict) {
   if (!c) return DRP_E_INVAL;
   c->strict = strict ? 1 : 0;
+  return DRP_OK;
+}
+
+int drp_set_blob_skip(drp_ctx *c, int mode) {
+  if (!c || mode < DRP_BLOB_SKIP_OFF || mode > DRP_BLOB_SKIP_ALWAYS) return DRP_E_INVAL;
+  c->blob_skip = mode;
   return DRP_OK;
 }
 
@@ -967,6 +978,137 @@ static int decode_batch_device_out(drp_ctx *c, const uint8_t *bytes, uint64_t n,
 }
 
 
+constexpr uint64_t kPieceMin = 64 << 10;     // bytes of a blob-skipping piece, at least
+constexpr uint64_t kPieceMargin = 64 << 10;  // past the predicted next blob header
+constexpr uint64_t kPiecesMin = 1 << 20;     // batches below this are staged whole
+
+// The staged rows' capacity for m bytes: from the density of the ctx's previous batch (a
+// stream's batches are alike), 1/32 per byte at first.
+static uint64_t stage_cap(const drp_ctx *c, uint64_t m) {
+  const double dens = c->frames_per_byte > 0 ? c->frames_per_byte * 1.25 : 1.0 / 32;
+  return (uint64_t)((double)m * dens) + 1024;
+}
+
+// Pass-through of in-batch blob payloads (drp_set_blob_skip): bytes [pos, n) of a host batch are
+// staged and decoded piece by piece. A piece ends kPieceMargin past where the next blob header
+// is expected (the distance from a piece's start to its blob header, learned); when the
+// decode of a piece ends inside a blob, the next piece starts after that blob, so the blob's
+// remaining payload is never copied. A piece that ends inside a header or a Change frame is
+// resumed at that frame. The rows of all pieces are consecutive, as a whole-batch decode
+// writes them (a blob the batch holds whole loses the PARTIAL mark its piece gave it).
+// DRP_E_RETRY: the capacity guess was short; the caller stages the batch whole.
+static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t pos, drp_carry *carry,
+                        uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail) {
+  hipStream_t st = c->st;
+  auto &S = c->staged;
+  const size_t stage_meta = 256;
+  if (!c->aux.ensure(stage_meta + sizeof(drp_stream_result) + 64)) return DRP_E_NOMEM;
+  uint64_t *soff = c->aux.at<uint64_t>(0);
+  uint64_t *ent = c->aux.at<uint64_t>(16);
+  drp_stream_result *dres = c->aux.at<drp_stream_result>(stage_meta);
+  const uint64_t cap = stage_cap(c, n - pos);
+  if (!c->dec_cols.ensure(carve_bytes(cap))) return DRP_E_NOMEM;
+  carve(c->dec_cols, cap, S.fr, S.co);
+  if (c->key_post != DRP_KEY_POST_HASH) S.co.key_hash = nullptr;
+  S.cap = cap;
+  S.pieces.clear();
+  uint64_t rows = 0, staged = 0, skipped = 0, run = c->blob_run;
+  float h2d_ms = 0;
+  drp_stream_result r;
+  for (;;) {
+    const uint64_t want = std::max(kPieceMin, run + kPieceMargin);
+    const uint64_t pe = std::min(n, pos + want), ps = pos & ~15ull, mp = pe - ps;
+    if (!c->in_stage.ensure(mp + 64)) return DRP_E_NOMEM;
+    const double t0 = now_ms();
+    CHK(hipMemcpyAsync(c->in_stage.p, bytes + ps, mp, hipMemcpyDefault, st));
+    uint64_t hv[3] = {0, mp, pos - ps};
+    CHK(hipMemcpyAsync(soff, hv, 16, hipMemcpyHostToDevice, st));
+    CHK(hipMemcpyAsync(ent, hv + 2, 8, hipMemcpyHostToDevice, st));
+    CHK(hipStreamSynchronize(st));
+    h2d_ms += (float)(now_ms() - t0);
+    staged += mp;
+    drp_frames fr;
+    drp_changes co;
+    fr.payload_off = S.fr.payload_off + rows;
+    fr.payload_len = S.fr.payload_len + rows;
+    fr.type = S.fr.type + rows;
+    co.key_off = S.co.key_off + rows;
+    co.key_len = S.co.key_len + rows;
+    co.subset_off = S.co.subset_off + rows;
+    co.subset_len = S.co.subset_len + rows;
+    co.value_off = S.co.value_off + rows;
+    co.value_len = S.co.value_len + rows;
+    co.change = S.co.change + rows;
+    co.from = S.co.from + rows;
+    co.to = S.co.to + rows;
+    co.flags = S.co.flags + rows;
+    co.key_hash = S.co.key_hash ? S.co.key_hash + rows : nullptr;
+    const int rc = run_decode(c, (const uint8_t *)c->in_stage.p, mp, soff, ent, 1, &fr, &co, cap - rows, dres);
+    if (rc == DRP_E_CAPACITY) return DRP_E_RETRY;
+    if (rc != DRP_OK) return rc;
+    CHK(hipMemcpyAsync(&r, dres, sizeof(r), hipMemcpyDeviceToHost, st));
+    uint64_t boff = 0;  // the cut blob's payload offset in the piece (tail BLOB)
+    CHK(hipStreamSynchronize(st));
+    if (r.tail_kind == DRP_TAIL_BLOB && r.frames) {
+      CHK(hipMemcpyAsync(&boff, fr.payload_off + r.frames - 1, 8, hipMemcpyDeviceToHost, st));
+      CHK(hipStreamSynchronize(st));
+    }
+    S.pieces.emplace_back(rows, ps);
+    const uint64_t bad = (r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0;
+    if (r.err_code || pe == n) {  // the batch's end or its error: this piece's tail is the batch's
+      if (r.err_code) {
+        *err_frame = S.nf0 + rows + r.err_frame;
+        *err_code = r.err_code;
+        *err_detail = r.err_detail;
+      }
+      rows += r.frames + bad;
+      carry->blob_remaining = r.blob_remaining;
+      carry->consumed = r.consumed + ps;
+      carry->tail_kind = r.tail_kind;
+      carry->frame_bytes = r.tail_kind == DRP_TAIL_CHANGE ? r.tail_frame_bytes : 0;
+      break;
+    }
+    rows += r.frames;
+    if (r.tail_kind == DRP_TAIL_BLOB) {
+      const uint64_t bend = pe + r.blob_remaining;  // the blob's end in the batch
+      run = ps + boff - pos;                        // (where this piece's blob header was)
+      if (bend <= n) {  // the batch holds the whole blob: its row is not partial
+        const uint8_t ty = DRP_TYPE_BLOB;
+        CHK(hipMemcpyAsync(S.fr.type + rows - 1, &ty, 1, hipMemcpyHostToDevice, st));
+        CHK(hipStreamSynchronize(st));
+        skipped += bend - pe;
+        pos = bend;
+        if (pos == n) {
+          carry->blob_remaining = 0;
+          carry->consumed = n;
+          carry->tail_kind = DRP_TAIL_NONE;
+          break;
+        }
+      } else {  // the blob continues past the batch: the carry says how far
+        skipped += n - pe;
+        carry->blob_remaining = bend - n;
+        carry->consumed = n;
+        carry->tail_kind = DRP_TAIL_BLOB;
+        break;
+      }
+    } else {
+      // no blob reached: resume at the frame the piece cut (or its end), with a longer piece
+      const uint64_t np = r.tail_kind == DRP_TAIL_NONE ? pe : ps + r.consumed;
+      run = std::max<uint64_t>(want, run) * 2;
+      if (np > pos) pos = np;
+    }
+  }
+  c->blob_run = run;
+  c->timing.h2d_ms = h2d_ms;
+  c->timing.h2d_bytes = staged;
+  c->timing.h2d_skipped = skipped;
+  c->blob_heavy = skipped * 4 >= n;  // (AUTO: keep skipping while it pays)
+  c->frames_per_byte = (double)rows / (double)(n - S.pieces[0].second);
+  S.rows = S.nf0 + rows;
+  *n_frames = S.nf0 + rows - ((*err_code == DRP_ERR_CHANGE || *err_code == DRP_ERR_REQUIRED) ? 1 : 0);
+  return DRP_OK;
+}
+
 // Decode a host batch (bytes [a, n), a = the 16-byte-aligned start of the bytes after a leading
 // blob continuation) into the ctx's device columns. The frame capacity starts at a guess and is
 // grown to the exact count when the first launch overflows it (the count is exact either way).
@@ -974,11 +1116,14 @@ static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry 
                         uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail) {
   hipStream_t st = c->st;
   auto &S = c->staged;
-  S.rows = S.nf0 = S.shift = 0;
+  S.rows = S.nf0 = 0;
+  S.pieces.clear();
   *err_frame = ~0ull;
   *err_code = DRP_ERR_NONE;
   *err_detail = 0;
   carry->frame_bytes = 0;
+  c->timing.h2d_bytes = 0;
+  c->timing.h2d_skipped = 0;
   const uint64_t brem = carry->blob_remaining;
   // A blob continuation (decode.js _id == 2 with _missing > 0 across _write calls) is row 0.
   if (brem) {
@@ -995,11 +1140,26 @@ static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry 
       return DRP_OK;
     }
   }
+  const bool host_in = !is_device_ptr(bytes) || ((uintptr_t)bytes & 15);
+  if (host_in && n - brem >= kPiecesMin &&
+      (c->blob_skip == DRP_BLOB_SKIP_ALWAYS ||
+       (c->blob_skip == DRP_BLOB_SKIP_AUTO && (c->blob_heavy || c->frames_per_byte == 0)))) {
+    // (AUTO: a ctx's first batch probes in pieces too; pieces grow geometrically while no blob
+    // is met, so a batch without blobs costs a few more launches once)
+    const drp_carry in = *carry;
+    const int rc = stage_pieces(c, bytes, n, brem, carry, n_frames, err_frame, err_code, err_detail);
+    if (rc != DRP_E_RETRY) return rc;
+    *carry = in;  // (capacity: staged whole below)
+    *err_frame = ~0ull;
+    *err_code = DRP_ERR_NONE;
+    *err_detail = 0;
+    S.pieces.clear();
+  }
   // the continuation's payload bytes are pass-through: only [a, n) goes to the device
   const uint64_t a = brem & ~15ull, m = n - a;
   const uint8_t *dbytes = bytes + a;
   float h2d_ms = 0;
-  if (!is_device_ptr(bytes) || ((uintptr_t)bytes & 15)) {
+  if (host_in) {
     if (!c->in_stage.ensure(m + 64)) return DRP_E_NOMEM;
     const double t0 = now_ms();
     if (m) {
@@ -1013,14 +1173,12 @@ static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry 
   if (!c->aux.ensure(stage_meta + sizeof(drp_stream_result) + 64)) return DRP_E_NOMEM;
   uint64_t *soff = c->aux.at<uint64_t>(0);
   uint64_t *ent = c->aux.at<uint64_t>(16);
+  uint64_t *bsum = c->aux.at<uint64_t>(24);
   drp_stream_result *dres = c->aux.at<drp_stream_result>(stage_meta);
   uint64_t hv[3] = {0, m, brem - a};
   CHK(hipMemcpyAsync(soff, hv, 16, hipMemcpyHostToDevice, st));
   CHK(hipMemcpyAsync(ent, hv + 2, 8, hipMemcpyHostToDevice, st));
-  // frames: sized from the density of the ctx's previous batch (a stream's batches are alike),
-  // 1/32 per byte at first; grown below to the exact count when the stream is denser
-  const double dens = c->frames_per_byte > 0 ? c->frames_per_byte * 1.25 : 1.0 / 32;
-  uint64_t cap = (uint64_t)((double)m * dens) + 1024;
+  uint64_t cap = stage_cap(c, m);
   drp_stream_result r;
   int rc = DRP_OK;
   for (int attempt = 0; attempt < 2; attempt++) {
@@ -1046,10 +1204,22 @@ static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry 
     cap = need + 1;
   }
   if (rc != DRP_OK) return rc;
+  if (host_in && c->blob_skip == DRP_BLOB_SKIP_AUTO && r.blobs) {
+    // the batch's blob payload bytes: mostly blobs -> the next batches are staged in pieces
+    uint64_t bb = 0;
+    CHK(hipMemsetAsync(bsum, 0, 8, st));
+    CHK(drp_launch_blob_bytes(S.fr.type, S.fr.payload_len, r.frames, bsum, st));
+    CHK(hipMemcpyAsync(&bb, bsum, 8, hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+    c->blob_heavy = bb * 2 >= m;
+  } else if (host_in) {
+    c->blob_heavy = false;
+  }
   c->timing.h2d_ms = h2d_ms;
+  c->timing.h2d_bytes = host_in ? m : 0;
   c->frames_per_byte = m ? (double)r.frames / (double)m : 0.0;
   const uint64_t bad = (r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0;
-  S.shift = a;
+  S.pieces.emplace_back(0, a);
   S.rows = S.nf0 + r.frames + bad;
   *n_frames = S.nf0 + r.frames;
   if (r.err_code) {
@@ -1104,8 +1274,13 @@ static int fetch_staged(drp_ctx *c, const drp_frames *frames, const drp_changes 
       CHK(cp(cols->key_hash, S.co.key_hash, 8));
     }
     CHK(hipStreamSynchronize(st));
-    if (S.shift)
-      for (uint64_t i = 0; i < ng; i++) frames->payload_off[dst + i] += S.shift;
+    // payload offsets relative to each piece's staging offset -> batch offsets
+    for (size_t k = 0; k < S.pieces.size(); k++) {
+      const uint64_t r0 = S.pieces[k].first, r1 = k + 1 < S.pieces.size() ? S.pieces[k + 1].first : ~0ull;
+      const uint64_t sh = S.pieces[k].second, lo = std::max(r0, g0), hi = std::min(r1, g0 + ng);
+      if (sh)
+        for (uint64_t g = lo; g < hi; g++) frames->payload_off[dst + (g - g0)] += sh;
+    }
   }
   c->timing.d2h_ms = (float)(now_ms() - t0);
   return DRP_OK;

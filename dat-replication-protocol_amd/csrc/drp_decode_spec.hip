@@ -2398,18 +2398,19 @@ __global__ __launch_bounds__(SEG_STB) void seg_stitch(DecodeParams P, SegRange R
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const TileGeo G = seg_geo(P, R.s);
   constexpr uint32_t W = SEG_SB * 2 * SEG_CAND;  // words per block
-  auto load = [&](uint64_t blk, uint32_t buf) {
+  // threads [t0, SEG_STB) copy block blk into buffer buf
+  auto load = [&](uint64_t blk, uint32_t buf, uint32_t t0) {
     const uint64_t w0 = blk * W, wn = umin64(R.nseg * 2 * SEG_CAND, w0 + W);
-    for (uint64_t w = w0 + tid; w < wn; w += SEG_STB) (&tab[buf][0][0])[w - w0] = R.cand[w];
+    for (uint64_t w = w0 + (tid - t0); w < wn; w += SEG_STB - t0) (&tab[buf][0][0])[w - w0] = R.cand[w];
   };
   const uint64_t nblk = (R.nseg + SEG_SB - 1) / SEG_SB;
-  load(0, 0);
+  load(0, 0, 0);
   __syncthreads();
   uint64_t e = R.seg_entry[0];
   for (uint64_t blk = 0; blk < nblk; blk++) {
     const uint32_t cur = (uint32_t)(blk & 1);
     if (tid >= WAVE) {
-      if (blk + 1 < nblk) load(blk + 1, cur ^ 1u);  // (the other waves: the next block)
+      if (blk + 1 < nblk) load(blk + 1, cur ^ 1u, WAVE);  // (the other waves: the next block)
     } else {
       for (uint32_t k = 0; k < SEG_SB; k++) {
         const uint64_t seg = blk * SEG_SB + k;
@@ -2469,6 +2470,17 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
     bsync();
   }
   for (uint64_t i = tid; i < tb - ta; i += NT) P.claim[ta + i] = lcl[i];
+}
+
+// payload bytes of the blob rows among rows [0, n) (a host batch's blob share: drp_api.hip
+// stages the next batches in pieces when blobs dominate)
+__global__ __launch_bounds__(256) void blob_bytes_kernel(const uint8_t *type, const uint32_t *plen, uint64_t n,
+                                                         uint64_t *out) {
+  uint64_t acc = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    if ((type[i] & 0x3Fu) == DRP_TYPE_BLOB) acc += plen[i];
+  acc = wave_sum64(acc);
+  if ((threadIdx.x & 63u) == 0 && acc) atomicAdd((unsigned long long *)out, (unsigned long long)acc);
 }
 
 __global__ __launch_bounds__(SCAN_BLK) void chunk_scan_kernel(const uint64_t *cnt, uint64_t *base, uint64_t t0,
@@ -2655,6 +2667,15 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
   if (e != hipSuccess) return e;
   return drp_launch_stream_counts(Q.tile_prefix, nstreams, Q.tile_count, Q.tile_base, Q.tile_nch, Q.tile_nch_base,
                                   Q.scount, st);
+}
+
+extern "C" hipError_t drp_launch_blob_bytes(const uint8_t *type, const uint32_t *plen, uint64_t n, uint64_t *out,
+                                            hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const uint64_t nb = (n + 255) / 256;
+  hipLaunchKernelGGL(spec::blob_bytes_kernel, dim3((uint32_t)(nb < 1024 ? nb : 1024)), dim3(256), 0, st, type, plen, n,
+                     out);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t drp_launch_chunk_scan(const uint64_t *cnt, uint64_t *base, uint64_t t0, uint64_t t1,

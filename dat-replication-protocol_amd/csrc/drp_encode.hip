@@ -236,7 +236,7 @@ __device__ __forceinline__ void wave_copy2(uint8_t *__restrict__ dst, const uint
       if (b0 + 64u * u >= nb) break;
       uint4 w = v[u];
       if (sh) {
-        const uint4 src_hi = lane == 63 ? v[u + 1] : v[u];
+        const uint4 src_hi = lane == 0 ? v[u + 1] : v[u];  // (lane 63 reads lane 0: the next column)
         uint4 hi;
         hi.x = (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)src_hi.x);
         hi.y = (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)src_hi.y);

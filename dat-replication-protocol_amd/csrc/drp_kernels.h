@@ -114,6 +114,7 @@ hipError_t drp_launch_chunk_verify(const drp::DecodeParams *P, uint64_t ntc, hip
 hipError_t drp_launch_chunk_emit(const drp::DecodeParams *P, uint64_t ntc, hipStream_t st);
 // emit_sparse over every tile (before emit_tiles): the tiles verification marked sparse
 hipError_t drp_launch_emit_sparse(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t st);
+hipError_t drp_launch_blob_bytes(const uint8_t *type, const uint32_t *plen, uint64_t n, uint64_t *out, hipStream_t st);
 hipError_t drp_launch_seg_repair(const drp::DecodeParams *P, uint64_t s, uint64_t t0, uint64_t tl, uint64_t *scratch,
                                  hipStream_t st);
 hipError_t drp_launch_spec_verify(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,

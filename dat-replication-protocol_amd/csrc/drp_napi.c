@@ -124,6 +124,7 @@ typedef struct {
   int key_post;   /* also the key hash column (drp_set_key_post; the key flags are always on) */
   void *khash;
   double t_h2d, t_gpu, t_d2h, t_convert; /* ms: batch to HBM, decode kernels, columns back, u64 -> Number */
+  double h2d_bytes, h2d_skipped;         /* bytes staged into HBM / blob payload bytes left in host memory */
 } dec_job;
 
 static void free_cols(dec_job *j) {
@@ -166,6 +167,8 @@ static void dec_run(dec_job *j) {
   drp_timing tm;
   if (drp_last_timing(j->box->c, &tm) == DRP_OK) {
     j->t_h2d = tm.h2d_ms;
+    j->h2d_bytes = (double)tm.h2d_bytes;
+    j->h2d_skipped = (double)tm.h2d_skipped;
     j->t_gpu = tm.total_ms;
     j->t_d2h = tm.d2h_ms;
   }
@@ -214,6 +217,8 @@ static napi_value dec_result(napi_env env, dec_job *j) {
   napi_set_named_property(env, res, "asciiKeys", yes); /* flags carry DRP_F_KEY_ASCII */
   if (napi_create_object(env, &t) == napi_ok) {
     set_num(env, t, "h2d", j->t_h2d);
+    set_num(env, t, "h2dBytes", j->h2d_bytes);
+    set_num(env, t, "h2dSkipped", j->h2d_skipped);
     set_num(env, t, "gpu", j->t_gpu);
     set_num(env, t, "d2h", j->t_d2h);
     set_num(env, t, "convert", j->t_convert);

@@ -123,7 +123,8 @@ function Decoder (opts) {
   this._text = null       // its bytes as one latin1 string (ASCII keys are cut from it)
   this._tooBig = 0        // its carried Change frame was larger than a Buffer can hold
   this._next = 0          // next frame to deliver
-  this.timing = { batches: 0, h2d: 0, gpu: 0, d2h: 0, convert: 0, replay: 0 } // ms, summed
+  // ms, summed (and the bytes staged into HBM / blob payload bytes that stayed in host memory)
+  this.timing = { batches: 0, h2d: 0, gpu: 0, d2h: 0, convert: 0, replay: 0, h2dBytes: 0, h2dSkipped: 0 }
 
   var self = this
   this._up = function () {
@@ -277,6 +278,8 @@ Decoder.prototype._ondecoded = function (err, res, batch) {
     tm.gpu += t.gpu
     tm.d2h += t.d2h
     tm.convert += t.convert
+    tm.h2dBytes += t.h2dBytes || 0
+    tm.h2dSkipped += t.h2dSkipped || 0
   }
   var entry = { res: res, buf: batch, tooBig: tooBig }
   if (this._res) {

@@ -22,7 +22,7 @@ TAIL_NONE, TAIL_HEADER, TAIL_CHANGE, TAIL_BLOB = 0, 1, 2, 3
 EXPORTS = [
     "drp_abi_version", "drp_open", "drp_close", "drp_stream", "drp_synchronize",
     "drp_last_timing", "drp_set_tile", "drp_set_strict", "drp_set_exact", "drp_set_key_post",
-    "drp_decode_scratch_bytes",
+    "drp_set_blob_skip", "drp_decode_scratch_bytes",
     "drp_decode_device", "drp_decode_batch", "drp_decode_stage", "drp_decode_fetch",
     "drp_encode_size", "drp_encode_device",
     "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results", "drp_device",
@@ -30,6 +30,7 @@ EXPORTS = [
     "drp_index_allgather", "drp_index_allgather_multi", "drp_index_allgather_host", "drp_device_count",
 ]
 KEY_POST_OFF, KEY_POST_HASH, KEY_POST_FLAGS = 0, 1, 2
+BLOB_SKIP_OFF, BLOB_SKIP_AUTO, BLOB_SKIP_ALWAYS = 0, 1, 2
 DRP_E_COMM = -7
 COMM_ID_BYTES = 128
 
@@ -69,7 +70,8 @@ class StreamStats(C.Structure):
 class Timing(C.Structure):
     _fields_ = [("decode_ms", C.c_float), ("finalize_ms", C.c_float), ("total_ms", C.c_float),
                 ("strict_reruns", U32), ("spec_repairs", U32), ("exact_retries", U32), ("verify_relisted", U32),
-                ("seg_repairs", U32), ("reserved", U32), ("h2d_ms", C.c_float), ("d2h_ms", C.c_float)]
+                ("seg_repairs", U32), ("reserved", U32), ("h2d_ms", C.c_float), ("d2h_ms", C.c_float),
+                ("h2d_bytes", U64), ("h2d_skipped", U64)]
 
 
 _lib = None
@@ -94,6 +96,7 @@ def lib():
         L.drp_set_strict.argtypes = [P, C.c_int]
         L.drp_set_exact.argtypes = [P, C.c_int]
         L.drp_set_key_post.argtypes = [P, C.c_int]
+        L.drp_set_blob_skip.argtypes = [P, C.c_int]
         L.drp_decode_scratch_bytes.argtypes = [P, U64, U64]
         L.drp_decode_scratch_bytes.restype = U64
         L.drp_decode_device.argtypes = [P, P, U64, P, P, U64, C.POINTER(Frames),
@@ -122,7 +125,8 @@ def lib():
         L.drp_index_allgather_host.argtypes = [C.POINTER(P), C.POINTER(P), C.c_int, C.POINTER(P), U64, P, P]
         L.drp_device_count.argtypes = [C.POINTER(C.c_int)]
         for f in ["drp_open", "drp_synchronize", "drp_last_timing", "drp_set_tile",
-                  "drp_set_strict", "drp_set_exact", "drp_set_key_post", "drp_decode_device", "drp_decode_batch",
+                  "drp_set_strict", "drp_set_exact", "drp_set_key_post", "drp_set_blob_skip", "drp_decode_device",
+                  "drp_decode_batch",
                   "drp_decode_stage", "drp_decode_fetch", "drp_encode_size",
                   "drp_encode_device", "drp_encode_batch", "drp_index_scan",
                   "drp_stream_stats_from_results", "drp_device", "drp_comm_id", "drp_comm_init_rank",
@@ -224,6 +228,11 @@ class Ctx:
     def set_exact(self, on):
         """Force the exact decode kernel (else: speculate-and-verify with exact fallback)."""
         _chk("drp_set_exact", self.L.drp_set_exact(self.h, 1 if on else 0))
+
+    def set_blob_skip(self, mode):
+        """Host batches: BLOB_SKIP_AUTO (default), _ALWAYS (every batch in blob-skipping
+        pieces) or _OFF (every batch staged whole); results are identical."""
+        _chk("drp_set_blob_skip", self.L.drp_set_blob_skip(self.h, mode))
 
     def set_tile(self, tile):
         _chk("drp_set_tile", self.L.drp_set_tile(self.h, tile))

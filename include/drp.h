@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DRP_ABI_VERSION 3
+#define DRP_ABI_VERSION 4
 
 /* ---- return codes -------------------------------------------------------- */
 #define DRP_OK 0
@@ -159,6 +159,8 @@ typedef struct drp_timing {
   /* host-batch calls (drp_decode_stage / drp_decode_fetch / drp_decode_batch), wall clock: */
   float h2d_ms;   /* staging the batch into HBM */
   float d2h_ms;   /* copying the columns back (drp_decode_fetch) */
+  uint64_t h2d_bytes;   /* bytes of the last host batch staged into HBM */
+  uint64_t h2d_skipped; /* its blob payload bytes never staged (pass-through, drp_set_blob_skip) */
 } drp_timing;
 
 /* ---- context ------------------------------------------------------------- */
@@ -190,6 +192,17 @@ int drp_set_exact(drp_ctx *ctx, int exact);
 int drp_set_key_post(drp_ctx *ctx, int mode);
 /* Look-back composes exact inclusive exits only, never the per-tile maps agg_t. Test hook. */
 int drp_set_strict(drp_ctx *ctx, int strict);
+/* Host batches (drp_decode_stage / drp_decode_batch): blob payloads are pass-through ranges into
+ * the caller's buffer, so their bytes need not reach HBM (decode.js:179-202 only slices them).
+ * DRP_BLOB_SKIP_AUTO (default): a ctx whose last batch was mostly blob payload stages the next
+ * batches in pieces, each ending a little past the next blob header (sized from the runs between
+ * blobs seen so far); a piece that ends inside a blob resumes after it, skipping its payload.
+ * DRP_BLOB_SKIP_ALWAYS: every host batch in pieces; DRP_BLOB_SKIP_OFF: every batch staged whole.
+ * Results are identical in every mode; drp_timing.h2d_bytes / h2d_skipped report the bytes. */
+#define DRP_BLOB_SKIP_OFF 0
+#define DRP_BLOB_SKIP_AUTO 1
+#define DRP_BLOB_SKIP_ALWAYS 2
+int drp_set_blob_skip(drp_ctx *ctx, int mode);
 /* Device scratch bytes needed to decode `n` bytes split into `nstreams` streams. */
 uint64_t drp_decode_scratch_bytes(drp_ctx *ctx, uint64_t n, uint64_t nstreams);
 

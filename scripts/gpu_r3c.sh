@@ -8,7 +8,7 @@ TAG=r3c
 mkdir -p gpurun_out
 DRP_TRACE=1 timeout -k 10 300 python -u scripts/probe_dense.py > gpurun_out/probe_dense.log 2> gpurun_out/probe_dense.err
 echo probe done
-bash scripts/gpu_session.sh $TAG "enc_old" ""
+bash scripts/gpu_session.sh $TAG "enc_old nt64" ""
 DRP_PIPE_CHUNK=64 timeout -k 10 400 python -u -m pytest -x -v --timeout 150 --timeout-method thread -m gpu \
   tests/test_gpu_decode.py tests/test_gpu_ref_fixtures.py tests/test_gpu_cascade.py tests/test_gpu_emit_split.py \
   tests/test_gpu_adversarial.py > gpurun_out/pipe_tests_$TAG.log 2>&1

@@ -6,6 +6,7 @@
 //   mode "digest": events carry sha256 of keys/values/blob data instead of hex
 //   mode "keyhash": decode({keyHash: true}); change events also carry keyHash (decimal)
 //   mode "ticks": one write per event-loop turn (synchronous acks)
+//   mode "h2d": digest events, then one {t: 'timing'} record with the decoder's byte counters
 // DRP_MAX_BATCH in the environment sets the decoder's batch threshold
 'use strict'
 var fs = require('fs')
@@ -22,7 +23,7 @@ var mode = process.argv[4] || ''
 var nth = Number(process.argv[5] || 0)
 var asyncAck = mode === 'async' || mode === 'destroy'
 var ticks = mode === 'ticks'
-var digest = mode === 'digest'
+var digest = mode === 'digest' || mode === 'h2d'
 function enc (b) {
   return digest ? crypto.createHash('sha256').update(b).digest('hex').slice(0, 16) : b.toString('hex')
 }
@@ -52,7 +53,11 @@ d.blob(function (b, cb) {
 })
 d.on('error', function (e) { out.push({ t: 'error', message: e.message }); done() })
 d.on('close', function () { out.push({ t: 'close' }) })
-d.on('finish', function () { out.push({ t: 'finish', changes: d.changes, blobs: d.blobs, bytes: d.bytes }); done() })
+d.on('finish', function () {
+  out.push({ t: 'finish', changes: d.changes, blobs: d.blobs, bytes: d.bytes })
+  if (mode === 'h2d') out.push({ t: 'timing', h2dBytes: d.timing.h2dBytes, h2dSkipped: d.timing.h2dSkipped })
+  done()
+})
 var printed = false
 function done () {
   if (printed) return

@@ -117,9 +117,9 @@ def test_cascade_512mb_under_50ms(ctx):
 def test_dense_cascade_1_7gb(ctx):
     """A 1.7 GB two-framing stream of dense small frames (200 B blobs whose payloads hold a
     denser shadow chain, tests/_streams.shadow_stream_np): the prediction follows the shadow in
-    every tile. The segmented repair would walk ~16K frames per chain per segment (~13 ms); the
-    decode must see the range is dense and take the exact kernel, bit-exact with the generator's
-    frame table, and finish within the bound printed and asserted here."""
+    every tile. The segmented repair (up to 8192 short segments, so a candidate chain walks only
+    its segment) must settle it bit-exact with the generator's frame table, within the bound
+    printed and asserted here."""
     import ctypes as C
 
     import torch

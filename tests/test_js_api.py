@@ -31,7 +31,7 @@ def test_package_loads_without_gpu_use():
                os.path.join(ROOT, "dat-replication-protocol_amd", "lib", "drp.node")))
     out = json.loads(subprocess.check_output([NODE, "-e", code], text=True, timeout=60))
     assert out == ["function", "function", ["abiVersion", "decode", "decodeSync", "deviceCount", "encode",
-                                            "indexAllgather", "open"], 3]
+                                            "indexAllgather", "open"], 4]
 
 
 def _enc(b, digest):
@@ -231,6 +231,25 @@ def test_c3_blobs_through_the_package():
         got = [e for e in run_js(wire, sizes, mode) if e["t"] != "close"]
         assert got[:-1] == exp
         assert got[-1] == {"t": "finish", "changes": r["changes"], "blobs": r["blobs"], "bytes": len(wire)}
+
+
+@pytest.mark.gpu
+@needs_node
+def test_c3_blob_payloads_stay_in_host_memory():
+    """SURVEY §8 f2 through the Node path: a C3-shaped stream (100 units of 1000 C2 frames + a
+    1 MiB blob, ~113 MB) in 1 MiB writes; the addon stages the decoder's batches in pieces that
+    skip blob payloads, so at most 25% of the wire is copied into HBM, and every event still
+    equals the oracle's."""
+    wire = S.c3_stream(random.Random(12), 100, frames_per_unit=1000)
+    r, exp = oracle_events(wire, digest=True)
+    out = [e for e in run_js(wire, str(1 << 20), "h2d") if e["t"] != "close"]
+    tm = out.pop()
+    assert tm["t"] == "timing"
+    assert out[:-1] == exp
+    assert out[-1] == {"t": "finish", "changes": r["changes"], "blobs": r["blobs"], "bytes": len(wire)}
+    print(f"staged {tm['h2dBytes']} B of {len(wire)} ({tm['h2dBytes'] / len(wire):.1%}), "
+          f"skipped {tm['h2dSkipped']} B")
+    assert tm["h2dBytes"] <= len(wire) // 4, tm
 
 
 @pytest.mark.gpu
