@@ -2442,10 +2442,16 @@ __global__ __launch_bounds__(SEG_STB) void seg_stitch(DecodeParams P, SegRange R
   if (tid == 0) R.seg_entry[R.nseg] = e;
 }
 
+// Per tile the chain also gives exact per-thread records (entry byte, frames, change frames), so
+// the verify pass after the repair proves such a tile from its records alone (verify_lite) instead
+// of re-walking it; a tile where the chain ends (an error or a frame cut by the stream end) keeps
+// its records and is re-walked by verify_counts.
 __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint64_t lcl[SEG_GMAX];
   __shared__ uint64_t nxt;
+  __shared__ uint8_t re[NT], rn[NT], rc[NT];
+  __shared__ uint32_t rok;
   const uint32_t tid = threadIdx.x;
   const uint64_t seg = blockIdx.x;
   TileGeo G = seg_geo(P, R.s);
@@ -2459,15 +2465,44 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
     if (q == NONE) break;
     const uint64_t u = ta + (q - seg_tile_a(G, ta)) / TILE;
     G.A = seg_tile_a(G, u);
-    stage(P, G, buf);
+    re[tid] = 0xFF;
+    rn[tid] = 0;
+    rc[tid] = 0;
+    stage(P, G, buf);  // (its barrier also orders the record resets)
     if (tid == 0) {
       const Img m{buf, P.bytes, G.A, G.se};
-      p = seg_advance(m, q, umin64(G.A + TILE, send));
+      const uint64_t lim = umin64(G.A + TILE, send);
+      uint32_t ok = 1;
+      p = q;
+      // seg_advance, keeping the records of the chain's frames in this tile
+      while (is_pos(p) && p < lim && p < m.se) {
+        const Hdr h = m.at(p);
+        if (h.kind != H_VALID) {
+          p = term_of(h, p);
+          ok = 0;
+          break;
+        }
+        const uint32_t o = (uint32_t)(p - G.A), th = o / SEGB;
+        if (re[th] == 0xFF) re[th] = (uint8_t)(o % SEGB);
+        if (h.id != 0) {
+          rn[th]++;
+          if (h.id == 1) rc[th]++;
+        }
+        p = h.succ;
+      }
       // the tile's claim: the first chain position past it, or where the chain ends in it
       lcl[u - ta] = (p & MARK_TERM) ? (p & ~M_ERR) : p;
+      rok = ok && lim == G.A + TILE;  // (a segment end inside the tile: its next segment walks the rest)
       nxt = (is_pos(p) && p < send) ? p : NONE;
     }
     bsync();
+    if (rok) {
+      const uint64_t ix = u * NT + tid;
+      P.ent[ix] = re[tid];
+      P.ent_n[ix] = rn[tid];
+      P.ent_c[ix] = rc[tid];
+    }
+    bsync();  // (the records are read before the next tile resets them)
   }
   for (uint64_t i = tid; i < tb - ta; i += NT) P.claim[ta + i] = lcl[i];
 }

@@ -17,3 +17,6 @@ for ch in 8192 32768 131072; do
   DRP_PIPE_CHUNK=$ch timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/pipe_c2_$ch.log 2>&1
   echo "pipe $ch done"
 done
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_dense -o run -- \
+  python3 -u $GRAFT_REPO_ROOT/scripts/probe_dense.py > $GRAFT_REPO_ROOT/gpurun_out/probe_dense_prof.log 2>&1)
+echo dense prof done
