@@ -8,9 +8,14 @@ export TMPDIR=/tmp
 TAG=${1:-run}
 AB=${2:-}
 mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread \
+# test failures (rc 1) do not stop the session; a timeout, abort or crash (any other rc) does
+set +e
+timeout -k 10 700 python -u -m pytest tests -m gpu --maxfail=8 -v -rA --timeout 150 --timeout-method thread \
   > gpurun_out/gpu_tests_$TAG.log 2>&1
-echo tests done
+rc=$?
+set -e
+echo "tests done rc=$rc"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
 echo smoke done
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_$TAG.log 2>&1
