@@ -96,7 +96,7 @@ struct drp_ctx {
   double frames_per_byte = 0;  // density of the last staged batch (sizes the next one's columns)
   int blob_skip = DRP_BLOB_SKIP_AUTO;
   bool blob_heavy = false;     // the last host batch was mostly blob payload (AUTO: stage in pieces)
-  uint64_t blob_run = 0;       // bytes from a piece's start to the next blob header, last seen
+  uint64_t blob_run = 0;       // bytes from a piece's start to its blob's payload, last seen
   drp_timing timing = {};
   std::vector<uint64_t> host_tmp;
   // the staged host-batch decode: row 0 is a host-built blob continuation when nf0 == 1; GPU
@@ -1012,11 +1012,13 @@ static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t p
   if (c->key_post != DRP_KEY_POST_HASH) S.co.key_hash = nullptr;
   S.cap = cap;
   S.pieces.clear();
-  uint64_t rows = 0, staged = 0, skipped = 0, run = c->blob_run;
+  uint64_t rows = 0, staged = 0, skipped = 0;
+  // the next piece: kPieceMargin past where the last blob seen suggests the next blob header is;
+  // doubled within this batch after each piece that met no blob
+  uint64_t want = std::max(kPieceMin, c->blob_run + kPieceMargin);
   float h2d_ms = 0;
   drp_stream_result r;
   for (;;) {
-    const uint64_t want = std::max(kPieceMin, run + kPieceMargin);
     const uint64_t pe = std::min(n, pos + want), ps = pos & ~15ull, mp = pe - ps;
     if (!c->in_stage.ensure(mp + 64)) return DRP_E_NOMEM;
     const double t0 = now_ms();
@@ -1063,7 +1065,7 @@ static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t p
       }
       rows += r.frames + bad;
       carry->blob_remaining = r.blob_remaining;
-      carry->consumed = r.consumed + ps;
+      carry->consumed = r.err_code ? n : r.consumed + ps;  // (an error ends the stream: nothing carried)
       carry->tail_kind = r.tail_kind;
       carry->frame_bytes = r.tail_kind == DRP_TAIL_CHANGE ? r.tail_frame_bytes : 0;
       break;
@@ -1071,7 +1073,8 @@ static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t p
     rows += r.frames;
     if (r.tail_kind == DRP_TAIL_BLOB) {
       const uint64_t bend = pe + r.blob_remaining;  // the blob's end in the batch
-      run = ps + boff - pos;                        // (where this piece's blob header was)
+      c->blob_run = ps + boff - pos;                // (where this piece's blob payload began)
+      want = std::max(kPieceMin, c->blob_run + kPieceMargin);
       if (bend <= n) {  // the batch holds the whole blob: its row is not partial
         const uint8_t ty = DRP_TYPE_BLOB;
         CHK(hipMemcpyAsync(S.fr.type + rows - 1, &ty, 1, hipMemcpyHostToDevice, st));
@@ -1094,11 +1097,10 @@ static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t p
     } else {
       // no blob reached: resume at the frame the piece cut (or its end), with a longer piece
       const uint64_t np = r.tail_kind == DRP_TAIL_NONE ? pe : ps + r.consumed;
-      run = std::max<uint64_t>(want, run) * 2;
+      want *= 2;
       if (np > pos) pos = np;
     }
   }
-  c->blob_run = run;
   c->timing.h2d_ms = h2d_ms;
   c->timing.h2d_bytes = staged;
   c->timing.h2d_skipped = skipped;

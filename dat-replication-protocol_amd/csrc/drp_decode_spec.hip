@@ -881,7 +881,7 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
 // bytes are not read). Random bytes essentially never pass; a real frame in another shape is left
 // undecided as before. Prediction only: verification is exact.
 #ifndef DRP_CHANGE_FILLS
-#define DRP_CHANGE_FILLS 1
+#define DRP_CHANGE_FILLS 1  // 1: nodes of the tile (not its halo); 2: every node; 0: none (A/B)
 #endif
 __device__ __forceinline__ bool change_fills(const uint32_t *w32, uint32_t po, uint32_t pl) {
   uint32_t off = 0, found = 0;
@@ -1198,7 +1198,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
       } else if (succ >= (DRP_HALO_NODES ? IMG - 16 : TILE)) {
         c = NX_FAR;   // past the listed positions: undecided (a restart that needs it checks in HBM),
         a = 2;        // unless it is a Change frame whose fields fill it exactly (strong by structure)
-        if (DRP_CHANGE_FILLS && id == 1u && change_fills(w32, o + k + 1u, L - 1u)) a = 1;
+        if (DRP_CHANGE_FILLS && id == 1u && (DRP_CHANGE_FILLS == 2 || o < TILE) && change_fills(w32, o + k + 1u, L - 1u))
+          a = 1;
       } else {
         const uint32_t th = succ / SEGB, b = succ % SEGB;
         const uint64_t lw = lmw[th];

@@ -193,7 +193,7 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
 }
 
 #ifndef DRP_ENC_COPY2
-#define DRP_ENC_COPY2 1  // 0: wave_copy (one source block pair per lane per step)
+#define DRP_ENC_COPY2 0  // 1: wave_copy2 (measured slower on C5: 4.23 vs 2.92 ms)
 #endif
 #ifndef DRP_ENC_BATCH
 #define DRP_ENC_BATCH 8  // 16-byte blocks per lane loaded before any is stored (wave_copy2)

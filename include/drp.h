@@ -85,7 +85,8 @@ typedef struct drp_frames {
   uint8_t *type;         /* DRP_TYPE_CHANGE / DRP_TYPE_BLOB (| DRP_FRAME_PARTIAL) */
 } drp_frames;
 
-/* Change columns, indexed by frame index (entries of blob frames are left untouched).
+/* Change columns, indexed by frame index (the entries of blob frames are unspecified: the device
+ * leaves them untouched; a host fetch copies whatever the device columns held there).
  * Offsets are relative to payload_off of the same frame. */
 typedef struct drp_changes {
   uint32_t *key_off, *key_len;

@@ -1,0 +1,65 @@
+"""Probe: why C5 decodes need repair passes. Encodes the bench's C5 rows on the device, decodes
+the wire with DRP_STATS=1 (libdrp prints the first missed tiles: t, entry, claim, exact exit) and
+dumps the bytes of those tiles (tile - 1 .. tile + 1) with the true frame starts in them to
+gpurun_out/c5_miss.json for offline study. Usage: DRP_STATS=1 python scripts/probe_c5_miss.py"""
+import ctypes as C
+import json
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    if os.environ.get("DRP_STATS") != "1":
+        # the stats line goes to stderr of a child that has the variable from the start
+        env = dict(os.environ, DRP_STATS="1")
+        r = subprocess.run([sys.executable, "-u", __file__], env=env, capture_output=True, text=True, timeout=300)
+        sys.stdout.write(r.stdout)
+        sys.stderr.write(r.stderr[-4000:])
+        misses = re.findall(r"t=(\d+) e=(0x[0-9a-f]+) claim=(0x[0-9a-f]+) exit=(0x[0-9a-f]+)", r.stderr)
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, "gpurun_out", "c5_miss_stats.txt"), "w") as f:
+            f.write(r.stderr)
+        print("misses:", misses[:5])
+        sys.exit(r.returncode)
+    import torch
+    import bench
+    import drp_amd
+    dev = torch.device("cuda", 0)
+    n = 1_000_000
+    cols, heap, frame = bench.c5_on_device(n, seed=55, dev=dev)
+    W = int(frame.sum())
+    out = torch.empty(W + 64, dtype=torch.uint8, device=dev)
+    foff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ctx = drp_amd.Ctx(0)
+    ctx.encode_device(cols, heap, n, foff, out, W + 64)
+    wire = out[:W]
+    so = torch.tensor([0, W], dtype=torch.int64, device=dev)
+    outs = bench.alloc_outputs(n + 64, dev)
+    res = torch.zeros(C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+    ctx.decode_device(wire, so, None, outs, n + 64, res)
+    torch.cuda.synchronize()
+    t = ctx.timing()
+    print(f"repairs {t.spec_repairs} seg {t.seg_repairs} relisted {t.verify_relisted} decode_ms {t.decode_ms:.3f}",
+          flush=True)
+    # dump the bytes of the tiles the stats name (printed by libdrp on stderr of this process)
+    fo = foff.cpu().numpy()
+    dump = {"tile": 8192, "frame_off_sample": []}
+    sys.stderr.flush()
+    for tt in [int(x) for x in os.environ.get("C5_TILES", "").split(",") if x]:
+        a, b = max(0, (tt - 1) * 8192), min(W, (tt + 2) * 8192 + 512)
+        import numpy as np
+        starts = fo[(fo >= a) & (fo < b)].tolist()
+        dump["frame_off_sample"].append({"tile": tt, "a": a, "hex": wire[a:b].cpu().numpy().tobytes().hex(),
+                                         "frame_starts": starts})
+    with open(os.path.join(ROOT, "gpurun_out", "c5_miss.json"), "w") as f:
+        json.dump(dump, f)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

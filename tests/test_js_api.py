@@ -314,7 +314,8 @@ function done () {
         json.dump([w.hex() for w in wires], f)
         path = f.name
     try:
-        out = json.loads(subprocess.check_output([NODE, "-e", code, path], text=True, timeout=120))
+        # (the last line: RCCL may print its version banner first when NCCL_DEBUG is set)
+        out = json.loads(subprocess.check_output([NODE, "-e", code, path], text=True, timeout=120).strip().splitlines()[-1])
     finally:
         os.unlink(path)
     frames = []
