@@ -81,10 +81,7 @@ double now_ms() {
 struct drp_ctx {
   int device = 0;
   hipStream_t st = nullptr;
-  hipStream_t st2 = nullptr;  // the pipelined decode's second stream (verification + emission)
   hipEvent_t ev[4] = {};
-  hipEvent_t pev[4] = {};     // pipelined decode: claims done / emission done (ring of two each)
-  uint64_t pipe_chunk = 0;    // tiles per chunk of the pipelined decode (0: not pipelined)
   uint32_t B = 128;
   int strict = 0;
   int exact = 0;  // 1: always the exact kernel (decode_tiles), never the speculative one
@@ -154,13 +151,6 @@ int drp_open(int device, drp_ctx **out) {
     return DRP_E_HIP;
   }
   for (auto &e : c->ev) (void)hipEventCreate(&e);
-  if (hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking) != hipSuccess) {
-    (void)hipStreamDestroy(c->st);
-    delete c;
-    return DRP_E_HIP;
-  }
-  for (auto &e : c->pev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-  if (const char *p = getenv("DRP_PIPE_CHUNK")) c->pipe_chunk = strtoull(p, nullptr, 10);
   if (const char *t = getenv("DRP_TILE")) {
     uint32_t tb = (uint32_t)atoi(t);
     if (tb == 4096 || tb == 8192) c->B = tb / 64;
@@ -183,9 +173,6 @@ void drp_close(drp_ctx *c) {
   c->out_stage.release();
   c->aux.release();
   for (auto &e : c->ev) hipEventDestroy(e);
-  for (auto &e : c->pev) (void)hipEventDestroy(e);
-  (void)hipStreamSynchronize(c->st2);
-  (void)hipStreamDestroy(c->st2);
   hipStreamDestroy(c->st);
   delete c;
 }
@@ -444,11 +431,11 @@ int run_decode_exact(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const ui
 // when a prediction failed (or a bounded wait expired): the caller then runs the exact kernel.
 constexpr int kSpecRepairPasses = 16;
 constexpr int kChain = 3;  // dirty-list repair passes queued per host read
-constexpr int kSegRepairAfter = 3;  // verify passes before the segmented repair of the streams still missing  // one verify pass each (0.7 ms on C5), vs ~1.5 s for an exact re-run there
+constexpr int kSegRepairAfter = 3;  // verify passes before the segmented repair of the streams still missing
 
 int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
                     const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
-                    uint64_t cap, drp_stream_result *res, bool skip_head = false) {
+                    uint64_t cap, drp_stream_result *res) {
   if (((uintptr_t)bytes & 15) != 0) return DRP_E_INVAL;
   const uint32_t B = drp_spec_tile_bytes() / 64;
   const DecLayout L = dec_layout(B, nbytes, ns);
@@ -463,20 +450,12 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   uint32_t *tstream = c->scratch.at<uint32_t>(L.tstream);
   uint64_t *sgscan = c->scratch.at<uint64_t>(L.scan_tmp);
   hipStream_t st = c->st;
-  const float pipe_ms = skip_head ? c->timing.decode_ms : 0.0f;
   CHK(hipEventRecord(c->ev[0], st));
-  if (!skip_head) {
-    CHK(hipMemsetAsync(rec, 0, 2 * NT * 8, st));  // claim, incl_e
-    CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
-    CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
-    CHK(hipMemsetAsync(ctrl, 0, 64, st));
-    CHK(drp_launch_tile_prefix(B, stream_off, ns, tile_prefix, st));
-  } else {
-    // the pipelined decode's claims stand (some repaired): its emission is redone from scratch
-    CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
-    CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
-    CHK(hipMemsetAsync(ctrl + 1, 0, 60, st));
-  }
+  CHK(hipMemsetAsync(rec, 0, 2 * NT * 8, st));  // claim, incl_e
+  CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
+  CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
+  CHK(hipMemsetAsync(ctrl, 0, 64, st));
+  CHK(drp_launch_tile_prefix(B, stream_off, ns, tile_prefix, st));
   DecodeParams P;
   memset(&P, 0, sizeof(P));
   P.bytes = bytes;
@@ -547,15 +526,9 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   // few passes (e.g. a protocol error on the exact chain) does the caller run the exact kernel.
   uint32_t h[16];
   const uint32_t miss = drp_spec_miss_bit();
-  if (!skip_head) {
-    CHK(drp_launch_spec_head(&P, NT, ns, tstream, st));
-    CHK(hipMemcpyAsync(h, ctrl, 64, hipMemcpyDeviceToHost, st));
-    CHK(hipStreamSynchronize(st));
-  } else {
-    memset(h, 0, sizeof h);
-    h[1] = miss;  // the pipelined decode missed: verify every tile again (a full pass) first
-    h[10] = 1;
-  }
+  CHK(drp_launch_spec_head(&P, NT, ns, tstream, st));
+  CHK(hipMemcpyAsync(h, ctrl, 64, hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
   const uint32_t relisted = h[5];
   int pass = 0;
   bool seg_done = false;
@@ -564,7 +537,9 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     uint32_t k = 0;
     bool full = h[10] != 0 || h[8] > P.dlist_cap;
     for (; pass < kSpecRepairPasses && (h[1] & miss); pass++) {
-      if (pass >= kSegRepairAfter && !seg_done) {
+      // a dirty list this long after a pass is a cascade already (C5's first list is ~300 tiles)
+      const uint64_t seg_early = std::max<uint64_t>(1024, NT / 256);
+      if ((pass >= kSegRepairAfter || h[8 + k] > seg_early) && !seg_done) {
         // the misses keep coming one tile per pass (wrong predictions that agree with each
         // other): recompute the claims of each stream from its first missed tile by exact
         // chain walks (drp_decode_spec.hip, segmented repair), then verify them
@@ -638,9 +613,9 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   if (retry) h[1] |= miss;
   float ms = 0;
   hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
-  c->timing.decode_ms = ms + pipe_ms;
+  c->timing.decode_ms = ms;
   hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
-  c->timing.total_ms = ms + pipe_ms;
+  c->timing.total_ms = ms;
   c->timing.finalize_ms = 0;
   c->timing.strict_reruns = 0;
   c->timing.exact_retries = 0;
@@ -666,152 +641,13 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   return DRP_OK;
 }
 
-// Pipelined decode of one long stream (DRP_PIPE_CHUNK tiles per chunk): the claims of chunk c + 1
-// run on the ctx's stream while chunk c is verified, scanned (its output base carried from the
-// chunks before it) and emitted on a second stream, so the instruction-bound claims kernel shares
-// the GPU with the memory-bound emission and emission re-reads a chunk the claims just read. No
-// host synchronisation per chunk: the prediction check is read once at the end, and a miss
-// anywhere hands the call to run_decode_spec's repair passes (skip_head: the claims stand) and its
-// full emission, so the results are the same whatever the prediction does.
-int run_decode_pipe(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
-                    const uint64_t *entry, const drp_frames *fr, const drp_changes *co, uint64_t cap,
-                    drp_stream_result *res) {
-  if (((uintptr_t)bytes & 15) != 0) return DRP_E_INVAL;
-  const uint64_t ns = 1;
-  const uint32_t B = drp_spec_tile_bytes() / 64;
-  const DecLayout L = dec_layout(B, nbytes, ns);
-  if (!c->scratch.ensure(L.total + 64)) return DRP_E_NOMEM;
-  const uint64_t NT = L.ntiles_max, CT = c->pipe_chunk;
-  uint64_t *tile_prefix = c->scratch.at<uint64_t>(L.tile_prefix);
-  uint64_t *rec = c->scratch.at<uint64_t>(L.rec);
-  uint64_t *tiles = c->scratch.at<uint64_t>(L.tiles);
-  uint64_t *perr = c->scratch.at<uint64_t>(L.perr);
-  uint64_t *scount = c->scratch.at<uint64_t>(L.scount);
-  uint32_t *ctrl = c->scratch.at<uint32_t>(L.ctrl);
-  uint64_t *carry = c->scratch.at<uint64_t>(L.total);  // (the 64 bytes past the layout)
-  uint32_t *wfrom = reinterpret_cast<uint32_t *>(carry + 1);
-  hipStream_t A = c->st, Bs = c->st2;
-  CHK(hipEventRecord(c->ev[0], A));
-  CHK(hipMemsetAsync(rec, 0, 2 * NT * 8, A));  // claim, incl_e
-  CHK(hipMemsetAsync(perr, 0xFF, ns * 8, A));
-  CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, A));
-  CHK(hipMemsetAsync(ctrl, 0, 64, A));
-  CHK(hipMemsetAsync(carry, 0, 16, A));
-  CHK(drp_launch_tile_prefix(B, stream_off, ns, tile_prefix, A));
-  DecodeParams P;
-  memset(&P, 0, sizeof(P));
-  P.bytes = bytes;
-  P.nbytes = nbytes;
-  P.stream_off = stream_off;
-  P.entry = entry;
-  P.nstreams = ns;
-  P.tile_prefix = tile_prefix;
-  P.payload_off = fr->payload_off;
-  P.payload_len = fr->payload_len;
-  P.type = fr->type;
-  P.key_off = co->key_off;
-  P.key_len = co->key_len;
-  P.subset_off = co->subset_off;
-  P.subset_len = co->subset_len;
-  P.value_off = co->value_off;
-  P.value_len = co->value_len;
-  P.change = co->change;
-  P.from = co->from;
-  P.to = co->to;
-  P.flags = co->flags;
-  P.cap = cap;
-  P.claim = rec;
-  P.incl_e = rec + NT;
-  P.work = reinterpret_cast<uint32_t *>(rec + 2 * NT);
-  P.work_n = ctrl + 2;
-  P.work_from = wfrom;
-  P.tile_exit = tiles;
-  P.tile_base = tiles + NT;
-  P.tile_count = tiles + 2 * NT;
-  P.payload_err = perr;
-  P.scount = scount;
-  P.counter = ctrl;
-  P.overflow = ctrl + 1;
-  P.ent = c->scratch.at<uint8_t>(L.ent);
-  P.ent_n = P.ent + NT * 128;
-  P.ent_c = P.ent_n + NT * 128;
-  P.tile_nch = tiles + 3 * NT;
-  P.tile_nch_base = tiles + 4 * NT;
-  P.vlist = reinterpret_cast<uint32_t *>(rec + 2 * NT) + NT;
-  P.vlist_n = ctrl + 5;
-  P.tile_k = c->scratch.at<uint8_t>(L.tk);
-  P.tile_sparse = c->scratch.at<uint8_t>(L.tsp);
-  P.first_miss = c->scratch.at<uint64_t>(L.fmiss);
-  P.pass_id = 1;
-  CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, A));
-  CHK(hipEventRecord(c->ev[1], A));
-  CHK(hipEventRecord(c->pev[3], A));
-  CHK(hipStreamWaitEvent(Bs, c->pev[3], 0));  // (the memsets and tile_prefix, for the second stream)
-  const uint64_t nchunks = (NT + CT - 1) / CT;
-  for (uint64_t k = 0; k < nchunks; k++) {
-    DecodeParams Q = P;
-    Q.tile0 = k * CT;
-    const uint64_t ntc = std::min(CT, NT - Q.tile0);
-    // claims of chunk k, at most two chunks ahead of the emission
-    if (k >= 2) CHK(hipStreamWaitEvent(A, c->pev[2 + (k & 1)], 0));
-    CHK(hipMemcpyAsync(wfrom, P.work_n, 4, hipMemcpyDeviceToDevice, A));
-    CHK(drp_launch_chunk_claims(&Q, ntc, A));
-    CHK(hipEventRecord(c->pev[k & 1], A));
-    // verification, output bases and emission of chunk k on the second stream
-    CHK(hipStreamWaitEvent(Bs, c->pev[k & 1], 0));
-    CHK(hipMemsetAsync(P.vlist_n, 0, 4, Bs));
-    CHK(drp_launch_chunk_verify(&Q, ntc, Bs));
-    CHK(drp_launch_chunk_scan(P.tile_count, P.tile_base, Q.tile0, Q.tile0 + ntc, tile_prefix, ns, carry, cap,
-                              P.overflow, Bs));
-    CHK(hipMemsetAsync(P.vlist_n, 0, 4, Bs));
-    CHK(drp_launch_chunk_emit(&Q, ntc, Bs));
-    CHK(hipEventRecord(c->pev[2 + (k & 1)], Bs));
-  }
-  uint64_t *sgscan = c->scratch.at<uint64_t>(L.scan_tmp);
-  CHK(drp_launch_tile_scan(P.tile_nch, tile_prefix, ns, NT, sgscan, P.tile_nch_base, ~0ull, P.overflow, Bs));
-  CHK(drp_launch_stream_counts(tile_prefix, ns, P.tile_count, P.tile_base, P.tile_nch, P.tile_nch_base, scount, Bs));
-  CHK(hipEventRecord(c->pev[2], Bs));
-  CHK(hipStreamWaitEvent(A, c->pev[2], 0));
-  CHK(hipEventRecord(c->ev[2], A));
-  uint32_t h[2];
-  CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, A));
-  CHK(hipStreamSynchronize(A));
-  float ms = 0;
-  hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
-  c->timing.decode_ms = ms;
-  c->timing.seg_repairs = 0;
-  c->timing.verify_relisted = 0;
-  if (h[1] & drp_spec_retry_mask()) {
-    // a prediction missed (or a bounded loop gave up): the repair passes and the full emission
-    TRACE("decode_pipe: flags %#x, repair passes from the pipelined claims", h[1]);
-    return run_decode_spec(c, bytes, nbytes, stream_off, entry, ns, fr, co, cap, res, true);
-  }
-  CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr, scount,
-                          fr->type, co->flags, cap, res, A));
-  CHK(drp_launch_key_post(bytes, tile_prefix, ns, P.tile_base, P.tile_count, cap, fr, co,
-                          c->key_post == DRP_KEY_POST_FLAGS, A));
-  CHK(hipEventRecord(c->ev[3], A));
-  CHK(hipStreamSynchronize(A));
-  hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
-  c->timing.total_ms = ms;
-  c->timing.finalize_ms = 0;
-  c->timing.strict_reruns = 0;
-  c->timing.exact_retries = 0;
-  c->timing.spec_repairs = 0;
-  if (h[1]) return DRP_E_CAPACITY;
-  return DRP_OK;
-}
-
 int run_decode(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
                const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
                uint64_t cap, drp_stream_result *res) {
   if (ns == 0) return DRP_OK;
   float spec_ms = 0, spec_total = 0;
   if (!c->exact && !c->strict) {
-    const uint32_t tile = drp_spec_tile_bytes();
-    const int r = (c->pipe_chunk && ns == 1 && nbytes / tile >= 2 * c->pipe_chunk)
-                      ? run_decode_pipe(c, bytes, nbytes, stream_off, entry, fr, co, cap, res)
-                      : run_decode_spec(c, bytes, nbytes, stream_off, entry, ns, fr, co, cap, res);
+    const int r = run_decode_spec(c, bytes, nbytes, stream_off, entry, ns, fr, co, cap, res);
     if (r != DRP_E_RETRY) return r;
     spec_ms = c->timing.decode_ms;
     spec_total = c->timing.total_ms;

@@ -566,8 +566,7 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
   // With a work list (the fast kernel ran first): the edge and dense tiles it listed, a few per
   // workgroup; without one: every tile, one per workgroup.
   const uint32_t nwork = P.work ? *P.work_n : 0u;
-  const uint32_t wfrom = (P.work && P.work_from) ? *P.work_from : 0u;  // (chunked: this chunk's entries)
-  for (uint32_t wi = wfrom + blockIdx.x; P.work ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
+  for (uint32_t wi = blockIdx.x; P.work ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
   const uint64_t t = P.work ? P.work[wi] : wi;
   bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
@@ -881,7 +880,7 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
 // bytes are not read). Random bytes essentially never pass; a real frame in another shape is left
 // undecided as before. Prediction only: verification is exact.
 #ifndef DRP_CHANGE_FILLS
-#define DRP_CHANGE_FILLS 1  // 1: nodes of the tile (not its halo); 2: every node; 0: none (A/B)
+#define DRP_CHANGE_FILLS 1  // 1: the tile's nodes and the halo's long frames; 2: every node; 0: none (A/B)
 #endif
 __device__ __forceinline__ bool change_fills(const uint32_t *w32, uint32_t po, uint32_t pl) {
   uint32_t off = 0, found = 0;
@@ -1157,6 +1156,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   constexpr uint32_t KPT = FCAP / NT;  // nodes per thread (at most)
   uint32_t ncode[KPT], npos[KPT];
   uint32_t na[KPT];
+  uint32_t cfw[KPT];  // a tile node's Change frame leaving the image: payload offset | length << 14
 #if DRP_K1_GIMG
   const uint32_t *w32 = reinterpret_cast<const uint32_t *>(P.bytes + G.A);  // (L2: the tile was just read)
 #else
@@ -1168,6 +1168,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     ncode[j] = NX_DEAD;
     na[j] = 0;
     npos[j] = 0;
+    cfw[j] = 0;
     if (i < total) {
       const uint32_t o = lpos[i], d = o >> 2, sh = (o & 3u) * 8u;
       const uint32_t a0 = w32[d], a1 = w32[d + 1], a2 = w32[d + 2];
@@ -1197,9 +1198,11 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
         a = 1;
       } else if (succ >= (DRP_HALO_NODES ? IMG - 16 : TILE)) {
         c = NX_FAR;   // past the listed positions: undecided (a restart that needs it checks in HBM),
-        a = 2;        // unless it is a Change frame whose fields fill it exactly (strong by structure)
-        if (DRP_CHANGE_FILLS && id == 1u && (DRP_CHANGE_FILLS == 2 || o < TILE) && change_fills(w32, o + k + 1u, L - 1u))
-          a = 1;
+        a = 2;        // unless it is a Change frame whose fields fill it exactly (below)
+        // (halo nodes: only frames longer than the halo, so C2's short frames there never pay for
+        // it; C5's long ones do, so a tile's last real frame is not left undecided by its successor)
+        if (DRP_CHANGE_FILLS && id == 1u && (DRP_CHANGE_FILLS == 2 || o < TILE || L > HALO) && L - 1u < (1u << 18))
+          cfw[j] = (o + k + 1u) | ((L - 1u) << 14);
       } else {
         const uint32_t th = succ / SEGB, b = succ % SEGB;
         const uint64_t lw = lmw[th];
@@ -1213,6 +1216,16 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
       ncode[j] = c;
       na[j] = a;
       npos[j] = o;
+    }
+  }
+  // Change frames that leave the image are strong by structure when their fields fill them
+  // exactly (change_fills). A loop of its own after the parse: inside it, its dependent loads kept
+  // the parse's loads of later nodes from being issued together (C2: claims 2.8 -> 5.2 ms).
+#pragma unroll
+  for (uint32_t j = 0; j < KPT; j++) {
+    if (cfw[j] && change_fills(w32, cfw[j] & 0x3FFFu, cfw[j] >> 14)) {
+      na[j] = 1;
+      lal[tid + j * NT] = 1;
     }
   }
   bsync();
@@ -1391,7 +1404,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
 
 __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) {
   __shared__ FastLds S;
-  const uint64_t t = P.tile0 + blockIdx.x;
+  const uint64_t t = blockIdx.x;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   const TileGeo G = tile_geo(P, t);
   if (t >= ntiles) return;  // (whole workgroup)
@@ -1429,7 +1442,7 @@ __device__ __forceinline__ uint32_t restart_bytes(uint32_t x) {  // 4-bit mask: 
 }
 __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
   const uint32_t tid = threadIdx.x, r = tid & (VL_G - 1u), gb = (tid & 63u) & ~(VL_G - 1u);
-  const uint64_t t = P.tile0 + ((uint64_t)blockIdx.x * VL_BLK + tid) / VL_G;
+  const uint64_t t = ((uint64_t)blockIdx.x * VL_BLK + tid) / VL_G;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   if (t >= ntiles) return;  // (whole 8-lane group: no barriers or cross-group exchanges below)
   const TileGeo G = tile_geo(P, t);
@@ -2057,7 +2070,7 @@ __global__ __launch_bounds__(256) void emit_sparse(DecodeParams P) {
   __shared__ uint32_t nl;
   __shared__ uint32_t fail[SP_TPB];
   const uint32_t tid = threadIdx.x;
-  const uint64_t t0 = P.tile0 + (uint64_t)blockIdx.x * SP_TPB;
+  const uint64_t t0 = (uint64_t)blockIdx.x * SP_TPB;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   if (tid == 0) nl = 0;
   if (tid < SP_TPB) fail[tid] = 0;
@@ -2136,7 +2149,7 @@ __global__ __launch_bounds__(256) void emit_sparse(DecodeParams P) {
 }
 
 #ifndef DRP_EMIT32
-#define DRP_EMIT32 1  // 0: the 64-bit fast emit (A/B)
+#define DRP_EMIT32 0  // 1: frames in 32-bit tile-relative form (A/B: 8.59 vs 8.50 ms C2, 2.56 vs 2.51 ms C5 decode)
 #endif
 
 #ifndef DRP_EMIT_FAST_WAVES
@@ -2168,7 +2181,6 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
     const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = wi % 8u;  // contiguous eighth, so
     t = (uint64_t)x * q + min(x, r) + wi / 8u;  // neighbouring tiles share an L2 (column lines)
   }
-  if (FAST) t += P.tile0;
   if (!FAST) bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
   if (t >= ntiles) continue;  // (whole workgroup)
@@ -2393,9 +2405,9 @@ __global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
 // The candidate tables of SEG_SB segments at a time are staged in LDS by the whole workgroup
 // (double-buffered: the next block loads while wave 0 follows the chain through this one), so
 // the serial part is a ballot per segment on LDS data.
-constexpr uint32_t SEG_SB = 32, SEG_STB = 1024;  // segments per staged block, threads
+constexpr uint32_t SEG_SB = 64, SEG_STB = 1024;  // segments per staged block, threads
 __global__ __launch_bounds__(SEG_STB) void seg_stitch(DecodeParams P, SegRange R) {
-  __shared__ uint64_t tab[2][SEG_SB][2 * SEG_CAND];  // 2 x 32 KB
+  __shared__ uint64_t tab[2][SEG_SB][2 * SEG_CAND];  // 2 x 64 KB
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const TileGeo G = seg_geo(P, R.s);
   constexpr uint32_t W = SEG_SB * 2 * SEG_CAND;  // words per block
@@ -2517,37 +2529,6 @@ __global__ __launch_bounds__(256) void blob_bytes_kernel(const uint8_t *type, co
     if ((type[i] & 0x3Fu) == DRP_TYPE_BLOB) acc += plen[i];
   acc = wave_sum64(acc);
   if ((threadIdx.x & 63u) == 0 && acc) atomicAdd((unsigned long long *)out, (unsigned long long)acc);
-}
-
-__global__ __launch_bounds__(SCAN_BLK) void chunk_scan_kernel(const uint64_t *cnt, uint64_t *base, uint64_t t0,
-                                                              uint64_t t1, const uint64_t *tile_prefix, uint64_t nstreams,
-                                                              uint64_t *carry, uint64_t cap, uint32_t *overflow) {
-  __shared__ uint64_t sw[SCAN_BLK / WAVE];
-  const uint64_t nt = tile_prefix[nstreams];
-  if (t1 > nt) t1 = nt;
-  uint64_t c = *carry;
-  for (uint64_t a = t0; a < t1; a += SCAN_SPAN) {
-    const uint64_t i0 = a + threadIdx.x * SCAN_PER;
-    uint64_t v[SCAN_PER], sum = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < SCAN_PER; k++) {
-      v[k] = i0 + k < t1 ? cnt[i0 + k] : 0;
-      sum += v[k];
-    }
-    uint64_t total;
-    uint64_t o = c + block_excl_scan64(sum, sw, total);
-#pragma unroll
-    for (uint32_t k = 0; k < SCAN_PER; k++) {
-      if (i0 + k < t1) {
-        base[i0 + k] = o;
-        if (i0 + k == nt - 1 && o + v[k] > cap) atomicOr(overflow, 1u);
-      }
-      o += v[k];
-    }
-    c += total;
-  }
-  __syncthreads();  // (every thread read *carry before it is written)
-  if (threadIdx.x == 0) *carry = c;
 }
 
 // per-stream change / blob counts (one thread per stream)
@@ -2711,42 +2692,6 @@ extern "C" hipError_t drp_launch_blob_bytes(const uint8_t *type, const uint32_t 
   const uint64_t nb = (n + 255) / 256;
   hipLaunchKernelGGL(spec::blob_bytes_kernel, dim3((uint32_t)(nb < 1024 ? nb : 1024)), dim3(256), 0, st, type, plen, n,
                      out);
-  return hipGetLastError();
-}
-
-extern "C" hipError_t drp_launch_chunk_scan(const uint64_t *cnt, uint64_t *base, uint64_t t0, uint64_t t1,
-                                            const uint64_t *tile_prefix, uint64_t nstreams, uint64_t *carry,
-                                            uint64_t cap, uint32_t *overflow, hipStream_t st) {
-  if (t1 <= t0) return hipSuccess;
-  hipLaunchKernelGGL(spec::chunk_scan_kernel, dim3(1), dim3(spec::SCAN_BLK), 0, st, cnt, base, t0, t1, tile_prefix,
-                     nstreams, carry, cap, overflow);
-  return hipGetLastError();
-}
-
-// Pipelined decode, one chunk of ntc tiles from P->tile0 (single stream; drp_api.hip): claims (the
-// general kernel takes the chunk's work-list entries from *P->work_from on), ...
-extern "C" hipError_t drp_launch_chunk_claims(const DecodeParams *P, uint64_t ntc, hipStream_t st) {
-  if (ntc == 0) return hipSuccess;
-  hipLaunchKernelGGL(spec::claims_fast, dim3((uint32_t)ntc), dim3(spec::NT), 0, st, *P);
-  hipLaunchKernelGGL(spec::spec_claims, dim3(64), dim3(spec::NT), 0, st, *P);
-  return hipGetLastError();
-}
-// ... verification (records-only, then verify_counts on the tiles it lists; caller zeroes vlist_n),
-extern "C" hipError_t drp_launch_chunk_verify(const DecodeParams *P, uint64_t ntc, hipStream_t st) {
-  if (ntc == 0) return hipSuccess;
-  const uint64_t nb = (ntc * spec::VL_G + spec::VL_BLK - 1) / spec::VL_BLK;
-  hipLaunchKernelGGL(spec::verify_lite, dim3((uint32_t)nb), dim3(spec::VL_BLK), 0, st, *P);
-  hipLaunchKernelGGL(spec::verify_counts, dim3(1024), dim3(spec::NT), 0, st, *P);
-  return hipGetLastError();
-}
-// ... and emission (sparse tiles, the fast kernel, the general one on its list; caller zeroes vlist_n)
-extern "C" hipError_t drp_launch_chunk_emit(const DecodeParams *P, uint64_t ntc, hipStream_t st) {
-  if (ntc == 0) return hipSuccess;
-  if (spec::SP_FRAMES && P->tile_sparse)
-    hipLaunchKernelGGL(spec::emit_sparse, dim3((uint32_t)((ntc + spec::SP_TPB - 1) / spec::SP_TPB)), dim3(256), 0, st,
-                       *P);
-  hipLaunchKernelGGL(spec::emit_tiles<true>, dim3((uint32_t)ntc), dim3(spec::NT), 0, st, *P);
-  hipLaunchKernelGGL(spec::emit_tiles<false>, dim3(1024), dim3(spec::NT), 0, st, *P);
   return hipGetLastError();
 }
 

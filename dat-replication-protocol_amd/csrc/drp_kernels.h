@@ -60,10 +60,6 @@ struct DecodeParams {
   // at its entry; a few frames in all): emit_sparse decodes its frames from HBM without staging
   // the tile, and emit_tiles skips it (emit_sparse clears the mark of a tile it cannot take)
   uint8_t *tile_sparse;
-  // chunked launches (the pipelined decode, drp_api.hip): the first tile of this launch (its grid
-  // covers the chunk), and the work-list entries the general claims kernel already took
-  uint64_t tile0;
-  const uint32_t *work_from;
   uint64_t *first_miss;  // per stream: the first tile a verify pass repaired (~0: none)
   // verify_counts appends the tiles whose entry a repair changed (the next repair pass verifies
   // only those); a count past dlist_cap or a nonzero dlist_n[2] means the next pass must be a
@@ -102,18 +98,7 @@ uint32_t drp_spec_retry_mask(void);
 uint32_t drp_spec_miss_bit(void);
 hipError_t drp_launch_spec_head(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                 uint32_t *tile_stream, hipStream_t st);
-// out[0] += sum of v[t0, t1) (out zeroed by the caller)
-// tile_base over tiles [t0, t1) = *carry + exclusive prefix of cnt; *carry += their total (one
-// workgroup; the chunks of the pipelined decode run in order on one stream)
-hipError_t drp_launch_chunk_scan(const uint64_t *cnt, uint64_t *base, uint64_t t0, uint64_t t1,
-                                 const uint64_t *tile_prefix, uint64_t nstreams, uint64_t *carry, uint64_t cap,
-                                 uint32_t *overflow, hipStream_t st);
-// the pipelined decode's per-chunk launches (P->tile0 = the chunk's first tile)
-hipError_t drp_launch_chunk_claims(const drp::DecodeParams *P, uint64_t ntc, hipStream_t st);
-hipError_t drp_launch_chunk_verify(const drp::DecodeParams *P, uint64_t ntc, hipStream_t st);
-hipError_t drp_launch_chunk_emit(const drp::DecodeParams *P, uint64_t ntc, hipStream_t st);
-// emit_sparse over every tile (before emit_tiles): the tiles verification marked sparse
-hipError_t drp_launch_emit_sparse(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t st);
+// out[0] = payload bytes of the blob rows among rows [0, n) (out zeroed by the caller)
 hipError_t drp_launch_blob_bytes(const uint8_t *type, const uint32_t *plen, uint64_t n, uint64_t *out, hipStream_t st);
 hipError_t drp_launch_seg_repair(const drp::DecodeParams *P, uint64_t s, uint64_t t0, uint64_t tl, uint64_t *scratch,
                                  hipStream_t st);
