@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${1:-r3d}
 mkdir -p gpurun_out
 bash scripts/gpu_session.sh $TAG "${2:-}" ""
-for ch in 8192 32768; do
+for ch in; do
   DRP_PIPE_CHUNK=$ch timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/pipe_c2_$ch.log 2>&1
   echo "pipe $ch done"
 done
