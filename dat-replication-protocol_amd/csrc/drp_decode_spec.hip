@@ -35,6 +35,8 @@
 #include "drp_device.h"
 #include "drp_kernels.h"
 
+#include <algorithm>
+
 namespace drp {
 namespace spec {
 
@@ -466,6 +468,16 @@ __device__ __forceinline__ void stage(const DecodeParams &P, const TileGeo &G, u
   bsync();
 }
 
+// The image load_image() fetched into registers (a prefetch), written to LDS as stage() does.
+__device__ __forceinline__ void put_image(uint8_t *buf, const uint4 (&v)[SEGB / 16], const uint4 &h) {
+  const uint32_t tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < (int)(SEGB / 16); k++) *reinterpret_cast<uint4 *>(buf + tid * SEGB + 16 * k) = v[k];
+  if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = h;
+  if (tid < 2) *reinterpret_cast<uint4 *>(buf + IMG + tid * 16) = make_uint4(0, 0, 0, 0);
+  bsync();
+}
+
 // Stage the tile and its halo with LDS-DMA (global_load_lds_dwordx4: no VGPRs hold the image;
 // wave w's k-th load fills LDS bytes [4096 w + 1024 k, +1024) from the same offsets of the tile),
 // except near the end of the batch buffer (guarded register loads there).
@@ -882,8 +894,8 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
 #ifndef DRP_CHANGE_FILLS
 #define DRP_CHANGE_FILLS 1  // 1: the tile's nodes and the halo's long frames; 2: every node; 0: none (A/B)
 #endif
-__device__ __forceinline__ bool change_fills(const uint32_t *w32, uint32_t po, uint32_t pl) {
-  uint32_t off = 0, found = 0;
+__device__ __forceinline__ bool change_fills(const uint32_t *w32, uint32_t po, uint32_t pl, uint32_t off = 0,
+                                             uint32_t found = 0) {
 #pragma unroll 1
   for (uint32_t f = 0; f < 8u && off < pl; f++) {
     const uint32_t q = po + off;
@@ -1156,7 +1168,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   constexpr uint32_t KPT = FCAP / NT;  // nodes per thread (at most)
   uint32_t ncode[KPT], npos[KPT];
   uint32_t na[KPT];
-  uint32_t cfw[KPT];  // a tile node's Change frame leaving the image: payload offset | length << 14
+  uint32_t cfw[KPT];  // a Change frame leaving the image: payload offset | length << 14
+  uint32_t cff[KPT];  // its first field's bytes | key seen << 20
 #if DRP_K1_GIMG
   const uint32_t *w32 = reinterpret_cast<const uint32_t *>(P.bytes + G.A);  // (L2: the tile was just read)
 #else
@@ -1169,6 +1182,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     na[j] = 0;
     npos[j] = 0;
     cfw[j] = 0;
+    cff[j] = 0;
     if (i < total) {
       const uint32_t o = lpos[i], d = o >> 2, sh = (o & 3u) * 8u;
       const uint32_t a0 = w32[d], a1 = w32[d + 1], a2 = w32[d + 2];
@@ -1201,8 +1215,19 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
         a = 2;        // unless it is a Change frame whose fields fill it exactly (below)
         // (halo nodes: only frames longer than the halo, so C2's short frames there never pay for
         // it; C5's long ones do, so a tile's last real frame is not left undecided by its successor)
-        if (DRP_CHANGE_FILLS && id == 1u && (DRP_CHANGE_FILLS == 2 || o < TILE || L > HALO) && L - 1u < (1u << 18))
-          cfw[j] = (o + k + 1u) | ((L - 1u) << 14);
+        // The first field is checked here from the header's own bytes (no load): subset or key
+        // (protocol-buffers writes fields in schema order), a length of <= 3 bytes, inside the
+        // payload. ~99% of shadow headers stop here, so change_fills' loads are rare on C2.
+        if (DRP_CHANGE_FILLS && id == 1u && (DRP_CHANGE_FILLS == 2 || o < TILE || L > HALO) && L - 1u < (1u << 18)) {
+          const uint32_t x = k + 1u < 4u ? __builtin_amdgcn_alignbit(wn, w, 8u * (k + 1u)) : wn;  // bytes k+1..k+4
+          const uint32_t tg = x & 0xFFu, lt = ~(x >> 8) & 0x808080u;
+          if ((tg == 0x0Au || tg == 0x12u) && lt) {
+            const uint32_t nb = ((uint32_t)__builtin_ctz(lt) >> 3) + 1u, y = x >> 8;
+            const uint32_t v = ((y & 0x7Fu) | ((y >> 1) & 0x3F80u) | ((y >> 2) & 0x1FC000u)) & ((1u << (7u * nb)) - 1u);
+            const uint32_t f1 = 1u + nb + v;  // the first field's bytes
+            if (f1 < L - 1u) cfw[j] = (o + k + 1u) | ((L - 1u) << 14), cff[j] = f1 | ((tg == 0x12u ? 1u : 0u) << 20);
+          }
+        }
       } else {
         const uint32_t th = succ / SEGB, b = succ % SEGB;
         const uint64_t lw = lmw[th];
@@ -1223,7 +1248,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   // the parse's loads of later nodes from being issued together (C2: claims 2.8 -> 5.2 ms).
 #pragma unroll
   for (uint32_t j = 0; j < KPT; j++) {
-    if (cfw[j] && change_fills(w32, cfw[j] & 0x3FFFu, cfw[j] >> 14)) {
+    if (cfw[j] && change_fills(w32, cfw[j] & 0x3FFFu, cfw[j] >> 14, cff[j] & 0xFFFFFu, cff[j] >> 20)) {
       na[j] = 1;
       lal[tid + j * NT] = 1;
     }
@@ -2280,6 +2305,10 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
 // spread over the CUs plus a short serial stitch, however the predictions failed.
 constexpr uint32_t SEG_CAND = 64, SEG_GMAX = 1024;  // candidates per segment, tiles per segment (max)
 constexpr uint64_t SEG_NMAX = 8192;  // segments per repair (max)
+#ifndef DRP_SEG_NTARGET
+#define DRP_SEG_NTARGET 2048
+#endif
+constexpr uint64_t SEG_NTARGET = DRP_SEG_NTARGET;  // segments per repair (aimed at)
 constexpr uint64_t SEG_GMIN = 4;     // tiles per segment (min)
 struct SegRange {
   uint64_t s, t0, tl, G, nseg;  // stream, tiles [t0, tl), tiles per segment, segments
@@ -2382,8 +2411,15 @@ __global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
     cpos[idx] = lb + (uint32_t)__builtin_ctzll(bits);
   bsync();
   uint64_t pos = (wid == 0 && lane < nc) ? cpos[lane] : NONE, start = pos;
-  // walk: the lanes' chains through the segment, tile by tile (a tile only when a chain is in it)
+  // walk: the lanes' chains through the segment, tile by tile (a tile only when a chain is in it);
+  // the next tile is fetched into registers while wave 0 walks this one (the chains usually go on
+  // there), so its load latency is not on the segment's serial path
+  uint4 pv[SEGB / 16], ph;
   for (;;) {
+    TileGeo Gn = G;
+    Gn.A = G.A + TILE;
+    const bool pre = Gn.A < send;
+    if (pre) load_image(P, Gn, pv, ph);
     if (wid == 0) {
       const Img mt{buf, P.bytes, G.A, G.se};  // (the image of the tile staged last)
       pos = seg_advance(mt, pos, umin64(G.A + TILE, send));
@@ -2394,7 +2430,8 @@ __global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
     const uint64_t q = nxt;
     if (q == NONE) break;
     G.A = seg_tile_a(G, ta + (q - seg_tile_a(G, ta)) / TILE);
-    stage(P, G, buf);  // (its barrier orders the walk's reads before the next image)
+    if (pre && G.A == Gn.A) put_image(buf, pv, ph);  // (the barrier above ordered the walk's reads)
+    else stage(P, G, buf);
   }
   if (wid == 0) {
     R.cand[seg * 2 * SEG_CAND + lane] = lane < nc ? start : NONE;
@@ -2473,6 +2510,8 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
   uint64_t p = R.seg_entry[seg];
   if (tid == 0) nxt = (is_pos(p) && p < send) ? p : NONE;
   bsync();
+  uint4 pv[SEGB / 16], ph;
+  uint64_t pa = NONE;  // the tile prefetched into pv / ph
   for (;;) {
     const uint64_t q = nxt;
     if (q == NONE) break;
@@ -2481,7 +2520,15 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
     re[tid] = 0xFF;
     rn[tid] = 0;
     rc[tid] = 0;
-    stage(P, G, buf);  // (its barrier also orders the record resets)
+    if (G.A == pa) put_image(buf, pv, ph);  // (its barrier also orders the record resets)
+    else stage(P, G, buf);
+    // the next tile into registers while thread 0 walks this one (the chain usually goes on there)
+    {
+      TileGeo Gn = G;
+      Gn.A = G.A + TILE;
+      pa = Gn.A < send ? Gn.A : NONE;
+      if (pa != NONE) load_image(P, Gn, pv, ph);
+    }
     if (tid == 0) {
       const Img m{buf, P.bytes, G.A, G.se};
       const uint64_t lim = umin64(G.A + TILE, send);
@@ -2710,8 +2757,10 @@ extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, u
   // chain), and the segments fill the CUs several workgroups deep.
   const uint64_t n = tl - t0 < spec::SEG_NMAX * spec::SEG_GMAX ? tl - t0 : spec::SEG_NMAX * spec::SEG_GMAX;
   R.tl = t0 + n;
-  const uint64_t g = (n + spec::SEG_NMAX - 1) / spec::SEG_NMAX;
-  R.G = g > spec::SEG_GMIN ? g : spec::SEG_GMIN;
+  // ~SEG_NTARGET segments: fewer make each workgroup's walk longer, more make the serial stitch
+  // longer (1.7 GB dense cascade: 8192 segments stitch in 1.8 ms)
+  const uint64_t g = std::min<uint64_t>((n + spec::SEG_NTARGET - 1) / spec::SEG_NTARGET, spec::SEG_GMAX);
+  R.G = g > spec::SEG_GMIN ? g : spec::SEG_GMIN;  // (n <= SEG_NMAX * SEG_GMAX: at most SEG_NMAX segments)
   R.nseg = (n + R.G - 1) / R.G;
   R.cand = scratch;
   R.seg_entry = scratch + 2 * spec::SEG_CAND * spec::SEG_NMAX;
