@@ -887,19 +887,20 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
 // A Change frame that leaves the listed positions (long frames: C5's 4 KB values) cannot have its
 // chain followed in the image. It is strong when its payload parses as a Change in the schema's
 // own shape: one-byte tags of the schema with their wire types (length-delimited subset, key and
-// value; varint change, from and to of <= 5 bytes), every field header inside the image, the
+// value; varint change, from and to of <= 5 bytes), every field header at most 512 bytes past the
+// image (read from the batch, not the LDS), the
 // required fields present, and the last field ending exactly at the payload end (the value's
 // bytes are not read). Random bytes essentially never pass; a real frame in another shape is left
 // undecided as before. Prediction only: verification is exact.
 #ifndef DRP_CHANGE_FILLS
 #define DRP_CHANGE_FILLS 1  // 1: the tile's nodes and the halo's long frames; 2: every node; 0: none (A/B)
 #endif
-__device__ __forceinline__ bool change_fills(const uint32_t *w32, uint32_t po, uint32_t pl, uint32_t off = 0,
-                                             uint32_t found = 0) {
+__device__ __forceinline__ bool change_fills(const uint32_t *w32, uint32_t po, uint32_t pl, uint32_t lim,
+                                             uint32_t off = 0, uint32_t found = 0) {
 #pragma unroll 1
   for (uint32_t f = 0; f < 8u && off < pl; f++) {
     const uint32_t q = po + off;
-    if (q + 12u > IMG) return false;
+    if (q + 12u > lim) return false;
     const uint32_t d = q >> 2, sh = (q & 3u) * 8u;
     const uint32_t a0 = w32[d], a1 = w32[d + 1], a2 = w32[d + 2];
     const uint32_t w = __builtin_amdgcn_alignbit(a1, a0, sh), wn = __builtin_amdgcn_alignbit(a2, a1, sh);
@@ -1248,7 +1249,10 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   // the parse's loads of later nodes from being issued together (C2: claims 2.8 -> 5.2 ms).
 #pragma unroll
   for (uint32_t j = 0; j < KPT; j++) {
-    if (cfw[j] && change_fills(w32, cfw[j] & 0x3FFFu, cfw[j] >> 14, cff[j] & 0xFFFFFu, cff[j] >> 20)) {
+    // (field headers may lie past the image, up to 512 bytes: a halo frame's key runs past it; w32
+    // reads the batch, which holds them: interior tiles end >= IMG before the stream end)
+    if (cfw[j] && change_fills(w32, cfw[j] & 0x3FFFu, cfw[j] >> 14, min(se_rel, IMG + 512u), cff[j] & 0xFFFFFu,
+                               cff[j] >> 20)) {
       na[j] = 1;
       lal[tid + j * NT] = 1;
     }
