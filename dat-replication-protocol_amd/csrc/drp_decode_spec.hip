@@ -934,6 +934,56 @@ __device__ __forceinline__ bool change_fills(const uint32_t *w32, uint32_t po, u
   return off == pl && found == 15u;
 }
 
+// change_fills after the first field, with one load level: the 28 bytes from q = po + off (the
+// numeric fields of <= 6 bytes each, then the value's tag and length) are loaded together and parsed
+// from registers. The value must end the payload. 1: strong; 0: not a Change of that shape (C2's
+// swallowing shadow headers, which read a real frame's fields and then its successor's header,
+// stop here after one load instead of six); 2: another shape (a subset before the key): the
+// field-by-field check decides.
+__device__ __forceinline__ uint32_t change_fills_win(const uint32_t *w32, uint32_t po, uint32_t pl, uint32_t lim,
+                                                     uint32_t off, uint32_t found) {
+  const uint32_t q = po + off;
+  if (q + 36u > lim) return 2u;  // (the nine dwords from q & ~3)
+  const uint32_t d = q >> 2, sh = (q & 3u) * 8u;
+  uint32_t a[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) a[i] = w32[d + i];
+  uint64_t x[4];  // bytes q .. q + 31
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    x[i] = (uint64_t)__builtin_amdgcn_alignbit(a[2 * i + 1], a[2 * i], sh) |
+           ((uint64_t)__builtin_amdgcn_alignbit(a[2 * i + 2], a[2 * i + 1], sh) << 32);
+  uint32_t used = 0;
+#pragma unroll
+  for (int f = 0; f < 4; f++) {
+    const uint32_t b0 = (uint32_t)x[0] & 0xFFu, tag = b0 >> 3;
+    const uint64_t y = x[0] >> 8;  // the varint's bytes (up to 5)
+    const uint64_t tm = ~y & 0x8080808080ull;
+    if (b0 >= 0x80u || !tm) return 0u;
+    const uint32_t k2 = ((uint32_t)__builtin_ctzll(tm) >> 3) + 1u;
+    const uint64_t v = ((y & 0x7Full) | ((y >> 1) & 0x3F80ull) | ((y >> 2) & 0x1FC000ull) | ((y >> 3) & 0xFE00000ull) |
+                        ((y >> 4) & 0x7F0000000ull)) & ((1ull << (7u * k2)) - 1ull);
+    if (tag - 3u <= 2u && (b0 & 7u) == 0u) {  // change / from / to
+      found |= 1u << (tag - 2u);
+      const uint32_t s = 1u + k2;
+      used += s;
+      if (off + used > pl) return 0u;
+      const uint32_t b = 8u * s;  // (2..6 bytes)
+      x[0] = (x[0] >> b) | (x[1] << (64u - b));
+      x[1] = (x[1] >> b) | (x[2] << (64u - b));
+      x[2] = (x[2] >> b) | (x[3] << (64u - b));
+      x[3] >>= b;
+      continue;
+    }
+    if (b0 == 0x32u) {  // the value: it must end the payload
+      return (found == 15u && (uint64_t)off + used + 1u + k2 + v == (uint64_t)pl) ? 1u : 0u;
+    }
+    if (b0 == 0x0Au || b0 == 0x12u) return 2u;  // a length-delimited field before the value
+    return 0u;
+  }
+  return 2u;
+}
+
 // Node word: successor code (node index or NX_*) | min(successor offset, 0x3FFF) << 16 | id << 30
 // (id 3: the node's own header is invalid).
 // Walk from node exit x (offset < s1r) through the thread's bytes: returns the exit (a node whose
@@ -1251,8 +1301,13 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   for (uint32_t j = 0; j < KPT; j++) {
     // (field headers may lie past the image, up to 512 bytes: a halo frame's key runs past it; w32
     // reads the batch, which holds them: interior tiles end >= IMG before the stream end)
-    if (cfw[j] && change_fills(w32, cfw[j] & 0x3FFFu, cfw[j] >> 14, min(se_rel, IMG + 512u), cff[j] & 0xFFFFFu,
-                               cff[j] >> 20)) {
+    uint32_t cr = 0;
+    if (cfw[j]) {
+      const uint32_t lim = min(se_rel, IMG + 512u), po = cfw[j] & 0x3FFFu, pl = cfw[j] >> 14;
+      cr = change_fills_win(w32, po, pl, lim, cff[j] & 0xFFFFFu, cff[j] >> 20);
+      if (cr == 2u) cr = change_fills(w32, po, pl, lim, cff[j] & 0xFFFFFu, cff[j] >> 20) ? 1u : 0u;
+    }
+    if (cr == 1u) {
       na[j] = 1;
       lal[tid + j * NT] = 1;
     }

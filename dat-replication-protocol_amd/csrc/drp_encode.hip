@@ -156,7 +156,11 @@ __device__ __forceinline__ uint4 enc_shift(uint4 lo, uint4 hi, uint32_t sh) {
 // cover them (funnel shift by the wave-uniform source misalignment), then a byte tail. The
 // second block of the last step lies in the aligned 16 bytes that hold the last source byte,
 // so no load leaves the source's pages.
-__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t lane) {
+#ifndef DRP_ENC_PIPE
+#define DRP_ENC_PIPE 0  // 1: the next step's loads issued before this step's store (A/B)
+#endif
+__device__ __forceinline__ void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint64_t n,
+                                          uint32_t lane) {
   if (n < 128) {
     for (uint64_t k = lane; k < n; k += 64) dst[k] = src[k];
     return;
@@ -184,10 +188,25 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
     for (int u = 0; u < DRP_ENC_UNROLL; u++) enc_st(da + b + 64 * u, enc_shift(lo[u], hi[u], sh));
   }
 #endif
+#if DRP_ENC_PIPE
+  // software-pipelined: step b + 64's two blocks are loaded before step b's store
+  if (b < nb) {
+    uint4 lo = enc_ld(sa + b), hi = sh ? enc_ld(sa + b + 1) : lo;
+    for (; b + 64 < nb; b += 64) {
+      const uint4 lo2 = enc_ld(sa + b + 64), hi2 = sh ? enc_ld(sa + b + 65) : lo2;
+      enc_st(da + b, enc_shift(lo, hi, sh));
+      lo = lo2;
+      hi = hi2;
+    }
+    enc_st(da + b, enc_shift(lo, hi, sh));
+    b += 64;
+  }
+#else
   for (; b < nb; b += 64) {
     const uint4 lo = enc_ld(sa + b);
     enc_st(da + b, sh == 0 ? lo : enc_shift(lo, enc_ld(sa + b + 1), sh));
   }
+#endif
   const uint32_t tail = (uint32_t)(n & 15);
   if (lane < tail) dst[(nb << 4) + lane] = src[(nb << 4) + lane];
 }
