@@ -1195,6 +1195,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     push_work(P, t);
     return FC_DENSE;
   }
+  if (tid == 0) xw[3] = 0;  // (nodes whose successor is a node: counted in the parse)
   loff[tid] = (uint16_t)off;
   {
     uint64_t bits = live;
@@ -1219,6 +1220,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   constexpr uint32_t KPT = FCAP / NT;  // nodes per thread (at most)
   uint32_t ncode[KPT], npos[KPT];
   uint32_t na[KPT];
+  uint32_t chained = 0;  // this thread's nodes whose successor is a node (in the image)
   uint32_t cfw[KPT];  // a Change frame leaving the image: payload offset | length << 14
   uint32_t cff[KPT];  // its first field's bytes | key seen << 20
 #if DRP_K1_GIMG
@@ -1292,14 +1294,20 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
       ncode[j] = c;
       na[j] = a;
       npos[j] = o;
+      chained += c < NX_TAILB;
     }
   }
+  if (chained) atomicAdd(&xw[3], chained);
   // Change frames that leave the image are strong by structure when their fields fill them
   // exactly (change_fills). A loop of its own after the parse: inside it, its dependent loads kept
   // the parse's loads of later nodes from being issued together (C2: claims 2.8 -> 5.2 ms).
   bsync();  // (the node list is complete)
+  // A tile with many frames chained inside its image (C2: ~95) predicts its chain without
+  // them: the check runs only in sparse tiles (C5: two real frames, their chains leave the image).
+  const bool cf_tile = xw[3] < 32u;
 #pragma unroll
   for (uint32_t j = 0; j < KPT; j++) {
+    if (!cf_tile) cfw[j] = 0;
     // (field headers may lie past the image, up to 512 bytes: a halo frame's key runs past it; w32
     // reads the batch, which holds them: interior tiles end >= IMG before the stream end)
     uint32_t cr = 0;
