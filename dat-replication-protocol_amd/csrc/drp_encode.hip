@@ -315,7 +315,14 @@ __device__ __forceinline__ uint32_t put_segs(uint8_t *o, uint32_t lane, const VS
 #define WAVE_COPY wave_copy
 #endif
 // one wave per frame (grid-stride over frames)
+#ifndef DRP_ENC_MINW
+#define DRP_ENC_MINW 0  // > 0: min waves per SIMD for the write kernel (8: 64 VGPRs, a 28-byte spill)
+#endif
+#if DRP_ENC_MINW
+__global__ __launch_bounds__(256, DRP_ENC_MINW) void enc_write_kernel(EncodeParams P) {
+#else
 __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
+#endif
   const uint32_t lane = lane_id();
   const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
