@@ -2435,7 +2435,7 @@ __device__ __forceinline__ uint64_t seg_end(const TileGeo &G, const SegRange &R,
 // or the segment end); a header that ends the chain returns MARK_TERM (| M_ERR) | p
 __device__ __forceinline__ uint64_t seg_advance(const Img &m, uint64_t p, uint64_t lim) {
   while (is_pos(p) && p < lim && p < m.se) {
-    const Hdr h = m.at(p);
+    const Hdr h = hdr_fast(m, p);  // (1..3-byte varints parsed in 32 bits; others as Img::at)
     if (h.kind != H_VALID) return term_of(h, p);
     p = h.succ;
   }
@@ -2615,7 +2615,7 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
       p = q;
       // seg_advance, keeping the records of the chain's frames in this tile
       while (is_pos(p) && p < lim && p < m.se) {
-        const Hdr h = m.at(p);
+        const Hdr h = hdr_fast(m, p);
         if (h.kind != H_VALID) {
           p = term_of(h, p);
           ok = 0;
