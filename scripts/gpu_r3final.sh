@@ -6,7 +6,7 @@ set -e
 export TMPDIR=/tmp
 TAG=${1:-final}
 mkdir -p gpurun_out
-bash scripts/gpu_session.sh $TAG "" ""
+bash scripts/gpu_session.sh $TAG "${2:-}" ""
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_c5 -o run -- \
   python3 -u $GRAFT_REPO_ROOT/bench.py --workload c5 --steps 5 --warmup 2 --no-cpu > $GRAFT_REPO_ROOT/gpurun_out/bench_c5_prof.log 2>&1)
 echo c5 prof done
