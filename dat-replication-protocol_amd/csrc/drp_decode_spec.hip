@@ -1195,7 +1195,6 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     push_work(P, t);
     return FC_DENSE;
   }
-  if (tid == 0) xw[3] = 0;  // (nodes whose successor is a node: counted in the parse)
   loff[tid] = (uint16_t)off;
   {
     uint64_t bits = live;
@@ -1297,39 +1296,26 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
       chained += c < NX_TAILB;
     }
   }
-  if (chained) atomicAdd(&xw[3], chained);
   // Change frames that leave the image are strong by structure when their fields fill them
   // exactly (change_fills). A loop of its own after the parse: inside it, its dependent loads kept
-  // the parse's loads of later nodes from being issued together (C2: claims 2.8 -> 5.2 ms).
-  bsync();  // (the node list is complete)
-  // A tile with many frames chained inside its image (C2: ~95) predicts its chain without
-  // them: the check runs only in sparse tiles (C5: two real frames, their chains leave the image).
-  const bool cf_tile = xw[3] < 32u;
+  // the parse's loads of later nodes from being issued together (C2: claims 2.8 -> 5.2 ms). Only
+  // a wave whose bytes chain few frames inside the image runs it (C5: two real frames per tile,
+  // their chains leave the image; C2: ~47 per wave, predicted without it).
+  if (wave_sum32(chained) < 16u) {
 #pragma unroll
-  for (uint32_t j = 0; j < KPT; j++) {
-    if (!cf_tile) cfw[j] = 0;
-    // (field headers may lie past the image, up to 512 bytes: a halo frame's key runs past it; w32
-    // reads the batch, which holds them: interior tiles end >= IMG before the stream end)
-    uint32_t cr = 0;
-    if (cfw[j]) {
-      // A header whose varint swallows a shorter header (a random byte >= 0x80 before a real
-      // one: same id, same payload start) is not checked when the shorter one's chain goes on
-      // for two frames in the image (C2: the real frame, 45 such shadows per tile); the suffix of
-      // a real long frame's header (C5: a 1-byte "length" inside the key) essentially never does.
-      const uint32_t o = npos[j], k = (cfw[j] & 0x3FFFu) - o - 1u, x = o + 1u, th = x / SEGB;
-      if (k >= 2u && x < IMG && ((lmw[th] >> (x % SEGB)) & 1ull)) {
-        const uint32_t c1 = lnd[loff[th] + (uint32_t)__builtin_popcountll(lmw[th] & ((1ull << (x % SEGB)) - 1ull))] & 0xFFFFu;
-        if (c1 < NX_TAILB && (lnd[c1] & 0xFFFFu) < NX_TAILB) cfw[j] = 0;
+    for (uint32_t j = 0; j < KPT; j++) {
+      // (field headers may lie past the image, up to 512 bytes: a halo frame's key runs past it;
+      // w32 reads the batch, which holds them: interior tiles end >= IMG before the stream end)
+      uint32_t cr = 0;
+      if (cfw[j]) {
+        const uint32_t lim = min(se_rel, IMG + 512u), po = cfw[j] & 0x3FFFu, pl = cfw[j] >> 14;
+        cr = change_fills_win(w32, po, pl, lim, cff[j] & 0xFFFFFu, cff[j] >> 20);
+        if (cr == 2u) cr = change_fills(w32, po, pl, lim, cff[j] & 0xFFFFFu, cff[j] >> 20) ? 1u : 0u;
       }
-    }
-    if (cfw[j]) {
-      const uint32_t lim = min(se_rel, IMG + 512u), po = cfw[j] & 0x3FFFu, pl = cfw[j] >> 14;
-      cr = change_fills_win(w32, po, pl, lim, cff[j] & 0xFFFFFu, cff[j] >> 20);
-      if (cr == 2u) cr = change_fills(w32, po, pl, lim, cff[j] & 0xFFFFFu, cff[j] >> 20) ? 1u : 0u;
-    }
-    if (cr == 1u) {
-      na[j] = 1;
-      lal[tid + j * NT] = 1;
+      if (cr == 1u) {
+        na[j] = 1;
+        lal[tid + j * NT] = 1;
+      }
     }
   }
   bsync();

@@ -15,3 +15,11 @@ echo c5 prof done
 echo dense prof done
 bash scripts/gpu_pmc.sh 20000000 c2
 echo pmc done
+# two ranks on the box's one GPU over gloo (the RCCL path is the driver's 8-GPU run): C5 round trip
+# and C4 stream shards with the stats all-gather and global index
+timeout -k 10 300 python -u bench.py --gpus 2 --backend gloo --workload c5 --steps 3 --warmup 1 --no-cpu \
+  > gpurun_out/bench_c5_gloo2.log 2>&1
+echo c5 gloo2 done
+timeout -k 10 300 python -u bench.py --gpus 2 --backend gloo --workload c4 --steps 3 --warmup 1 --no-cpu \
+  > gpurun_out/bench_c4_gloo2.log 2>&1
+echo c4 gloo2 done
