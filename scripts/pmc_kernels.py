@@ -1,6 +1,6 @@
 """Per-kernel PMC summary of scripts/gpu_pmc.sh passes (gpurun_out/pmc/<pass>/): average per dispatch
 and per frame, FETCH_SIZE doubled per the gfx950 note (MI355X_MICROARCH.md: 128-B requests
-tallied at 64 B). Usage: python scripts/pmc_kernels.py [frames] [--write profiles/pmc_decode.json]"""
+tallied at 64 B). Usage: python scripts/pmc_kernels.py [frames] [--dir gpurun_out/pmc] [--write profiles/pmc_decode.json]"""
 import collections
 import csv
 import glob
@@ -8,11 +8,13 @@ import json
 import sys
 
 KNAME = "speculative decode: claims_fast + verify_lite + tile scans + emit_tiles"  # = bench.py's kname
-args = [a for a in sys.argv[1:] if not a.startswith("--")]
+PMC_DIR = sys.argv[sys.argv.index("--dir") + 1] if "--dir" in sys.argv else "gpurun_out/pmc"
+args = [a for a in sys.argv[1:] if not a.startswith("--") and a != PMC_DIR and
+        not (("--write" in sys.argv) and a == sys.argv[sys.argv.index("--write") + 1])]
 frames = float(args[0]) if args else 20e6
 tot = collections.defaultdict(float)
 disp = collections.defaultdict(set)
-for f in glob.glob("gpurun_out/pmc/*/**/*counter_collection.csv", recursive=True):
+for f in glob.glob(PMC_DIR + "/*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
         if "drp" not in k:
