@@ -1,16 +1,11 @@
 #!/bin/bash
 # Round-3 session d: the GPU suite (failures reported, not fatal), smoke, bench lines (C2 default,
-# C5, C4), the kernel-trace summary, A/B variants, the pipelined decode's C2 lines, and a kernel
-# trace of the dense-cascade probe. Each GPU step has its own limit; a crash or timeout ends it.
+# C5, C4), the kernel-trace summary, A/B variants, and kernel traces of C5 and the dense probe. Each GPU step has its own limit; a crash or timeout ends it.
 set -e
 export TMPDIR=/tmp
 TAG=${1:-r3d}
 mkdir -p gpurun_out
 bash scripts/gpu_session.sh $TAG "${2:-}" ""
-for ch in; do
-  DRP_PIPE_CHUNK=$ch timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/pipe_c2_$ch.log 2>&1
-  echo "pipe $ch done"
-done
 (cd /tmp && DRP_TRACE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_dense -o run -- \
   python3 -u $GRAFT_REPO_ROOT/scripts/probe_dense.py > $GRAFT_REPO_ROOT/gpurun_out/probe_dense_prof.log 2>&1)
 echo dense prof done
