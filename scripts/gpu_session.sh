@@ -32,6 +32,3 @@ for v in $AB; do
   DRP_LIB=exp/$v/libdrp.so timeout -k 10 200 python -u bench.py --workload c5 --steps 5 --warmup 2 --no-cpu > gpurun_out/ab_c5_$v.log 2>&1
   echo "$v bench done"
 done
-if [ "$3" = "l3" ]; then
-  bash scripts/gpu_l3probe.sh l3_$TAG
-fi
