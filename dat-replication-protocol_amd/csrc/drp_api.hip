@@ -86,6 +86,9 @@ struct drp_ctx {
   int strict = 0;
   int exact = 0;  // 1: always the exact kernel (decode_tiles), never the speculative one
   int key_post = 0;  // DRP_KEY_POST_*: key hashes and/or key flags on every decode
+  // claims_fast's structural check of long frames: on after a decode whose frames average
+  // >= 512 bytes (or none yet); DRP_CHANGE_CHECKS=0/1 forces it (A/B, tests)
+  int change_checks = 1, change_checks_env = -1;
   int cus = 256;
   uint32_t waves_per_cu = 16;
   DevBuf scratch, in_stage, out_stage, aux;
@@ -156,6 +159,7 @@ int drp_open(int device, drp_ctx **out) {
     if (tb == 4096 || tb == 8192) c->B = tb / 64;
   }
   if (const char *d = getenv("DRP_DECODE")) c->exact = strcmp(d, "exact") == 0;
+  if (const char *d = getenv("DRP_CHANGE_CHECKS")) c->change_checks = c->change_checks_env = atoi(d) ? 1 : 0;
   if (const char *w = getenv("DRP_WAVES_PER_CU")) {
     int v = atoi(w);
     if (v > 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
@@ -507,6 +511,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.dlist_cap = NT;
   P.dstamp = reinterpret_cast<uint32_t *>(rec + 4 * NT);  // (after the dirty lists)
   P.pass_id = 1;
+  P.change_checks = (uint32_t)c->change_checks;
   if (const char *e = getenv("DRP_KSTRONG_HBM")) P.kstrong_hbm = atoi(e);  // (tests: weaker predictions)
   CHK(hipMemsetAsync(P.dstamp, 0, NT * 4, st));
   if (const char *e = getenv("DRP_DIRTY_CAP")) P.dlist_cap = std::min<uint64_t>(NT, strtoull(e, nullptr, 10));  // (tests)
@@ -608,8 +613,10 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     CHK(hipEventRecord(c->ev[2], st));
   }
   CHK(hipEventRecord(c->ev[3], st));
-  CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
+  CHK(hipMemcpyAsync(h, ctrl, 16, hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
+  if (!retry && c->change_checks_env < 0)  // (h[3]: the call's frames, from stream_counts)
+    c->change_checks = h[3] == 0 || nbytes / h[3] >= 512 ? 1 : 0;
   if (retry) h[1] |= miss;
   float ms = 0;
   hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);

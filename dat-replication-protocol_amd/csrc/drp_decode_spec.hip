@@ -1107,6 +1107,7 @@ enum : uint32_t { FC_OK = 0, FC_DENSE = 1, FC_ABLATE = 2 };
 // The fast claims of interior tile t: writes the per-thread records (P.ent*) and P.claim[t], and
 // returns this thread's record (eb, en, ecn) and, in thread NT - 1, the claim. FC_DENSE: more than
 // FCAP live positions (the tile went to the general kernel's work list; nothing written).
+template <bool CF>
 __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const TileGeo &G, uint64_t t, FastLds &S,
                                                 uint32_t &eb_o, uint32_t &en_o, uint32_t &ecn_o, uint64_t &cl_o) {
 #if DRP_K1_GIMG
@@ -1270,7 +1271,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
         // The first field is checked here from the header's own bytes (no load): subset or key
         // (protocol-buffers writes fields in schema order), a length of <= 3 bytes, inside the
         // payload. ~99% of shadow headers stop here, so change_fills' loads are rare on C2.
-        if (DRP_CHANGE_FILLS && id == 1u && (DRP_CHANGE_FILLS == 2 || o < TILE || L > HALO) && L - 1u < (1u << 18)) {
+        if (CF && id == 1u && (DRP_CHANGE_FILLS == 2 || o < TILE || L > HALO) && L - 1u < (1u << 18)) {
           const uint32_t x = k + 1u < 4u ? __builtin_amdgcn_alignbit(wn, w, 8u * (k + 1u)) : wn;  // bytes k+1..k+4
           const uint32_t tg = x & 0xFFu, lt = ~(x >> 8) & 0x808080u;
           if ((tg == 0x0Au || tg == 0x12u) && lt) {
@@ -1301,7 +1302,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   // the parse's loads of later nodes from being issued together (C2: claims 2.8 -> 5.2 ms). Only
   // a wave whose bytes chain few frames inside the image runs it (C5: two real frames per tile,
   // their chains leave the image; C2: ~47 per wave, predicted without it).
-  if (wave_sum32(chained) < 16u) {
+  if (CF && wave_sum32(chained) < 16u) {
 #pragma unroll
     for (uint32_t j = 0; j < KPT; j++) {
       // (field headers may lie past the image, up to 512 bytes: a halo frame's key runs past it;
@@ -1492,6 +1493,10 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   return FC_OK;
 }
 
+// CF: with the structural check of frames that leave the image (long frames, C5). The host picks
+// the form from the frame density of the ctx's previous decode: dense streams (C2) are predicted
+// as well without it, and its code costs them ~4% (DESIGN.md "Long frames").
+template <bool CF>
 __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) {
   __shared__ FastLds S;
   const uint64_t t = blockIdx.x;
@@ -1504,7 +1509,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   }
   uint32_t eb, en, ecn;
   uint64_t cl;
-  (void)fast_claims(P, G, t, S, eb, en, ecn, cl);
+  (void)fast_claims<CF>(P, G, t, S, eb, en, ecn, cl);
 }
 
 // ==== kernel 2: exact entries, verification, frame counts =====================================
@@ -2646,9 +2651,14 @@ __global__ __launch_bounds__(256) void blob_bytes_kernel(const uint8_t *type, co
 // per-stream change / blob counts (one thread per stream)
 __global__ void stream_counts_kernel(const uint64_t *tile_prefix, uint64_t nstreams, const uint64_t *count,
                                      const uint64_t *base, const uint64_t *nch, const uint64_t *nch_base,
-                                     uint64_t *scount) {
+                                     uint64_t *scount, uint32_t *total) {
   const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nstreams) return;
+  if (total && s == nstreams - 1) {  // frames of the whole call (the host's density estimate)
+    const uint64_t nt = tile_prefix[nstreams];
+    const uint64_t f = nt ? base[nt - 1] + count[nt - 1] : 0;
+    *total = f > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)f;
+  }
   const uint64_t tf = tile_prefix[s], tl = tile_prefix[s + 1];
   uint64_t ch = 0, fr = 0;
   if (tl > tf) {
@@ -2693,11 +2703,11 @@ extern "C" hipError_t drp_launch_tile_scan(const uint64_t *in, const uint64_t *t
 
 extern "C" hipError_t drp_launch_stream_counts(const uint64_t *tile_prefix, uint64_t nstreams, const uint64_t *count,
                                                const uint64_t *base, const uint64_t *nch, const uint64_t *nch_base,
-                                               uint64_t *scount, hipStream_t st) {
+                                               uint64_t *scount, hipStream_t st, uint32_t *total) {
   if (nstreams == 0) return hipSuccess;
   const uint32_t blk = 256;
   hipLaunchKernelGGL(spec::stream_counts_kernel, dim3((uint32_t)((nstreams + blk - 1) / blk)), dim3(blk), 0, st,
-                     tile_prefix, nstreams, count, base, nch, nch_base, scount);
+                     tile_prefix, nstreams, count, base, nch, nch_base, scount, total);
   return hipGetLastError();
 }
 
@@ -2720,7 +2730,10 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
   }
 #if DRP_CLAIMS_FAST
   // interior tiles in the fast form; the edge and dense tiles it lists in the general one
-  hipLaunchKernelGGL(spec::claims_fast, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  if (DRP_CHANGE_FILLS && Q.change_checks)
+    hipLaunchKernelGGL(spec::claims_fast<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  else
+    hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
   const uint32_t gw = (uint32_t)(nt_max < 16384 ? nt_max : 16384);
   hipLaunchKernelGGL(spec::spec_claims, dim3(gw), dim3(spec::NT), 0, st, Q);
 #else
@@ -2795,7 +2808,7 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
   e = drp_launch_tile_scan(Q.tile_nch, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_nch_base, ~0ull, Q.overflow, st);
   if (e != hipSuccess) return e;
   return drp_launch_stream_counts(Q.tile_prefix, nstreams, Q.tile_count, Q.tile_base, Q.tile_nch, Q.tile_nch_base,
-                                  Q.scount, st);
+                                  Q.scount, st, Q.counter + 3);
 }
 
 extern "C" hipError_t drp_launch_blob_bytes(const uint8_t *type, const uint32_t *plen, uint64_t n, uint64_t *out,

@@ -69,6 +69,7 @@ struct DecodeParams {
   uint32_t *vlist_ovf;  // vlist is a dirty list: its overflow word (set: pass the overflow on, verify nothing)
   uint32_t *dstamp;     // per tile: the last pass id whose dirty list holds it (one entry per tile per list)
   uint32_t pass_id;     // this verify pass (1: the head's; zeroed stamps before it)
+  uint32_t change_checks;  // 1: claims_fast checks long frames' Change structure (drp_api.hip picks)
   int kstrong_hbm;      // 0: DRP_KSTRONG_HBM; else frames a deferred candidate must survive (tests)
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
   unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
@@ -114,7 +115,7 @@ hipError_t drp_launch_tile_scan(const uint64_t *in, const uint64_t *tile_prefix,
 // per-stream change / blob counts from the per-tile counts and their scans
 hipError_t drp_launch_stream_counts(const uint64_t *tile_prefix, uint64_t nstreams, const uint64_t *count,
                                     const uint64_t *base, const uint64_t *nch, const uint64_t *nch_base,
-                                    uint64_t *scount, hipStream_t st);
+                                    uint64_t *scount, hipStream_t st, uint32_t *total = nullptr);
 hipError_t drp_launch_finalize(const uint8_t *bytes, const uint64_t *stream_off, uint64_t nstreams,
                                const uint64_t *tile_prefix, const uint64_t *tile_exit,
                                const uint64_t *tile_base, const uint64_t *tile_count,

@@ -221,7 +221,7 @@ def test_c3_many_blobs(ctx):
     assert_same(g, O.decode_batch(wire, chunk=65536), "c3x40")
 
 
-def test_c5_predicted_without_repairs(ctx):
+def test_c5_predicted_without_repairs():
     """A 200K-Change C5 stream (random 4 KB values, keys of 1..256 bytes) is predicted without a
     single miss: no repair pass, no exact re-run (C5's long frames are strong by structure,
     DESIGN.md "Long frames"), and the decode is bit-exact with the encoder's input. The repair
@@ -234,6 +234,9 @@ def test_c5_predicted_without_repairs(ctx):
     from _gpu import drp_amd
     dev = torch.device("cuda", 0)
     n = 200_000
+    # a ctx of its own: the structural check of long frames is chosen from the ctx's previous
+    # decodes (dense streams leave it off), and this one decodes C5 from the start
+    ctx = drp_amd.Ctx(0)
     cols, heap, frame = bench.c5_on_device(n, seed=55, dev=dev)
     W = int(frame.sum())
     out = torch.zeros(W + 64, dtype=torch.uint8, device=dev)
@@ -247,6 +250,7 @@ def test_c5_predicted_without_repairs(ctx):
     t = ctx.timing()
     print(f"repair passes {t.spec_repairs}, exact re-runs {t.strict_reruns}")
     bench.verify_c5(cols, heap, wire, outs, res, n, dev, samples=64)
+    ctx.close()
     assert t.strict_reruns == 0 and t.spec_repairs == 0, (t.spec_repairs, t.strict_reruns)
 
 
