@@ -2604,7 +2604,10 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
       const uint64_t lim = umin64(G.A + TILE, send);
       uint32_t ok = 1;
       p = q;
-      // seg_advance, keeping the records of the chain's frames in this tile
+      // seg_advance, keeping the records of the chain's frames in this tile: positions rise, so
+      // the current thread's record is kept in registers and written once when the chain leaves
+      // its bytes (LDS writes only: no read-modify-write on the walk's serial path)
+      uint32_t cth = NT, ce = 0, cn = 0, cc = 0;
       while (is_pos(p) && p < lim && p < m.se) {
         const Hdr h = hdr_fast(m, p);
         if (h.kind != H_VALID) {
@@ -2613,12 +2616,25 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
           break;
         }
         const uint32_t o = (uint32_t)(p - G.A), th = o / SEGB;
-        if (re[th] == 0xFF) re[th] = (uint8_t)(o % SEGB);
-        if (h.id != 0) {
-          rn[th]++;
-          if (h.id == 1) rc[th]++;
+        if (th != cth) {
+          if (cth < NT) {
+            re[cth] = (uint8_t)ce;
+            rn[cth] = (uint8_t)cn;
+            rc[cth] = (uint8_t)cc;
+          }
+          cth = th;
+          ce = o % SEGB;
+          cn = 0;
+          cc = 0;
         }
+        cn += h.id != 0;
+        cc += h.id == 1;
         p = h.succ;
+      }
+      if (cth < NT) {
+        re[cth] = (uint8_t)ce;
+        rn[cth] = (uint8_t)cn;
+        rc[cth] = (uint8_t)cc;
       }
       // the tile's claim: the first chain position past it, or where the chain ends in it
       lcl[u - ta] = (p & MARK_TERM) ? (p & ~M_ERR) : p;
