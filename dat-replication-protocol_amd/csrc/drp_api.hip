@@ -1206,10 +1206,14 @@ static int stage_src(drp_ctx *c, const drp_change_src *src, const uint8_t *heap,
   const size_t need = al(heap_bytes + 16) + 10 * al(n * 8 + 8);
   if (!c->in_stage.ensure(need)) return DRP_E_NOMEM;
   size_t o = 0;
+  hipError_t copy_err = hipSuccess;  // first failed staging copy, returned below
   auto put = [&](const void *h, size_t bytes) -> void * {
     void *d = c->in_stage.at<char>(o);
     o += al(bytes + 8);
-    if (bytes) hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->st);
+    if (bytes) {
+      const hipError_t e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->st);
+      if (copy_err == hipSuccess) copy_err = e;
+    }
     return d;
   };
   dheap = (const uint8_t *)put(heap, heap_bytes);
@@ -1223,6 +1227,7 @@ static int stage_src(drp_ctx *c, const drp_change_src *src, const uint8_t *heap,
   dsrc.from = (const uint64_t *)put(src->from, n * 8);
   dsrc.to = (const uint64_t *)put(src->to, n * 8);
   dsrc.flags = (const uint8_t *)put(src->flags, n);
+  CHK(copy_err);
   CHK(hipGetLastError());
   return DRP_OK;
 }
