@@ -120,6 +120,10 @@ function Decoder (opts) {
   this._blob = null       // the open BlobStream
   this._res = null        // decoded batch being replayed
   this._buf = null        // its bytes
+  this._chunks = null     // the written chunks it was made of, and where each starts in it
+  this._starts = null
+  this._ck = 0            // the chunk holding the blob bytes delivered next
+  this._blobPos = -1      // batch offset of the next piece of a blob row being delivered
   this._text = null       // its bytes as one latin1 string (ASCII keys are cut from it)
   this._tooBig = 0        // its carried Change frame was larger than a Buffer can hold
   this._next = 0          // next frame to deliver
@@ -164,7 +168,10 @@ Decoder.prototype._write = function (data, enc, cb) {
   this._queue.push(data)
   this._queued += data.length
   if (this._queued >= MAX_BATCH) {
-    this._held = cb // backpressure: acknowledged once this batch has been delivered
+    // backpressure: acknowledged once every queued byte has been handed to the GPU (_kick), so at
+    // most one batch on the GPU, one decoded and waiting, one replaying and MAX_BATCH queued bytes
+    // are held in memory at a time
+    this._held = cb
     return this._kick()
   }
   cb()
@@ -238,17 +245,24 @@ Decoder.prototype._kick = function () {
     this._carry = null
   }
   var batch = chunks.length === 1 ? chunks[0] : Buffer.concat(chunks)
+  // where each chunk starts in the batch: blob payloads are delivered as slices of the written
+  // chunks themselves (decode.js:179-202 slices the chunk it was given), not of the batch copy
+  var starts = new Array(chunks.length)
+  for (var j = 0, at = 0; j < chunks.length; j++) {
+    starts[j] = at
+    at += chunks[j].length
+  }
   this._inflight = true
   var held = this._queued ? null : this._held // all of its bytes are on their way to the GPU now
   if (held) this._held = null
   var self = this
   native.decode(this._ctx, batch, this._blobLeft, function (err, res) {
-    self._ondecoded(err, res, batch)
+    self._ondecoded(err, res, batch, chunks, starts)
   }, this._keyPost)
   if (held) held()
 }
 
-Decoder.prototype._ondecoded = function (err, res, batch) {
+Decoder.prototype._ondecoded = function (err, res, batch, chunks, starts) {
   this._inflight = false
   if (this.destroyed) return
   if (err) return this.destroy(err)
@@ -281,7 +295,7 @@ Decoder.prototype._ondecoded = function (err, res, batch) {
     tm.h2dBytes += t.h2dBytes || 0
     tm.h2dSkipped += t.h2dSkipped || 0
   }
-  var entry = { res: res, buf: batch, tooBig: tooBig }
+  var entry = { res: res, buf: batch, chunks: chunks, starts: starts, tooBig: tooBig }
   if (this._res) {
     this._ready = entry
     return
@@ -294,6 +308,10 @@ Decoder.prototype._play = function (e) {
   var batch = e.buf
   this._res = res
   this._buf = batch
+  this._chunks = e.chunks
+  this._starts = e.starts
+  this._ck = 0
+  this._blobPos = -1
   this._tooBig = e.tooBig
   this._text = res.asciiKeys && batch.length <= TEXT_MAX && batch.length <= TEXT_PER_FRAME * res.n
     ? batch.toString('latin1') : null
@@ -330,8 +348,7 @@ Decoder.prototype._replay = function () {
   // (no callback can re-enter this loop: _down only resumes a paused replay)
   while (i < n && this._pending <= 0) {
     if ((type[i] & TYPE_MASK) !== 1) {
-      this._deliverBlob(i)
-      i++
+      if (this._deliverBlob(i)) i++ // (one push per written chunk the payload spans)
       if (this.destroyed) break
       continue
     }
@@ -370,6 +387,8 @@ Decoder.prototype._replay = function () {
   }
   this._res = null
   this._buf = null
+  this._chunks = null
+  this._starts = null
   this._text = null
   var next = this._ready
   this._ready = null
@@ -377,25 +396,42 @@ Decoder.prototype._replay = function () {
   else this._kick()
 }
 
-// blob frame (or the continuation of one opened in an earlier batch)
+// One piece of blob frame i (or of the continuation of one opened in an earlier batch): the
+// part of its payload inside the next written chunk, pushed as a slice of that chunk with one
+// callback, as _onblobdata pushes each chunk's part (decode.js:179-202); true once the frame's
+// last piece is delivered (and the blob ended, unless it continues past the batch).
 Decoder.prototype._deliverBlob = function (i) {
   var res = this._res
-  var buf = this._buf
   var type = res.type[i]
   var off = res.off[i]
-  if (!(type & CONT)) {
-    this.blobs++
-    this._blob = new BlobStream(this)
-    this._onblob(this._blob, this._down)
+  var end = off + Math.min(res.len[i], this._buf.length - off)
+  var pos = this._blobPos
+  if (pos < 0) {
+    pos = off
+    if (!(type & CONT)) {
+      this.blobs++
+      this._blob = new BlobStream(this)
+      this._onblob(this._blob, this._down)
+    }
   }
-  var avail = Math.min(res.len[i], buf.length - off)
+  var chunks = this._chunks
+  var starts = this._starts
+  var k = this._ck
+  while (k + 1 < chunks.length && starts[k + 1] <= pos) k++
+  this._ck = k
+  var stop = Math.min(end, starts[k] + chunks[k].length)
+  var data = pos < stop ? chunks[k].slice(pos - starts[k], stop - starts[k]) : this._buf.slice(pos, pos)
   var blob = this._blob
-  if (!(type & PARTIAL)) {
-    this._pending++ // released by the handler's cb (decode.js:171-177)
+  var last = stop >= end
+  this._blobPos = last ? -1 : stop
+  blob._push(data, this._up())
+  if (!last) return false
+  if (!(type & PARTIAL)) { // decode.js:171-177
+    this._pending++ // released by the blob handler's cb
     this._blob = null
+    blob._end()
   }
-  blob._push(buf.slice(off, off + avail), this._up())
-  if (!(type & PARTIAL)) blob._end()
+  return true
 }
 
 module.exports = Decoder

@@ -6,7 +6,8 @@
 //   mode "digest": events carry sha256 of keys/values/blob data instead of hex
 //   mode "keyhash": decode({keyHash: true}); change events also carry keyHash (decimal)
 //   mode "ticks": one write per event-loop turn (synchronous acks)
-//   mode "h2d": digest events, then one {t: 'timing'} record with the decoder's byte counters
+//   mode "h2d": digest events, then one {t: 'timing'} record with the decoder's byte counters and
+//               how many blob pieces were slices of the written chunks
 // DRP_MAX_BATCH in the environment sets the decoder's batch threshold
 'use strict'
 var fs = require('fs')
@@ -42,9 +43,15 @@ d.change(function (c, cb) {
   }
   if (asyncAck) setImmediate(cb); else cb()
 })
+var pieces = 0
+var shared = 0 // blob pieces that are slices of the written chunks (no copy: decode.js:179-202)
 d.blob(function (b, cb) {
   var parts = []
-  b.on('data', function (x) { parts.push(x) })
+  b.on('data', function (x) {
+    parts.push(x)
+    pieces++
+    if (x.buffer === wire.buffer) shared++
+  })
   b.on('end', function () {
     var data = Buffer.concat(parts)
     out.push({ t: 'blob', data: enc(data), len: data.length })
@@ -55,7 +62,10 @@ d.on('error', function (e) { out.push({ t: 'error', message: e.message }); done(
 d.on('close', function () { out.push({ t: 'close' }) })
 d.on('finish', function () {
   out.push({ t: 'finish', changes: d.changes, blobs: d.blobs, bytes: d.bytes })
-  if (mode === 'h2d') out.push({ t: 'timing', h2dBytes: d.timing.h2dBytes, h2dSkipped: d.timing.h2dSkipped })
+  if (mode === 'h2d') {
+    out.push({ t: 'timing', h2dBytes: d.timing.h2dBytes, h2dSkipped: d.timing.h2dSkipped,
+      blobPieces: pieces, blobPiecesShared: shared })
+  }
   done()
 })
 var printed = false

@@ -238,8 +238,9 @@ def test_c3_blobs_through_the_package():
 def test_c3_blob_payloads_stay_in_host_memory():
     """SURVEY §8 f2 through the Node path: a C3-shaped stream (100 units of 1000 C2 frames + a
     1 MiB blob, ~113 MB) in 1 MiB writes; the addon stages the decoder's batches in pieces that
-    skip blob payloads, so at most 25% of the wire is copied into HBM, and every event still
-    equals the oracle's."""
+    skip blob payloads, so at most 25% of the wire is copied into HBM, every blob piece handed to
+    the blob stream is a slice of a written chunk (no host copy, decode.js:179-202), and every
+    event still equals the oracle's."""
     wire = S.c3_stream(random.Random(12), 100, frames_per_unit=1000)
     r, exp = oracle_events(wire, digest=True)
     out = [e for e in run_js(wire, str(1 << 20), "h2d") if e["t"] != "close"]
@@ -250,6 +251,7 @@ def test_c3_blob_payloads_stay_in_host_memory():
     print(f"staged {tm['h2dBytes']} B of {len(wire)} ({tm['h2dBytes'] / len(wire):.1%}), "
           f"skipped {tm['h2dSkipped']} B")
     assert tm["h2dBytes"] <= len(wire) // 4, tm
+    assert tm["blobPieces"] >= r["blobs"] and tm["blobPiecesShared"] == tm["blobPieces"], tm
 
 
 @pytest.mark.gpu
@@ -393,6 +395,22 @@ def test_js_layer_batch_edges_cpu():
             got = [e for e in run_js(wire, sizes, mode, batch=64, mock=True) if e["t"] != "close"]
             assert got[:-1] == exp, (sizes, mode)
             assert got[-1] == {"t": "finish", "changes": r["changes"], "blobs": r["blobs"], "bytes": len(wire)}
+
+
+@needs_node
+@pytest.mark.parametrize("sizes,mode,batch", [("65536", "h2d", None), ("4093,1,65536", "h2d", 1 << 18),
+                                              ("1000", "h2d", 4096)])
+def test_js_layer_blob_pieces_are_write_slices_cpu(sizes, mode, batch):
+    """SURVEY §8 f2 on CPU (mock addon): blob payloads reach the blob stream as slices of the
+    written chunks, one piece per chunk a payload spans (decode.js:179-202 pushes each _write's
+    part), never as slices of the coalesced batch copy; the events equal the oracle's."""
+    wire = S.c3_stream(random.Random(5), 3, frames_per_unit=300, blob_len=200_000)
+    r, exp = oracle_events(wire, digest=True)
+    out = [e for e in run_js(wire, sizes, mode, batch=batch, mock=True) if e["t"] != "close"]
+    tm = out.pop()
+    assert out[:-1] == exp
+    assert out[-1] == {"t": "finish", "changes": r["changes"], "blobs": r["blobs"], "bytes": len(wire)}
+    assert tm["blobPieces"] > r["blobs"] and tm["blobPiecesShared"] == tm["blobPieces"], tm
 
 
 @needs_node
