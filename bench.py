@@ -254,6 +254,18 @@ def node_path(frames=4_000_000, reps=3):
                 {"error": (r.stderr or r.stdout)[-400:]}
     finally:
         os.unlink(path)
+    # the Encoder (encode.js over the addon): change() calls -> GPU encode per tick batch -> a
+    # discarding sink; the reference's own encoder measured in the build container (BASELINE.md,
+    # shim codec): 0.19 M frames/s for 1M x 64 B values, 0.14 M frames/s for 200k x 4 KB values
+    for name, shape, rows, ref in [("encode_c1", "c1", 1_000_000, 0.19e6), ("encode_c5", "c5", 200_000, 0.14e6)]:
+        r = subprocess.run([node, os.path.join(ROOT, "scripts", "bench_node_encode.js"), shape, str(rows), "3"],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode == 0:
+            out[name] = json.loads(r.stdout.strip().splitlines()[-1])
+            out[name]["reference_js_container_frames_per_s"] = ref
+            out[name]["vs_reference_js_container"] = out[name]["frames_per_s"] / ref
+        else:
+            out[name] = {"error": (r.stderr or r.stdout)[-400:]}
     return out
 
 
@@ -358,12 +370,14 @@ def verify_c5(cols, heap, wire, o, res, n, dev, samples=256):
             assert torch.equal(wire[po + off_w:po + off_w + ln], heap[off_h:off_h + ln]), i
 
 
-def main_c5(args, dev, rank=0, world=1):
-    """--workload c5: batched encode -> decode round trip of 1M Changes with 4 KB values per
-    step per GPU (BASELINE configs[4]: 8 x MI355X); each rank round-trips its own rows (weak
-    scaling), then the 32 B per-stream stats are all-gathered (drp_index_allgather over RCCL; gloo
-    only to rehearse ranks on one GPU). value = Changes round-tripped per second, whole job."""
+def run_c5(args, dev, rank=0, world=1, steps=None, warmup=None, cpu=True):
+    """C5: batched encode -> decode round trip of 1M Changes with 4 KB values per step per GPU
+    (BASELINE configs[4]: 8 x MI355X); each rank round-trips its own rows (weak scaling), then the
+    32 B per-stream stats are all-gathered (drp_index_allgather over RCCL; gloo only to rehearse
+    ranks on one GPU). value = Changes round-tripped per second, whole job. Returns rank 0's line."""
     dist = world > 1
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
     n = args.c5_changes
     cols, heap, frame = c5_on_device(n, seed=55 + rank, dev=dev)
     W = int(frame.sum())
@@ -397,7 +411,7 @@ def main_c5(args, dev, rank=0, world=1):
             enc_ms.append(evs[0].elapsed_time(evs[1]))
             dec_ms.append(evs[1].elapsed_time(evs[2]))
 
-    for _ in range(max(1, args.warmup)):
+    for _ in range(max(1, warmup)):
         step(False)
     torch.cuda.synchronize(dev)
     assert int(foff[n]) == W, (int(foff[n]), W)
@@ -408,7 +422,7 @@ def main_c5(args, dev, rank=0, world=1):
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step(True)
     torch.cuda.synchronize(dev)
     if dist:
@@ -427,31 +441,157 @@ def main_c5(args, dev, rank=0, world=1):
               "gloo all-gather of the 32 B stream stats + index scan") if dist else "no collective (1 GPU)"
     out_line = {
         "metric": f"round-tripped Change frames/sec (batched encode + decode), {world} MI355X",
-        "value": n * world * args.steps / elapsed, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "value": n * world * steps / elapsed, "unit": "frames/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic: C5 columns + heap generated on device (seeded per rank), resident in HBM",
         "config": {"workload": f"C5: {n} Changes per GPU, 4096 B values, key U[1,256], change/from/to U[0,2^32)",
                    "wire_bytes_per_gpu": W, "heap_bytes_per_gpu": H,
                    "parallelism": f"one stream per GPU, {world} GPU(s); {gather}"},
-        "wire_GBps": 2 * W * world * args.steps / elapsed / 1e9,
+        "wire_GBps": 2 * W * world * steps / elapsed / 1e9,
         "roofline": {"bound": "hbm", "achieved": (b_enc + b_dec) / (e + d) / 1e9, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": (b_enc + b_dec) / (e + d) / 1e9 / HBM_PEAK_GBPS,
-                     "traffic": None, "kernel": "encode (enc_size, enc_scan, enc_write) + speculative decode",
+                     "traffic": traffic_from_profile("c5", n), "traffic_source": TRAFFIC_SOURCE % "c5",
+                     "kernel": "encode (enc_size, enc_scan, enc_write) + speculative decode",
                      "bytes_model": "encode 49*C + H + W, decode W + 13*F + 49*C (rank 0)"},
         "encode": {"ms": e * 1e3, "GBps": b_enc / e / 1e9, "frac": b_enc / e / 1e9 / HBM_PEAK_GBPS},
         "decode": {"ms": d * 1e3, "GBps": b_dec / d / 1e9, "frac": b_dec / d / 1e9 / HBM_PEAK_GBPS,
                    "exact_fallbacks": t.strict_reruns, "repair_passes": t.spec_repairs,
                    "segmented_repairs": t.seg_repairs},
     }
-    if rank == 0:
-        if world == 1 and not args.no_cpu:
-            out_line["cpu_baseline"] = cpu_baseline_c5()
-        print(json.dumps(out_line), flush=True)
-    drp_dist.close_comms()
+    if rank == 0 and world == 1 and cpu and not args.no_cpu:
+        out_line["cpu_baseline"] = cpu_baseline_c5()
     ctx.close()
+    del cols, heap, out, outs, foff
+    torch.cuda.empty_cache()
+    return out_line if rank == 0 else None
+
+
+def run_decode(args, dev, rank, world, workload, steps, warmup):
+    """C2 (one 8.6 GB stream per GPU) or C4 (8192 independent streams sharded over the ranks):
+    `steps` timed decodes after `warmup`, each followed for N > 1 by the all-gather of the 32 B
+    per-stream stats and the global index scan. Returns rank 0's line (no CPU legs)."""
+    dist = world > 1
+    if workload == "c2":
+        nframes = args.frames
+        wire = c2_on_device(nframes, seed=1234 + rank, dev=dev)
+        stream_off = torch.tensor([0, wire.numel()], dtype=torch.int64, device=dev)
+        counts, (lo, _) = np.array([nframes]), (rank, rank + 1)
+        nstreams_total = world
+    else:
+        wire, stream_off, counts, (lo, _) = c4_on_device(args.streams, rank, world, dev)
+        nframes = int(counts.sum())
+        nstreams_total = args.streams
+    nlocal = stream_off.numel() - 1
+    cap = nframes + 64
+    outs = alloc_outputs(cap, dev)
+    res = torch.zeros(nlocal * C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+
+    ctx = drp_amd.Ctx(dev.index, tile=args.tile)
+    state = {"base": None}
+
+    def step():
+        ctx.decode_device(wire, stream_off, None, outs, cap, res)
+        if dist:  # the only collective: all-gather of 32-byte per-stream stats
+            stats = drp_dist.local_stats_device(ctx, res, stream_off)
+            if args.backend == "nccl":  # libdrp's RCCL communicator over xGMI (drp_index_allgather)
+                _, state["base"] = drp_dist.global_index_rccl(ctx, stats, nstreams_total)
+            else:  # gloo rehearsal of several ranks on one GPU
+                table = drp_dist.gather_stats(stats, nstreams_total)
+                state["base"] = drp_dist.global_index_device(ctx, table)
+
+    for _ in range(max(1, warmup)):
+        step()
+    if workload == "c2":
+        verify_c2(outs, res, nframes, dev)
+    else:
+        verify_c4(outs, res, counts, state["base"], lo, dev)
+
+    ext = torch.cuda.ExternalStream(ctx.stream, device=dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
-        torch.distributed.destroy_process_group()
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    dec_ms, fallbacks, repairs, relisted = [], 0, 0, 0
+    t0 = time.perf_counter()
+    ev0.record(ext)
+    for _ in range(steps):
+        step()
+        t = ctx.timing()
+        dec_ms.append(t.decode_ms)
+        fallbacks += t.strict_reruns
+        repairs += t.spec_repairs
+        relisted += t.verify_relisted
+    ev1.record(ext)
+    torch.cuda.synchronize(dev)
+    if dist:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    frames_all = torch.tensor([float(nframes)], dtype=torch.float64, device=dev)
+    if dist:
+        cdev = dev if args.backend == "nccl" else torch.device("cpu")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        frames_all = frames_all.to(cdev)
+        torch.distributed.all_reduce(frames_all)
+    frames_node = int(frames_all.item())
+    ctx.close()
+    del wire, outs, res
+    torch.cuda.empty_cache()
+    if rank != 0:
+        return None
+
+    frames_total = frames_node * steps
+    wire_total = frames_node * FRAME * steps
+    ms_per_step = elapsed / steps * 1e3
+    dec_avg_s = float(np.mean(dec_ms)) / 1e3
+    b_dec = nframes * FRAME + 13 * nframes + 49 * nframes  # W + 13F + 49C (SURVEY §8d), this GPU
+    achieved = b_dec / dec_avg_s / 1e9
+    tile = args.tile or 8192
+    exact = os.environ.get("DRP_DECODE") == "exact"
+    kname = (f"decode_tiles<{tile // 64}>" if exact else
+             "speculative decode: claims_fast + verify_lite + tile scans + emit_tiles")
+    gather = ("; drp_index_allgather (RCCL) of 32 B stream stats + index scan" if args.backend == "nccl" else
+              "; gloo all-gather of 32 B stream stats + index scan") if dist else "; no collective (1 GPU)"
+    if workload == "c2":
+        config = {"workload": f"C2: {nframes / 1e6:g}M Change frames x 86 B (64 B values), one "
+                              f"{nframes * FRAME / 1e9:.2f} GB stream per GPU",
+                  "frames_per_gpu": nframes, "wire_bytes_per_gpu": nframes * FRAME,
+                  "parallelism": f"replicas: one stream per GPU, {world} GPU(s){gather}"}
+    else:
+        config = {"workload": f"C4: {nstreams_total} independent streams of U[8192,16384] C2 frames, "
+                              f"contiguous shards over {world} GPU(s)",
+                  "frames_node": frames_node, "streams": nstreams_total,
+                  "parallelism": f"stream shards, {world} GPU(s){gather}"}
+    config["tile_bytes"] = tile
+    return {
+        "metric": "decoded Change frames/sec + wire GB/s (whole node) at 1/2/4/8 MI355X",
+        "value": frames_total / elapsed,
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: C2-shaped generator on device (seeded), resident in HBM before timing",
+        "config": config,
+        "wire_GBps": wire_total / elapsed / 1e9,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profile(workload, nframes),
+                     "traffic_source": TRAFFIC_SOURCE % workload,
+                     "kernel": kname, "kernel_ms": dec_avg_s * 1e3,
+                     "exact_fallbacks": fallbacks, "repair_passes": repairs,
+                     "verify_relisted_tiles": relisted // max(1, steps),
+                     "bytes_per_launch": b_dec,
+                     "bytes_model": "W + 13*frames + 49*changes (86+13+49 = 148 B/frame)"},
+        "step_ms_hip_events": ev_ms / steps,
+    }
 
 
 def main():
@@ -463,6 +603,8 @@ def main():
     ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2")
     ap.add_argument("--c5-changes", type=int, default=1_000_000, help="C5 Changes per step")
     ap.add_argument("--streams", type=int, default=8192, help="C4 streams across all GPUs")
+    ap.add_argument("--sub-steps", type=int, default=5, help="timed steps of the c4/c5 sub-lines")
+    ap.add_argument("--no-sub", action="store_true", help="C2 only: no c4/c5 sub-lines")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse "
@@ -494,155 +636,55 @@ def main():
             torch.distributed.init_process_group(args.backend)
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    cpu = world == 1 and rank == 0 and not args.no_cpu
 
     if args.workload == "c5":
-        return main_c5(args, dev, rank, world)
-    if args.workload == "c2":
-        nframes = args.frames
-        wire = c2_on_device(nframes, seed=1234 + rank, dev=dev)
-        stream_off = torch.tensor([0, wire.numel()], dtype=torch.int64, device=dev)
-        counts, (lo, _) = np.array([nframes]), (rank, rank + 1)
-        nstreams_total = world
+        out = run_c5(args, dev, rank, world)
     else:
-        wire, stream_off, counts, (lo, _) = c4_on_device(args.streams, rank, world, dev)
-        nframes = int(counts.sum())
-        nstreams_total = args.streams
-    nlocal = stream_off.numel() - 1
-    cap = nframes + 64
-    outs = alloc_outputs(cap, dev)
-    res = torch.zeros(nlocal * C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize(dev)
-
-    ctx = drp_amd.Ctx(dev.index, tile=args.tile)
-    state = {"base": None}
-
-    def step():
-        ctx.decode_device(wire, stream_off, None, outs, cap, res)
-        if dist:  # the only collective: all-gather of 32-byte per-stream stats
-            stats = drp_dist.local_stats_device(ctx, res, stream_off)
-            if args.backend == "nccl":  # libdrp's RCCL communicator over xGMI (drp_index_allgather)
-                _, state["base"] = drp_dist.global_index_rccl(ctx, stats, nstreams_total)
-            else:  # gloo rehearsal of several ranks on one GPU
-                table = drp_dist.gather_stats(stats, nstreams_total)
-                state["base"] = drp_dist.global_index_device(ctx, table)
-
-    for _ in range(max(1, args.warmup)):
-        step()
-    if args.workload == "c2":
-        verify_c2(outs, res, nframes, dev)
-    else:
-        verify_c4(outs, res, counts, state["base"], lo, dev)
-
-    ext = torch.cuda.ExternalStream(ctx.stream, device=dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if dist:
-        torch.distributed.barrier()
-    torch.cuda.synchronize(dev)
-    dec_ms, fallbacks, repairs, relisted = [], 0, 0, 0
-    t0 = time.perf_counter()
-    ev0.record(ext)
-    for _ in range(args.steps):
-        step()
-        t = ctx.timing()
-        dec_ms.append(t.decode_ms)
-        fallbacks += t.strict_reruns
-        repairs += t.spec_repairs
-        relisted += t.verify_relisted
-    ev1.record(ext)
-    torch.cuda.synchronize(dev)
-    if dist:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    ev_ms = ev0.elapsed_time(ev1)
-    frames_all = torch.tensor([float(nframes)], dtype=torch.float64, device=dev)
-    if dist:
-        cdev = dev if args.backend == "nccl" else torch.device("cpu")
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        frames_all = frames_all.to(cdev)
-        torch.distributed.all_reduce(frames_all)
-    frames_node = int(frames_all.item())
-
-    frames_total = frames_node * args.steps
-    wire_total = frames_node * FRAME * args.steps
-    ms_per_step = elapsed / args.steps * 1e3
-    dec_avg_s = float(np.mean(dec_ms)) / 1e3
-    b_dec = nframes * FRAME + 13 * nframes + 49 * nframes  # W + 13F + 49C, this GPU
-    achieved = b_dec / dec_avg_s / 1e9
-    tile = args.tile or 8192
-    exact = os.environ.get("DRP_DECODE") == "exact"
-    kname = (f"decode_tiles<{tile // 64}>" if exact else
-             "speculative decode: claims_fast + verify_lite + tile scans + emit_tiles")
-    gather = ("; drp_index_allgather (RCCL) of 32 B stream stats + index scan" if args.backend == "nccl" else
-              "; gloo all-gather of 32 B stream stats + index scan") if dist else "; no collective (1 GPU)"
-    if args.workload == "c2":
-        workload = {"workload": f"C2: {nframes / 1e6:g}M Change frames x 86 B (64 B values), one "
-                                f"{nframes * FRAME / 1e9:.2f} GB stream per GPU",
-                    "frames_per_gpu": nframes, "wire_bytes_per_gpu": nframes * FRAME,
-                    "parallelism": f"replicas: one stream per GPU, {world} GPU(s){gather}"}
-    else:
-        workload = {"workload": f"C4: {nstreams_total} independent streams of U[8192,16384] C2 frames, "
-                                f"contiguous shards over {world} GPU(s)",
-                    "frames_node": frames_node, "streams": nstreams_total,
-                    "parallelism": f"stream shards, {world} GPU(s){gather}"}
-    workload["tile_bytes"] = tile
-
-    if rank == 0:
-        out = {
-            "metric": "decoded Change frames/sec + wire GB/s (whole node) at 1/2/4/8 MI355X",
-            "value": frames_total / elapsed,
-            "unit": "frames/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic: C2-shaped generator on device (seeded), resident in HBM before timing",
-            "config": workload,
-            "wire_GBps": wire_total / elapsed / 1e9,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profile(kname, nframes),
-                         "traffic_source": "not measured in this run: profiles/pmc_decode.json (rocprofv3 "
-                                           "FETCH_SIZE x2 + WRITE_SIZE per frame, separate --pmc passes of "
-                                           "scripts/gpu_pmc.sh on a 20M-frame C2 launch) x this launch's frames",
-                         "kernel": kname, "kernel_ms": dec_avg_s * 1e3,
-                         "exact_fallbacks": fallbacks, "repair_passes": repairs,
-                         "verify_relisted_tiles": relisted // max(1, args.steps),
-                         "bytes_per_launch": b_dec,
-                         "bytes_model": "W + 13*frames + 49*changes (86+13+49 = 148 B/frame)"},
-            "step_ms_hip_events": ev_ms / args.steps,
-        }
-        if world == 1 and not args.no_cpu:
+        out = run_decode(args, dev, rank, world, args.workload, args.steps, args.warmup)
+        if cpu:
             if args.workload == "c2":
                 out["cpu_baseline"] = cpu_baseline()
                 out["cpu_baseline_all_cores"] = cpu_baseline_streams()
             else:
                 out["cpu_baseline"] = cpu_baseline_streams()
+        if args.workload == "c2" and not args.no_sub:
+            # BASELINE configs[3] and [4] as sub-lines of the same run (own timing, roofline and
+            # CPU baseline); the top-level value stays C2's
+            c4 = run_decode(args, dev, rank, world, "c4", args.sub_steps, args.warmup)
+            c5 = run_c5(args, dev, rank, world, steps=args.sub_steps, warmup=args.warmup, cpu=cpu)
+            if rank == 0:
+                if cpu:
+                    c4["cpu_baseline"] = out["cpu_baseline_all_cores"]
+                for k in ("metric", "higher_is_better", "scaling", "vs_baseline", "dtype", "n_gpus"):
+                    c4.pop(k, None)
+                    c5.pop(k, None)
+                out["c4"], out["c5"] = c4, c5
+        if cpu:
             out["h2d"] = h2d_rate(dev)
             if args.workload == "c2":
                 out["node_path"] = node_path()
+    if rank == 0:
         print(json.dumps(out), flush=True)
     drp_dist.close_comms()
-    ctx.close()
     if dist:
         torch.distributed.destroy_process_group()
 
 
-def traffic_from_profile(kname, nframes):
-    """HBM bytes per decode from the committed rocprofv3 PMC summary of this decode path
-    (FETCH_SIZE x2 + WRITE_SIZE per frame summed over its kernels, guide §HBM, measured on a
-    C2 launch by scripts/gpu_pmc.sh), times this launch's frames; None if absent or stale."""
-    p = os.path.join(ROOT, "profiles", "pmc_decode.json")
+TRAFFIC_SOURCE = ("not measured in this run: profiles/pmc_%s.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per "
+                  "frame over the path's kernels, separate --pmc passes of scripts/gpu_pmc.sh) x this launch's frames")
+
+
+def traffic_from_profile(workload, nframes):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload's decode
+    path (profiles/pmc_<workload>.json: FETCH_SIZE x2 + WRITE_SIZE per frame summed over the
+    path's kernels, guide §HBM), times this launch's frames; None when no such summary exists
+    (a per-frame figure of one workload is never applied to another)."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     try:
         with open(p) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
-    if d.get("kernel") != kname:
         return None
     return d["hbm_bytes_per_frame"] * nframes if d.get("hbm_bytes_per_frame") else None
 

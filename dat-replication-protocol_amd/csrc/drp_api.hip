@@ -39,7 +39,7 @@ struct DevBuf {
   size_t cap = 0;
   bool ensure(size_t n) {
     if (n <= cap) return true;
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
     size_t want = n + n / 4 + 4096;
@@ -48,7 +48,7 @@ struct DevBuf {
     return true;
   }
   void release() {
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
   }
@@ -91,6 +91,14 @@ struct drp_ctx {
   int change_checks = 1, change_checks_env = -1;
   int cus = 256;
   uint32_t waves_per_cu = 16;
+  // test / measurement knobs, read once by drp_open (never on a decode): DRP_KSTRONG_HBM weakens
+  // predictions, DRP_DIRTY_CAP caps the repair dirty lists, DRP_STATS / DRP_TRACE_FILE collect
+  // kernel counters and per-tile traces into dstats (allocated here when asked for)
+  uint32_t kstrong_hbm = 0;
+  uint64_t dirty_cap = ~0ull;
+  bool stats = false;
+  const char *trace_file = nullptr;
+  unsigned long long *dstats = nullptr;
   DevBuf scratch, in_stage, out_stage, aux;
   DevBuf dec_cols;  // device columns of the staged host-batch decode (drp_decode_stage)
   double frames_per_byte = 0;  // density of the last staged batch (sizes the next one's columns)
@@ -164,20 +172,26 @@ int drp_open(int device, drp_ctx **out) {
     int v = atoi(w);
     if (v > 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
   }
+  if (const char *e = getenv("DRP_KSTRONG_HBM")) c->kstrong_hbm = (uint32_t)atoi(e);
+  if (const char *e = getenv("DRP_DIRTY_CAP")) c->dirty_cap = strtoull(e, nullptr, 10);
+  c->trace_file = getenv("DRP_TRACE_FILE");
+  if (getenv("DRP_STATS") && hipMalloc((void **)&c->dstats, 64 * 8) == hipSuccess) c->stats = true;
   *out = c;
   return DRP_OK;
 }
 
 void drp_close(drp_ctx *c) {
   if (!c) return;
-  hipSetDevice(c->device);
-  hipStreamSynchronize(c->st);
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->st);
   c->scratch.release();
   c->in_stage.release();
   c->out_stage.release();
   c->aux.release();
-  for (auto &e : c->ev) hipEventDestroy(e);
-  hipStreamDestroy(c->st);
+  c->dec_cols.release();
+  if (c->dstats) (void)hipFree(c->dstats);
+  for (auto &e : c->ev) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->st);
   delete c;
 }
 
@@ -335,14 +349,13 @@ int run_decode_exact_once(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, con
   P.counter = ctrl;
   P.overflow = ctrl + 1;
   P.strict = (uint32_t)c->strict;
-  unsigned long long *dstats = nullptr;
-  if (getenv("DRP_STATS")) {
-    CHK(hipMalloc((void **)&dstats, 64 * 8));
+  unsigned long long *dstats = c->stats ? c->dstats : nullptr;
+  if (dstats) {
     CHK(hipMemsetAsync(dstats, 0, 64 * 8, st));
     P.stats = dstats;
   }
   unsigned long long *dtrace = nullptr;
-  if (dstats && getenv("DRP_TRACE_FILE")) {
+  if (dstats && c->trace_file) {
     CHK(hipMalloc((void **)&dtrace, NT * 64));
     CHK(hipMemsetAsync(dtrace, 0, NT * 64, st));
     P.trace = dtrace;
@@ -375,9 +388,9 @@ int run_decode_exact_once(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, con
   CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
   CHK(hipStreamSynchronize(st));
   float ms = 0;
-  hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
+  (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
   c->timing.decode_ms = ms;
-  hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
+  (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
   c->timing.total_ms = ms;
   c->timing.finalize_ms = 0;
   c->timing.spec_repairs = 0;
@@ -396,16 +409,15 @@ int run_decode_exact_once(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, con
     fprintf(stderr, "[drp-stats]");
     for (int i = 0; i < 35; i++) fprintf(stderr, " %s=%llu", nm[i], hs[i]);
     fprintf(stderr, " decode_ms=%.3f\n", c->timing.decode_ms);
-    hipFree(dstats);
   }
   if (dtrace) {
     std::vector<unsigned long long> ht(NT * 8);
     CHK(hipMemcpy(ht.data(), dtrace, NT * 64, hipMemcpyDeviceToHost));
-    if (FILE *f = fopen(getenv("DRP_TRACE_FILE"), "wb")) {
+    if (FILE *f = fopen(c->trace_file, "wb")) {
       fwrite(ht.data(), 8, ht.size(), f);
       fclose(f);
     }
-    hipFree(dtrace);
+    (void)hipFree(dtrace);
   }
   if (h[1] & ~1u) return kWaitExpired;  // bounded wait expired / inconsistent walk inside the kernel
   if (h[1]) return DRP_E_CAPACITY;
@@ -512,13 +524,12 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.dstamp = reinterpret_cast<uint32_t *>(rec + 4 * NT);  // (after the dirty lists)
   P.pass_id = 1;
   P.change_checks = (uint32_t)c->change_checks;
-  if (const char *e = getenv("DRP_KSTRONG_HBM")) P.kstrong_hbm = atoi(e);  // (tests: weaker predictions)
+  P.kstrong_hbm = c->kstrong_hbm;  // (tests: weaker predictions)
   CHK(hipMemsetAsync(P.dstamp, 0, NT * 4, st));
-  if (const char *e = getenv("DRP_DIRTY_CAP")) P.dlist_cap = std::min<uint64_t>(NT, strtoull(e, nullptr, 10));  // (tests)
+  P.dlist_cap = std::min<uint64_t>(NT, c->dirty_cap);  // (tests: DRP_DIRTY_CAP)
   CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
-  unsigned long long *dstats = nullptr;
-  if (getenv("DRP_STATS")) {
-    CHK(hipMalloc((void **)&dstats, 64 * 8));
+  unsigned long long *dstats = c->stats ? c->dstats : nullptr;
+  if (dstats) {
     CHK(hipMemsetAsync(dstats, 0, 64 * 8, st));
     P.stats = dstats;
   }
@@ -619,9 +630,9 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     c->change_checks = h[3] == 0 || nbytes / h[3] >= 512 ? 1 : 0;
   if (retry) h[1] |= miss;
   float ms = 0;
-  hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
+  (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
   c->timing.decode_ms = ms;
-  hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
+  (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
   c->timing.total_ms = ms;
   c->timing.finalize_ms = 0;
   c->timing.strict_reruns = 0;
@@ -641,7 +652,6 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     for (int k = 0; k < 14; k++)
       if (ph[k][0]) fprintf(stderr, " %s=%.0f", ph[k], (double)hs[40 + k] / (double)(h[0] ? h[0] : 1));
     fprintf(stderr, " repairs=%d (avg cycles per tile) link_rounds=%llu\n", pass, hs[56]);
-    (void)hipFree(dstats);
   }
   if (h[1] & drp_spec_retry_mask()) return DRP_E_RETRY;
   if (h[1]) return DRP_E_CAPACITY;
@@ -860,6 +870,7 @@ static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t p
   // doubled within this batch after each piece that met no blob
   uint64_t want = std::max(kPieceMin, c->blob_run + kPieceMargin);
   float h2d_ms = 0;
+  drp_timing sum = {};
   drp_stream_result r;
   for (;;) {
     const uint64_t pe = std::min(n, pos + want), ps = pos & ~15ull, mp = pe - ps;
@@ -891,6 +902,14 @@ static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t p
     const int rc = run_decode(c, (const uint8_t *)c->in_stage.p, mp, soff, ent, 1, &fr, &co, cap - rows, dres);
     if (rc == DRP_E_CAPACITY) return DRP_E_RETRY;
     if (rc != DRP_OK) return rc;
+    // (run_decode describes one launch sequence: the call's timing is the sum over its pieces)
+    sum.decode_ms += c->timing.decode_ms;
+    sum.total_ms += c->timing.total_ms;
+    sum.strict_reruns += c->timing.strict_reruns;
+    sum.spec_repairs += c->timing.spec_repairs;
+    sum.exact_retries += c->timing.exact_retries;
+    sum.verify_relisted += c->timing.verify_relisted;
+    sum.seg_repairs += c->timing.seg_repairs;
     CHK(hipMemcpyAsync(&r, dres, sizeof(r), hipMemcpyDeviceToHost, st));
     uint64_t boff = 0;  // the cut blob's payload offset in the piece (tail BLOB)
     CHK(hipStreamSynchronize(st));
@@ -944,6 +963,7 @@ static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t p
       if (np > pos) pos = np;
     }
   }
+  c->timing = sum;
   c->timing.h2d_ms = h2d_ms;
   c->timing.h2d_bytes = staged;
   c->timing.h2d_skipped = skipped;

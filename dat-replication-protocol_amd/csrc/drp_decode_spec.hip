@@ -88,7 +88,7 @@ constexpr uint64_t RDY = 1ull << 63;          // published word: value | RDY
 constexpr uint64_t C_ID = 1ull << 62;         // claim: identity (no chain survives the tile)
 constexpr uint64_t M_ERR = 1ull << 60;        // with MARK_TERM: the chain ended at an error header
 constexpr uint64_t NONE = ~0ull;              // internal: no chain
-constexpr uint32_t SPIN = 1u << 22;
+
 constexpr uint32_t F_MISS = 1u << 12;         // overflow bit: prediction failed -> exact re-run
 constexpr uint32_t F_WAIT = 1u << 13;
          // overflow bit: bounded wait expired -> exact re-run
@@ -1309,7 +1309,9 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
       // w32 reads the batch, which holds them: interior tiles end >= IMG before the stream end)
       uint32_t cr = 0;
       if (cfw[j]) {
-        const uint32_t lim = min(se_rel, IMG + 512u), po = cfw[j] & 0x3FFFu, pl = cfw[j] >> 14;
+        // (the LDS-image build reads its IMG + 32 bytes only; the default reads the batch)
+        const uint32_t lim = min(se_rel, DRP_K1_GIMG ? IMG + 512u : IMG + 32u - 36u), po = cfw[j] & 0x3FFFu,
+                       pl = cfw[j] >> 14;
         cr = change_fills_win(w32, po, pl, lim, cff[j] & 0xFFFFFu, cff[j] >> 20);
         if (cr == 2u) cr = change_fills(w32, po, pl, lim, cff[j] & 0xFFFFFu, cff[j] >> 20) ? 1u : 0u;
       }

@@ -462,8 +462,38 @@ static napi_value js_device_count(napi_env env, napi_callback_info info) {
 /* indexAllgather(ctxs: [ctx per device], stats: [Float64Array(perGpu * 4) per device])
  *   -> {table: Float64Array(ngpu * perGpu * 4), base: Float64Array(ngpu * perGpu)}
  * The per-stream (frames, changes, blobs, wireBytes) records of every device, all-gathered over
- * RCCL (drp_comm_init_all + drp_index_allgather_host: one communicator per device of this
- * process) and scanned into the global index of each stream's first frame. Synchronous. */
+ * RCCL (drp_index_allgather_host: one communicator per device of this process) and scanned into
+ * the global index of each stream's first frame. Synchronous. Each ctx's mutex is held for the
+ * call (its stream is the one the collective and the scan run on, and its calls are serialised:
+ * native.js hands the same contexts to decoders and encoders). The communicators depend only on
+ * the device list, so they are created once per device list (drp_comm_init_all) and reused. */
+static struct {
+  int ng;
+  int dev[64];
+  drp_comm *comm[64];
+} comm_cache;
+
+static void comm_cache_clear(void *arg) {
+  (void)arg;
+  for (int g = 0; g < comm_cache.ng; g++) drp_comm_destroy(comm_cache.comm[g]);
+  comm_cache.ng = 0;
+}
+
+/* the cached communicators of this device list, created on first use (or on a new list) */
+static int comms_for(drp_ctx **ctxs, int ng, drp_comm **out) {
+  int same = comm_cache.ng == ng;
+  for (int g = 0; g < ng && same; g++) same = comm_cache.dev[g] == drp_device(ctxs[g]);
+  if (!same) {
+    comm_cache_clear(NULL);
+    int rc = drp_comm_init_all(ctxs, ng, comm_cache.comm);
+    if (rc != DRP_OK) return rc;
+    comm_cache.ng = ng;
+    for (int g = 0; g < ng; g++) comm_cache.dev[g] = drp_device(ctxs[g]);
+  }
+  for (int g = 0; g < ng; g++) out[g] = comm_cache.comm[g];
+  return DRP_OK;
+}
+
 static napi_value js_index_allgather(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
@@ -477,6 +507,7 @@ static napi_value js_index_allgather(napi_env env, napi_callback_info info) {
     return NULL;
   }
   drp_ctx *ctxs[64];
+  ctx_box *boxes[64] = {0};
   drp_comm *comms[64] = {0};
   drp_stream_stats *local[64] = {0};
   size_t per = 0;
@@ -497,6 +528,7 @@ static napi_value js_index_allgather(napi_env env, napi_callback_info info) {
     }
     per = len / 4;
     ctxs[g] = b->c;
+    boxes[g] = b;
     local[g] = (drp_stream_stats *)malloc(per * sizeof(drp_stream_stats) + 8);
     if (!local[g]) {
       rc = DRP_E_NOMEM;
@@ -517,13 +549,26 @@ static napi_value js_index_allgather(napi_env env, napi_callback_info info) {
     base = (uint64_t *)malloc(ng * per * 8 + 8);
     if (!global || !base) rc = DRP_E_NOMEM;
   }
-  if (rc == DRP_OK) rc = drp_comm_init_all(ctxs, (int)ng, comms);
-  if (rc == DRP_OK)
-    rc = drp_index_allgather_host(ctxs, comms, (int)ng, (const drp_stream_stats *const *)local, per, global, base);
-  for (uint32_t g = 0; g < ng; g++) {
-    drp_comm_destroy(comms[g]);
-    free(local[g]);
+  /* lock every ctx (in list order; a ctx listed twice is locked once): this is the only caller
+     that holds more than one, and it runs on the JS thread, so the order cannot invert */
+  uint32_t locked = 0;
+  if (rc == DRP_OK) {
+    for (; locked < ng; locked++) {
+      int dup = 0;
+      for (uint32_t k = 0; k < locked && !dup; k++) dup = boxes[k] == boxes[locked];
+      if (!dup) pthread_mutex_lock(&boxes[locked]->mu);
+    }
+    rc = comms_for(ctxs, (int)ng, comms);
+    if (rc == DRP_OK)
+      rc = drp_index_allgather_host(ctxs, comms, (int)ng, (const drp_stream_stats *const *)local, per, global, base);
+    if (rc != DRP_OK) comm_cache_clear(NULL); /* (a failed collective leaves nothing cached) */
   }
+  for (uint32_t g = locked; g-- > 0;) {
+    int dup = 0;
+    for (uint32_t k = 0; k < g && !dup; k++) dup = boxes[k] == boxes[g];
+    if (!dup) pthread_mutex_unlock(&boxes[g]->mu);
+  }
+  for (uint32_t g = 0; g < ng; g++) free(local[g]);
   napi_value out = NULL;
   if (rc == DRP_OK) {
     napi_value tab_ab, base_ab, tab, bs;
@@ -563,6 +608,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"indexAllgather", NULL, js_index_allgather, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
+  napi_add_env_cleanup_hook(env, comm_cache_clear, NULL);
   napi_value v;
   napi_create_int32(env, drp_abi_version(), &v);
   napi_set_named_property(env, exports, "abiVersion", v);

@@ -1,6 +1,8 @@
 """Per-kernel PMC summary of scripts/gpu_pmc.sh passes (gpurun_out/pmc/<pass>/): average per dispatch
 and per frame, FETCH_SIZE doubled per the gfx950 note (MI355X_MICROARCH.md: 128-B requests
-tallied at 64 B). Usage: python scripts/pmc_kernels.py [frames] [--dir gpurun_out/pmc] [--write profiles/pmc_decode.json]"""
+tallied at 64 B). Usage: python scripts/pmc_kernels.py [frames] [--dir gpurun_out/pmc] [--workload c2|c4|c5]
+[--write profiles/pmc_<workload>.json] (c5: the encode kernels are counted too: its roofline prices the
+round trip)"""
 import collections
 import csv
 import glob
@@ -9,8 +11,9 @@ import sys
 
 KNAME = "speculative decode: claims_fast + verify_lite + tile scans + emit_tiles"  # = bench.py's kname
 PMC_DIR = sys.argv[sys.argv.index("--dir") + 1] if "--dir" in sys.argv else "gpurun_out/pmc"
-args = [a for a in sys.argv[1:] if not a.startswith("--") and a != PMC_DIR and
-        not (("--write" in sys.argv) and a == sys.argv[sys.argv.index("--write") + 1])]
+WORKLOAD = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else "c2"
+opt_vals = {sys.argv[sys.argv.index(o) + 1] for o in ("--dir", "--write", "--workload") if o in sys.argv}
+args = [a for a in sys.argv[1:] if not a.startswith("--") and a not in opt_vals]
 frames = float(args[0]) if args else 20e6
 tot = collections.defaultdict(float)
 disp = collections.defaultdict(set)
@@ -43,12 +46,13 @@ for k in kern:
     print(" ".join(out))
 if "--write" in sys.argv:
     path = sys.argv[sys.argv.index("--write") + 1]
-    dec = {k: v for k, v in per.items() if not k.startswith("enc")}
+    dec = {k: v for k, v in per.items() if WORKLOAD == "c5" or not k.startswith("enc")}
     # the ctx's first decode (bench warmup) runs claims_fast<true>, the steady state <false>
     if "void claims_fast<false>" in dec and "void claims_fast<true>" in dec:
         dec.pop("void claims_fast<true>")
     hbm = sum(v["fetch_B_per_frame"] + v["write_B_per_frame"] for v in dec.values())
-    json.dump({"kernel": KNAME, "workload": f"C2, {frames:g} frames (bench.py --frames {frames:g}), per dispatch",
+    json.dump({"kernel": KNAME, "workload": f"{WORKLOAD.upper()}, {frames:g} frames per dispatch "
+               f"(scripts/gpu_pmc.sh {WORKLOAD})",
                "frames": frames, "note": "rocprofv3 --pmc, one pass per counter group (scripts/gpu_pmc.sh); "
                "FETCH_SIZE doubled per MI355X_MICROARCH.md; per wave for SQ counters",
                "hbm_bytes_per_frame": round(hbm, 2), "per_kernel": dec}, open(path, "w"), indent=1)

@@ -54,7 +54,7 @@ def summarize(path):
             chunk = sorted(v[i * REPS + 1:(i + 1) * REPS])  # (first decode of a size: cold)
             if chunk:
                 med = chunk[len(chunk) // 2]
-                print(f"  {n:>10} frames  {med:8.3f} ms  {med * 1e6 / n:7.2f} ns/frame")
+                print(f"  {n:>10} frames  {med:8.3f} ms  {med * 1e9 / n:7.1f} ps/frame")
 
 
 if __name__ == "__main__":

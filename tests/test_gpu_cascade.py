@@ -38,13 +38,14 @@ def test_cascade_parity(ctx, period, at, small, chg):
 
 
 @pytest.mark.parametrize("cap", ["1", "0"])
-def test_dirty_list_overflow_full_pass(ctx, monkeypatch, cap):
+def test_dirty_list_overflow_full_pass(monkeypatch, cap):
     """Repair passes verify only the tiles a repair changed (dirty lists, drp_api.hip); a list
     past its capacity (forced here with DRP_DIRTY_CAP) must fall back to a full verify pass with
     the same results. A 600 KB blob after the shadow's start also gives a miss whose successors
     run through identity claims (the run cap of 64 tiles)."""
-    from _gpu import assert_same
-    monkeypatch.setenv("DRP_DIRTY_CAP", cap)
+    from _gpu import assert_same, drp_amd
+    monkeypatch.setenv("DRP_DIRTY_CAP", cap)  # (read by drp_open)
+    ctx = drp_amd.Ctx(0)
     for period, at, small, chg in CASCADES[:3]:
         wire = S.shadow_stream(int(8 * 2**20 / period), period=period, shadow_at=at, small=small, change_every=chg)
         g = ctx.decode_batch(wire)
@@ -55,6 +56,7 @@ def test_dirty_list_overflow_full_pass(ctx, monkeypatch, cap):
     parts.insert(150, S.frame(b"\x01\x02" * 300_000, 2))
     wire = b"".join(parts)
     assert_same(ctx.decode_batch(wire), O.decode_batch(wire), f"blob run cap {cap}")
+    ctx.close()
 
 
 def _c5_with_error(nframes, at, seed=5):
@@ -158,7 +160,7 @@ def test_dense_cascade_1_7gb(ctx):
 
 
 @pytest.mark.parametrize("khbm", ["2", "3"])
-def test_weak_prediction_c5_round_trip(ctx, monkeypatch, khbm):
+def test_weak_prediction_c5_round_trip(monkeypatch, khbm):
     """DRP_KSTRONG_HBM weakens claims_fast's check of deferred candidates (frames that leave the
     image), so the full C5 round trip (1M Changes, 4.2 GB) gets many more wrong predictions:
     misses in adjacent tiles and runs through identity claims, so one repair can list a tile that
@@ -171,7 +173,8 @@ def test_weak_prediction_c5_round_trip(ctx, monkeypatch, khbm):
 
     import bench
     from _gpu import drp_amd
-    monkeypatch.setenv("DRP_KSTRONG_HBM", khbm)
+    monkeypatch.setenv("DRP_KSTRONG_HBM", khbm)  # (read by drp_open)
+    ctx = drp_amd.Ctx(0)
     dev = torch.device("cuda", 0)
     n = 1_000_000
     cols, heap, frame = bench.c5_on_device(n, seed=55, dev=dev)
@@ -190,3 +193,4 @@ def test_weak_prediction_c5_round_trip(ctx, monkeypatch, khbm):
     print(f"C5 with DRP_KSTRONG_HBM={khbm}: repair passes {t.spec_repairs}, segmented {t.seg_repairs}")
     assert t.strict_reruns == 0
     bench.verify_c5(cols, heap, wire, outs, res, n, dev)
+    ctx.close()

@@ -254,6 +254,52 @@ def test_c5_predicted_without_repairs():
     assert t.strict_reruns == 0 and t.spec_repairs == 0, (t.spec_repairs, t.strict_reruns)
 
 
+def test_c5_after_c2_on_one_context():
+    """native.js pools contexts across streams, so a C5 stream can land on a context whose last
+    decode was dense C2, which turned claims_fast's long-frame check off: that decode then relies
+    on the repair passes (and segmented repair). It must still be bit-exact with the encoder's
+    input and never fall back to the exact kernel; the next decode on the context has the check
+    back on and needs no repair."""
+    import ctypes as C
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from _gpu import drp_amd
+    dev = torch.device("cuda", 0)
+    ctx = drp_amd.Ctx(0)
+    nc2 = 2_000_000
+    w2 = bench.c2_on_device(nc2, seed=9, dev=dev)
+    o2 = bench.alloc_outputs(nc2 + 64, dev)
+    r2 = torch.zeros(C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+    for _ in range(2):  # (the first decode of a context runs the check; the second one does not)
+        ctx.decode_device(w2, torch.tensor([0, w2.numel()], dtype=torch.int64, device=dev), None, o2, nc2 + 64, r2)
+    torch.cuda.synchronize(dev)
+    bench.verify_c2(o2, r2, nc2, dev)
+    del w2, o2
+    n = 200_000
+    cols, heap, frame = bench.c5_on_device(n, seed=56, dev=dev)
+    W = int(frame.sum())
+    out = torch.zeros(W + 64, dtype=torch.uint8, device=dev)
+    foff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ctx.encode_device(cols, heap, n, foff, out, W + 64)
+    outs = bench.alloc_outputs(n + 64, dev)
+    res = torch.zeros(C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+    wire = out[:W]
+    so = torch.tensor([0, W], dtype=torch.int64, device=dev)
+    reps = []
+    for _ in range(2):
+        outs["change"].fill_(0)
+        ctx.decode_device(wire, so, None, outs, n + 64, res)
+        torch.cuda.synchronize(dev)
+        t = ctx.timing()
+        reps.append((t.spec_repairs, t.seg_repairs, t.strict_reruns))
+        bench.verify_c5(cols, heap, wire, outs, res, n, dev, samples=64)
+    ctx.close()
+    print(f"C5 after C2 (repairs, segmented, exact): {reps}")
+    assert reps[0][2] == 0 and reps[1] == (0, 0, 0), reps
+
+
 def test_encode_rejects_out_of_range_rows(ctx):
     """A row whose key/subset/value range leaves the heap is DRP_E_INVAL, not a device fault
     (drp.h: every call returns a code)."""
