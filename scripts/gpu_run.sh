@@ -1,0 +1,75 @@
+#!/bin/bash
+# One GPU session, steps chosen by name (replaces the per-session drivers of earlier rounds).
+# Every GPU step has its own time limit; the first timeout, abort or crash ends the script (test
+# failures, rc 1, do not). Output: gpurun_out/<tag>/.
+# Usage: gpurun --timeout 1200 -- 'bash scripts/gpu_run.sh <tag> <step>...'
+#   tests          the GPU suite (pytest -m gpu)
+#   tests:<expr>   the GPU tests matching a -k expression
+#   smoke          __graft_entry__.smoke()
+#   bench          the default bench line (C2 + c4/c5 sub-lines + CPU legs + Node path)
+#   quick          the default bench line without CPU legs and the Node path
+#   prof           rocprofv3 --kernel-trace --stats of a quick C2 + C4 + C5 run (no CPU legs)
+#   pmc:<w>        FETCH_SIZE / WRITE_SIZE / SQ passes of workload w (c2, c4, c5) (scripts/gpu_pmc.sh)
+#   ab:<variant>   quick C2 + C5 lines with exp/<variant>/libdrp.so (scripts/build_variant.sh)
+#   probe:<script> python3 scripts/<script> (a measurement script)
+set -e
+export TMPDIR=/tmp
+TAG=$1
+shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+for step in "$@"; do
+  case $step in
+    tests | tests:*)
+      K=${step#tests}
+      K=${K#:}
+      set +e
+      timeout -k 10 900 python -u -m pytest tests -m gpu ${K:+-k "$K"} --maxfail=8 -v -rA --timeout 150 \
+        --timeout-method thread > $OUT/gpu_tests.log 2>&1
+      rc=$?
+      set -e
+      echo "tests rc=$rc: $(tail -1 $OUT/gpu_tests.log)"
+      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+      ;;
+    smoke)
+      timeout -k 10 150 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+      echo "smoke: $(tail -1 $OUT/smoke.log)"
+      ;;
+    bench)
+      timeout -k 10 600 python -u bench.py > $OUT/bench.log 2>&1
+      echo bench done
+      ;;
+    quick)
+      timeout -k 10 300 python -u bench.py --no-cpu > $OUT/bench_quick.log 2>&1
+      echo quick done
+      ;;
+    prof)
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/prof -o run -- \
+        python3 -u $ROOT/bench.py --steps 5 --warmup 2 --no-cpu > $ROOT/$OUT/bench_prof.log 2>&1)
+      echo prof done
+      ;;
+    pmc:*)
+      W=${step#pmc:}
+      F=20000000
+      [ "$W" = c2 ] || F=100000000
+      timeout -k 10 700 bash scripts/gpu_pmc.sh $F $W $OUT/pmc_$W
+      echo "pmc $W done"
+      ;;
+    ab:*)
+      V=${step#ab:}
+      DRP_LIB=exp/$V/libdrp.so timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --no-cpu \
+        > $OUT/ab_$V.log 2>&1
+      echo "ab $V done"
+      ;;
+    probe:*)
+      S=${step#probe:}
+      timeout -k 10 400 python3 -u scripts/$S > $OUT/probe_${S%%.*}.log 2>&1
+      echo "probe $S done"
+      ;;
+    *)
+      echo "unknown step $step"
+      exit 2
+      ;;
+  esac
+done
