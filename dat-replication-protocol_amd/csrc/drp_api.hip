@@ -99,6 +99,8 @@ struct drp_ctx {
   bool stats = false;
   const char *trace_file = nullptr;
   unsigned long long *dstats = nullptr;
+  DecodeParams lastP = {};  // the last speculative decode's parameters (measurement hook)
+  uint64_t lastNT = 0;
   DevBuf scratch, in_stage, out_stage, aux;
   DevBuf dec_cols;  // device columns of the staged host-batch decode (drp_decode_stage)
   double frames_per_byte = 0;  // density of the last staged batch (sizes the next one's columns)
@@ -273,6 +275,41 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   return L;
 }
 
+// Measurement hook, not part of the product path (scripts/probe_overlap.py): after a
+// single-stream decode on the ctx, times its claims kernel alone, its emit kernel alone and both
+// side by side on two streams: ms[0..2].
+int drp_probe_overlap(drp_ctx *c, float *ms) {
+  if (!c || !ms || !c->lastNT) return DRP_E_INVAL;
+  hipStream_t b = nullptr;
+  hipEvent_t ev[6];
+  CHK(hipStreamCreateWithFlags(&b, hipStreamNonBlocking));
+  for (auto &e : ev) CHK(hipEventCreate(&e));
+  CHK(drp_probe_overlap_launch(&c->lastP, c->lastNT, c->st, b, ev));
+  CHK(hipStreamSynchronize(c->st));
+  CHK(hipStreamSynchronize(b));
+  (void)hipEventElapsedTime(&ms[0], ev[0], ev[1]);
+  (void)hipEventElapsedTime(&ms[1], ev[1], ev[2]);
+  (void)hipEventElapsedTime(&ms[2], ev[3], ev[5]);
+  for (auto &e : ev) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(b);
+  return DRP_OK;
+}
+
+int drp_host_alloc(uint64_t bytes, void **out) {
+  if (!out || !bytes) return DRP_E_INVAL;
+  *out = nullptr;
+  if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return DRP_E_NOMEM;
+  }
+  return DRP_OK;
+}
+
+void drp_host_free(void *p) {
+  if (p) (void)hipHostFree(p);
+}
+
 uint64_t drp_decode_scratch_bytes(drp_ctx *c, uint64_t n, uint64_t nstreams) {
   return dec_layout(c ? c->B : 128, n, nstreams).total;
 }
@@ -380,9 +417,9 @@ int run_decode_exact_once(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, con
   CHK(drp_launch_stream_counts(tile_prefix, ns, P.tile_count, P.tile_base, P.tile_nch, P.tile_nch_base, scount, st));
   CHK(hipEventRecord(c->ev[2], st));
   CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
-                          scount, fr->type, co->flags, cap, res, st));
+                          scount, fr->type, co->flags, cap, res, nullptr, 0, st));
   CHK(drp_launch_key_post(bytes, tile_prefix, ns, P.tile_base, P.tile_count, cap, fr, co,
-                          c->key_post == DRP_KEY_POST_FLAGS, st));
+                          c->key_post == DRP_KEY_POST_FLAGS, nullptr, 0, st));
   CHK(hipEventRecord(c->ev[3], st));
   uint32_t h[2];
   CHK(hipMemcpyAsync(h, ctrl, 8, hipMemcpyDeviceToHost, st));
@@ -543,9 +580,28 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   uint32_t h[16];
   const uint32_t miss = drp_spec_miss_bit();
   CHK(drp_launch_spec_head(&P, NT, ns, tstream, st));
-  CHK(hipMemcpyAsync(h, ctrl, 64, hipMemcpyDeviceToHost, st));
-  CHK(hipStreamSynchronize(st));
-  const uint32_t relisted = h[5];
+  CHK(hipMemcpyAsync(ctrl + 14, ctrl + 5, 4, hipMemcpyDeviceToDevice, st));  // (verify's relisted tiles)
+  // Emission, the output bases and the per-stream results go right behind verification, with no
+  // host read in between: the emit, finalize and key kernels read the flag word and do nothing
+  // after a failed prediction, which is repaired below before they run again. A decode whose
+  // prediction holds makes one host round trip.
+  const uint32_t *abort_flag = P.overflow;
+  auto launch_tail = [&]() -> int {
+    CHK(drp_launch_spec_tail(&P, NT, ns, tstream, sgscan, st));
+    CHK(hipEventRecord(c->ev[2], st));
+    CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
+                            scount, fr->type, co->flags, cap, res, abort_flag, drp_spec_retry_mask(), st));
+    CHK(drp_launch_key_post(bytes, tile_prefix, ns, P.tile_base, P.tile_count, cap, fr, co,
+                            c->key_post == DRP_KEY_POST_FLAGS, abort_flag, drp_spec_retry_mask(), st));
+    CHK(hipEventRecord(c->ev[3], st));
+    CHK(hipMemcpyAsync(h, ctrl, 64, hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+    return DRP_OK;
+  };
+  if (const int rt = launch_tail()) return rt;
+  c->lastP = P;
+  c->lastNT = NT;
+  const uint32_t relisted = h[14];
   int pass = 0;
   bool seg_done = false;
   if ((h[1] & drp_spec_retry_mask()) == miss) {
@@ -611,21 +667,10 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
       }
     }
     TRACE("decode_spec: %d repair pass(es), flags=%#x", pass, h[1]);
+    if (!(h[1] & drp_spec_retry_mask()))  // repaired: emission and results again
+      if (const int rt = launch_tail()) return rt;
   }
   const bool retry = (h[1] & drp_spec_retry_mask()) != 0;
-  if (!retry) {
-    CHK(drp_launch_spec_tail(&P, NT, ns, tstream, sgscan, st));
-    CHK(hipEventRecord(c->ev[2], st));
-    CHK(drp_launch_finalize(bytes, stream_off, ns, tile_prefix, P.tile_exit, P.tile_base, P.tile_count, perr,
-                            scount, fr->type, co->flags, cap, res, st));
-    CHK(drp_launch_key_post(bytes, tile_prefix, ns, P.tile_base, P.tile_count, cap, fr, co,
-                          c->key_post == DRP_KEY_POST_FLAGS, st));
-  } else {
-    CHK(hipEventRecord(c->ev[2], st));
-  }
-  CHK(hipEventRecord(c->ev[3], st));
-  CHK(hipMemcpyAsync(h, ctrl, 16, hipMemcpyDeviceToHost, st));
-  CHK(hipStreamSynchronize(st));
   if (!retry && c->change_checks_env < 0)  // (h[3]: the call's frames, from stream_counts)
     c->change_checks = h[3] == 0 || nbytes / h[3] >= 512 ? 1 : 0;
   if (retry) h[1] |= miss;
@@ -1190,7 +1235,9 @@ int drp_encode_device(drp_ctx *c, const drp_change_src *src, const uint8_t *heap
   if (!c || !src || !frame_off) return DRP_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
   const uint64_t nblk = (n + 1023) / 1024;
-  if (!c->aux.ensure(4096 + nblk * 8 + 64)) return DRP_E_NOMEM;
+  const uint64_t nob = out ? drp_encode_out_blocks(cap) : 0;
+  const size_t ob = al(4096 + nblk * 8 + 64), dn = al(ob + nob * 8);
+  if (!c->aux.ensure(dn + nob * 4 + 64)) return DRP_E_NOMEM;
   EncodeParams P;
   P.src = *src;
   P.heap = heap;
@@ -1201,6 +1248,10 @@ int drp_encode_device(drp_ctx *c, const drp_change_src *src, const uint8_t *heap
   P.cap = cap;
   P.block_sum = c->aux.at<uint64_t>(4096);
   P.overflow = c->aux.at<uint32_t>(1024);
+  P.dense_n = c->aux.at<uint32_t>(1028);
+  P.oblk_first = c->aux.at<uint64_t>(ob);
+  P.dense = c->aux.at<uint32_t>(dn);
+  P.nob = nob;
   CHK(hipMemsetAsync(P.overflow, 0, 4, c->st));
   if (n == 0) {
     CHK(hipMemsetAsync(frame_off, 0, 8, c->st));

@@ -1510,9 +1510,10 @@ __global__ void finalize_kernel(const uint8_t *bytes, const uint64_t *stream_off
                                 const uint64_t *tile_base, const uint64_t *tile_count,
                                 const uint64_t *payload_err, const uint64_t *scount,
                                 const uint8_t *type, const uint8_t *flags, uint64_t cap,
-                                drp_stream_result *res) {
+                                drp_stream_result *res, const uint32_t *abort_flag, uint32_t abort_mask) {
   const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nstreams) return;
+  if (abort_flag && (*abort_flag & abort_mask)) return;  // (a failed prediction: run again after its repair)
   const uint64_t ntiles = tile_prefix[nstreams];
   const uint64_t tf = tile_prefix[s], tl = tile_prefix[s + 1];
   const uint64_t so = stream_off[s], se = stream_off[s + 1];
@@ -1623,11 +1624,13 @@ extern "C" hipError_t drp_launch_finalize(const uint8_t *bytes, const uint64_t *
                                           const uint64_t *tile_base, const uint64_t *tile_count,
                                           const uint64_t *payload_err, const uint64_t *scount,
                                           const uint8_t *type, const uint8_t *flags, uint64_t cap,
-                                          drp_stream_result *res, hipStream_t st) {
+                                          drp_stream_result *res, const uint32_t *abort_flag,
+                                          uint32_t abort_mask, hipStream_t st) {
   const uint32_t blk = 256;
   const uint32_t grid = (uint32_t)((nstreams + blk - 1) / blk);
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(finalize_kernel, dim3(grid), dim3(blk), 0, st, bytes, stream_off, nstreams, tile_prefix,
-                     tile_exit, tile_base, tile_count, payload_err, scount, type, flags, cap, res);
+                     tile_exit, tile_base, tile_count, payload_err, scount, type, flags, cap, res, abort_flag,
+                     abort_mask);
   return hipGetLastError();
 }

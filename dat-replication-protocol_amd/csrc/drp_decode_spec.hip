@@ -1098,12 +1098,129 @@ struct FastLds {
   uint32_t xw[8];
   uint32_t xf[2 * NT / WAVE], wl[NT / WAVE], fl[NT / WAVE];
   uint64_t xm[4];  // candidate masks (two waves): [w] strong, [2 + w] strong and far
+  uint8_t sp_eb[NT], sp_en[NT], sp_ec[NT];  // the sparse form's records (sparse_claims)
+  uint64_t sp_claim;
+  uint32_t sp_ok;
 #ifdef DRP_K1_PAD
   uint8_t pad[DRP_K1_PAD];  // (A/B only: caps the workgroups per CU through LDS)
 #endif
 };
 enum : uint32_t { FC_OK = 0, FC_DENSE = 1, FC_ABLATE = 2 };
 
+__device__ __forceinline__ void sparse_claims(const DecodeParams &P, const TileGeo &G, FastLds &S, uint32_t total,
+                                              uint32_t se_rel) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool live = lane < total;
+  const uint32_t nd = live ? S.lnd[lane] : (NX_DEAD | (3u << 30));
+  const uint32_t pos = live ? S.lpos[lane] : 0xFFFFu;
+  const uint32_t c = nd & 0xFFFFu, id = nd >> 30, q = (nd >> 16) & 0x3FFFu;
+  uint32_t a = live ? S.lal[lane] : 0u;
+  // survival: KSTRONG - 1 rounds of "my successor's state", from one snapshot per round
+#pragma unroll
+  for (int r = 1; r < KSTRONG; r++) {
+    const uint32_t b = (uint32_t)__shfl((int)a, (int)(c < WAVE ? c : lane), WAVE);
+    if (a == 1u && c < NX_NEAR && b != 1u) a = b;
+  }
+  const bool tile_node = live && pos < TILE;
+  const uint64_t strong = __ballot(tile_node && a == 1u);
+  const uint64_t und = __ballot(tile_node && a == 2u);
+  if (lane < NT / 2) {  // (records default: no entry)
+    S.sp_eb[lane] = 0xFF;
+    S.sp_eb[lane + NT / 2] = 0xFF;
+    S.sp_en[lane] = S.sp_en[lane + NT / 2] = 0;
+    S.sp_ec[lane] = S.sp_ec[lane + NT / 2] = 0;
+  }
+  uint32_t ok = 1;
+  uint64_t claim = C_ID;
+  if (!strong) {
+    ok = und == 0;  // (undecided nodes: the general phases check them in HBM)
+  } else {
+    const uint32_t g0 = (uint32_t)__builtin_ctzll(strong);
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)g0);
+    if ((c0 == NX_FAR || c0 == NX_NEAR) && (strong & (strong - 1))) ok = 0;  // (rule 2's case)
+    // the chain from g0 (a uniform walk over the lanes' successor codes)
+    uint64_t chain = 0;
+    uint32_t j = g0, last = g0, exitn = 0xFFFFFFFFu;
+#pragma unroll 1
+    for (uint32_t step = 0; ok && step < WAVE; step++) {
+      const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)pos, (int)j);
+      if (pj >= TILE) {  // the first chain position past the tile: the claim
+        exitn = j;
+        break;
+      }
+      chain |= 1ull << j;
+      last = j;
+      const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)nd, (int)j);
+      if ((nj >> 30) == 3u) ok = 0;  // (an invalid header on the chain)
+      const uint32_t cj = nj & 0xFFFFu;
+      if (cj < WAVE) {
+        j = cj;
+        continue;
+      }
+      if (cj == NX_DEAD) ok = 0;  // (the chain dies: ambiguous)
+      break;
+    }
+    if (ok && (strong & ~chain)) ok = 0;  // a strong node off the chain
+    if (ok && exitn == 0xFFFFFFFFu) {
+      // the chain ends inside the tile: past its last node only decided (dead) nodes may follow
+      const uint32_t pl = (uint32_t)__builtin_amdgcn_readlane((int)pos, (int)last);
+      const uint64_t after = und & ~((2ull << last) - 1ull);
+      if (after) ok = 0;
+      const uint32_t nl = (uint32_t)__builtin_amdgcn_readlane((int)nd, (int)last);
+      const uint32_t cl = nl & 0xFFFFu, ql = (nl >> 16) & 0x3FFFu;
+      if (cl == NX_TAILB || cl == NX_TAILC) {
+        claim = MARK_TERM | (G.A + pl);  // a tail ends the chain
+      } else if ((cl == NX_FAR || cl == NX_NEAR) && ql < 0x3FFFu) {
+        claim = G.A + ql;  // its frame leaves the listed positions: the successor it declares
+      } else {
+        ok = 0;
+      }
+    } else if (ok) {
+      claim = G.A + (uint32_t)__builtin_amdgcn_readlane((int)pos, (int)exitn);
+    }
+    if (ok) {  // the records: each thread's first chain node, its delivered frames and changes
+      // (chain nodes are in position order: a thread's chain nodes are consecutive chain lanes)
+      const bool on = ((chain >> lane) & 1ull) != 0;
+      const uint32_t th = pos / SEGB;
+      const uint64_t below = chain & ((1ull << lane) - 1ull);
+      const uint32_t prev = below ? 63u - (uint32_t)__builtin_clzll(below) : lane;
+      const uint32_t pth = (uint32_t)__shfl((int)pos, (int)prev, WAVE) / SEGB;
+      const bool first = on && (!below || pth != th);
+      const bool delivered = on && c != NX_TAILC && id != 3u;
+      const uint64_t dm = __ballot(delivered && id != 0u), cm = __ballot(delivered && id == 1u);
+      const uint64_t firsts = __ballot(first);
+      if (first) {
+        const uint64_t later = firsts & ~((2ull << lane) - 1ull);  // (lane 63: none)
+        const uint64_t mine = (later ? ((1ull << __builtin_ctzll(later)) - 1ull) : ~0ull) & ~((1ull << lane) - 1ull);
+        S.sp_eb[th] = (uint8_t)((pos % SEGB) | (lane == g0 ? 0x40u : 0u));
+        S.sp_en[th] = (uint8_t)__builtin_popcountll(dm & mine);
+        S.sp_ec[th] = (uint8_t)__builtin_popcountll(cm & mine);
+      }
+    }
+  }
+  if (lane == 0) {
+    S.sp_ok = ok;
+    S.sp_claim = claim;
+  }
+  (void)se_rel;
+}
+
+// The sparse form of fast_claims' prediction (wave 0 of the workgroup; at most 64 nodes, lane i =
+// node i in position order, parsed into lnd / lal by the caller). Survival is propagated along the
+// successor links with lane shuffles; the prediction is the chain from the first strong tile node,
+// taken only when it is unambiguous: that node does not jump past the tile while another strong
+// node follows, every strong tile node lies on its chain, the chain does not die, and no undecided
+// node (a frame leaving the image that the structural check did not prove) follows the chain's last
+// tile node. Then the records are the chain's: each thread's first chain node (the first carrier
+// flagged as a restart, as the general link rounds flag it), its delivered frames and Change frames,
+// and the claim is the first chain position past the tile (or the chain's end). S.sp_ok = 0 sends
+// the tile to the general phases. No strong node and no undecided one: an identity claim.
+#ifndef DRP_SPARSE_CLAIMS
+#define DRP_SPARSE_CLAIMS 1  // 0: every tile through the general phases (A/B)
+#endif
+struct FastLds;
+__device__ __forceinline__ void sparse_claims(const DecodeParams &P, const TileGeo &G, FastLds &S, uint32_t total,
+                                              uint32_t se_rel);
 // The fast claims of interior tile t: writes the per-thread records (P.ent*) and P.claim[t], and
 // returns this thread's record (eb, en, ecn) and, in thread NT - 1, the claim. FC_DENSE: more than
 // FCAP live positions (the tile went to the general kernel's work list; nothing written).
@@ -1326,6 +1443,28 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   abl_out(P, t, (uint64_t)(ncode[0] + na[1]));
   return FC_ABLATE;
 #endif
+  // Sparse tiles (at most 64 nodes with the halo's: C5's long frames, blob payloads): one wave
+  // decides the prediction with one node per lane and no further barriers, when it is
+  // unambiguous; anything else takes the general phases below (lnd / lal are left as they are).
+  if (DRP_SPARSE_CLAIMS && total <= WAVE) {
+    if (wid == 0) sparse_claims(P, G, S, total, se_rel);
+    bsync();
+    if (S.sp_ok) {
+      const uint64_t ix = t * NT + tid;
+      eb_o = S.sp_eb[tid];
+      en_o = S.sp_en[tid];
+      ecn_o = S.sp_ec[tid];
+      P.ent[ix] = (uint8_t)eb_o;
+      P.ent_n[ix] = (uint8_t)en_o;
+      P.ent_c[ix] = (uint8_t)ecn_o;
+      cl_o = 0;
+      if (tid == NT - 1) {
+        P.claim[t] = S.sp_claim;
+        cl_o = S.sp_claim;
+      }
+      return FC_OK;
+    }
+  }
   lmw[tid] = 0;  // (now the strong masks)
   dmw[tid] = 0;
   // ---- survival: KSTRONG - 1 rounds propagate death / undecided back along the chains ------------
@@ -2166,6 +2305,7 @@ __global__ __launch_bounds__(256) void emit_sparse(DecodeParams P) {
   __shared__ uint32_t lst[SP_TPB * SP_FRAMES];  // tile (in the workgroup) << 16 | thread << 8 | rank
   __shared__ uint32_t nl;
   __shared__ uint32_t fail[SP_TPB];
+  if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
   const uint32_t tid = threadIdx.x;
   const uint64_t t0 = (uint64_t)blockIdx.x * SP_TPB;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
@@ -2270,6 +2410,7 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wid = tid >> 6;
   uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
+  if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   const uint32_t nwork = (!FAST && P.vlist) ? *P.vlist_n : 0u;
   for (uint32_t wi = blockIdx.x; (!FAST && P.vlist) ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
@@ -2355,6 +2496,208 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
   badf = lane_min64(badf);
   if (lane == 0 && badf != ~0ull) atomicMin((unsigned long long *)&P.payload_err[G.s], (unsigned long long)badf);
   }
+}
+
+// ---- the lean fast emit ------------------------------------------------------------------------
+// Most tiles hold only Change payloads in protocol-buffers@2's own field order with short varints
+// (the shape every encoder writes) and at most a few frames per 64-byte thread segment. For those,
+// emit_lean walks each thread's frames from its verified entry and decodes each one in place from
+// the LDS image: the header from one 8-byte window, the fields in canonical order (one window per
+// field, or one window for change / from / to / the value header when their varints are one byte),
+// 32-bit image offsets, and column stores at the tile's row base plus a 32-bit byte offset. Any
+// other shape (field order, repeated or unknown fields, varints of more than 5 bytes, headers
+// near the image end, length varints of more than 3 bytes) sends the whole tile to the general
+// kernel (emit_tiles<false> over P.vlist), which writes the same columns for the rest.
+#ifndef DRP_EMIT_LEAN
+#define DRP_EMIT_LEAN 1  // 0: emit_tiles<true> as the fast emit (A/B)
+#endif
+#ifndef DRP_EMIT_LEAN_WAVES
+#define DRP_EMIT_LEAN_WAVES 6
+#endif
+// bytes o .. o + 7 of the image (three dword reads; the image has 32 bytes of slack)
+__device__ __forceinline__ uint64_t lds_u64(const uint8_t *lds, uint32_t o) {
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(lds) + (o >> 2);
+  const uint32_t sh = (o & 3u) * 8u, a0 = q[0], a1 = q[1], a2 = q[2];
+  return (uint64_t)__builtin_amdgcn_alignbit(a1, a0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, sh) << 32);
+}
+// a varint of 1..5 bytes at the start of x: its length (0: none ends within 5 bytes) and value
+__device__ __forceinline__ uint32_t vint5(uint64_t x, uint64_t &v) {
+  const uint64_t tm = ~x & 0x8080808080ull;
+  if (!tm) return 0;
+  const uint32_t k = ((uint32_t)__builtin_ctzll(tm) >> 3) + 1u;
+  v = ((x & 0x7Full) | ((x >> 1) & 0x3F80ull) | ((x >> 2) & 0x1FC000ull) | ((x >> 3) & 0xFE00000ull) |
+       ((x >> 4) & 0x7F0000000ull)) &
+      ((1ull << (7u * k)) - 1ull);
+  return k;
+}
+// a length-delimited field (tag already checked) at image offset q: its content offset and length;
+// false when the header leaves [0, lim) or the content leaves the payload (ending at end)
+__device__ __forceinline__ bool ld_field(uint64_t x, uint32_t q, uint32_t end, uint32_t lim, uint32_t &o2,
+                                         uint32_t &len) {
+  uint64_t v;
+  const uint32_t k = vint5(x >> 8, v);
+  o2 = q + 1u + k;
+  if (!k || o2 > lim || o2 > end || v > (uint64_t)(end - o2)) return false;
+  len = (uint32_t)v;
+  return true;
+}
+// a varint field (tag already checked) at q: its value; false as above
+__device__ __forceinline__ bool vi_field(uint64_t x, uint32_t q, uint32_t end, uint32_t lim, uint32_t &q2,
+                                         uint64_t &v) {
+  const uint32_t k = vint5(x >> 8, v);
+  q2 = q + 1u + k;
+  return k && q2 <= lim && q2 <= end;
+}
+// The canonical Change at image offset po (pl bytes; the payload may run past the image, its
+// field headers may not): [0x0a subset] 0x12 key 0x18 change 0x20 from 0x28 to [0x32 value],
+// ending exactly at the payload end. Offsets relative to the payload, as decode_change's.
+__device__ __forceinline__ bool change_canon(const uint8_t *lds, uint32_t po, uint32_t pl, uint32_t lim,
+                                             ChangeCols &c) {
+  const uint32_t end = po + pl;
+  c.subset_off = c.subset_len = c.value_off = c.value_len = 0;
+  c.flags = 0;
+  c.err = 0;
+  uint32_t q = po, o2, len;
+  uint64_t x = lds_u64(lds, q);
+  if ((x & 0xFFu) == 0x0Au) {
+    if (!ld_field(x, q, end, lim, o2, len)) return false;
+    c.subset_off = o2 - po;
+    c.subset_len = len;
+    c.flags = DRP_F_SUBSET;
+    q = o2 + len;
+    if (q >= lim) return false;
+    x = lds_u64(lds, q);
+  }
+  if ((x & 0xFFu) != 0x12u || !ld_field(x, q, end, lim, o2, len)) return false;
+  c.key_off = o2 - po;
+  c.key_len = len;
+  q = o2 + len;
+  if (q + 8u <= lim) {
+    x = lds_u64(lds, q);
+    // change / from / to (and the value header) with one-byte varints: 18 a 20 b 28 c [32 d]
+    if ((x & 0x00FF00FF00FF00FFull) == 0x0032002800200018ull && (x & 0x8080808080808080ull) == 0 &&
+        q + 8u + (uint32_t)(x >> 56) == end) {
+      c.change = (x >> 8) & 0xFFu;
+      c.from = (x >> 24) & 0xFFu;
+      c.to = (x >> 40) & 0xFFu;
+      c.value_off = q + 8u - po;
+      c.value_len = (uint32_t)(x >> 56);
+      c.flags |= DRP_F_VALUE;
+      return true;
+    }
+  }
+  if (q >= lim) return false;
+  x = lds_u64(lds, q);
+  if ((x & 0xFFu) != 0x18u || !vi_field(x, q, end, lim, q, c.change) || q >= lim) return false;
+  x = lds_u64(lds, q);
+  if ((x & 0xFFu) != 0x20u || !vi_field(x, q, end, lim, q, c.from) || q >= lim) return false;
+  x = lds_u64(lds, q);
+  if ((x & 0xFFu) != 0x28u || !vi_field(x, q, end, lim, q, c.to)) return false;
+  if (q == end) return true;
+  if (q >= lim) return false;
+  x = lds_u64(lds, q);
+  if ((x & 0xFFu) != 0x32u || !ld_field(x, q, end, lim, o2, len) || o2 + len != end) return false;
+  c.value_off = o2 - po;
+  c.value_len = len;
+  c.flags |= DRP_F_VALUE;
+  return true;
+}
+// a store at a uniform column base plus a 32-bit byte offset (global_store ... saddr)
+template <class T>
+__device__ __forceinline__ void st_col(T *base, uint32_t i, T v) {
+  *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (uint32_t)(i * (uint32_t)sizeof(T))) = v;
+}
+
+__global__ __launch_bounds__(NT, DRP_EMIT_LEAN_WAVES) void emit_lean(DecodeParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+  __shared__ uint32_t wsum[NT / WAVE];
+  __shared__ uint32_t defer;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
+  const uint64_t ntiles = P.tile_prefix[P.nstreams];
+  uint64_t t;
+  {  // XCD-contiguous tile order, as the fast emit_tiles
+    const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = blockIdx.x % 8u;
+    t = (uint64_t)x * q + min(x, r) + blockIdx.x / 8u;
+  }
+  const TileGeo G = tile_geo(P, t);
+  if (t >= ntiles) return;  // (whole workgroup)
+  if (P.tile_sparse && P.tile_sparse[t]) return;  // emit_sparse wrote it
+  const uint64_t A = G.A;
+  const uint32_t se_rel = (uint32_t)umin64(G.se - A, 0x7FFFFFFFull);
+  const uint32_t lim = se_rel < IMG ? se_rel : IMG;  // image bytes of the stream
+  const uint64_t base = ldc(P.tile_base + t);
+  const uint32_t k0 = P.tile_k ? P.tile_k[t] : 0u;
+  const uint8_t eb = tid < k0 ? (uint8_t)0xFF : P.ent[t * NT + tid];  // exact entry of this thread's bytes
+  const uint8_t en = P.ent_n[t * NT + tid];                            // frames from it
+  if (tid == 0) defer = 0;
+  stage_glds(P, G, buf);
+  const uint32_t n = (eb & 0x80) ? 0u : en;
+  const uint32_t ni = wave_scan_dpp(n);
+  if (lane == 63) wsum[wid] = ni;
+  bsync();
+  uint32_t i = ni - n;
+#pragma unroll
+  for (uint32_t w = 0; w < NT / WAVE; w++)
+    if (w < wid) i += wsum[w];
+  const RowCols C = row_cols(P, base);
+  bool ok = true;
+  if (n) {
+    uint32_t o = tid * SEGB + (eb & 63u);
+    const uint32_t s1r = tid * SEGB + SEGB;
+    while (o < s1r && o < se_rel) {
+      if (o + 16u > lim) {  // a header near the image or stream end: the general kernel
+        ok = false;
+        break;
+      }
+      const uint32_t w = (uint32_t)lds_u64(buf, o);
+      const uint32_t tm = ~w & 0x808080u;
+      if (!tm) {  // a length varint of 4 bytes or more
+        ok = false;
+        break;
+      }
+      const uint32_t k = ((uint32_t)__builtin_ctz(tm) >> 3) + 1u;
+      const uint32_t L = ((w & 0x7Fu) | ((w >> 1) & 0x3F80u) | ((w >> 2) & 0x1FC000u)) & ((1u << (7u * k)) - 1u);
+      const uint32_t id = (w >> (8u * k)) & 0xFFu;
+      if (id == 0u) {  // (a type-0 header: nothing delivered, the next header follows its id byte)
+        o += k + 1u;
+        continue;
+      }
+      if (id > 2u || L == 0u) break;  // a protocol error ends the chain here (finalize reports it)
+      const uint32_t po = o + k + 1u, pl = L - 1u;
+      const bool tail = L > se_rel - o - k;  // cut by the stream end
+      if (tail && id == 1u) break;           // (a Change cut by the stream end is carried, not delivered)
+      if (i < C.lim) {
+        st_col(C.poff, i, A + po);
+        st_col(C.plen, i, pl);
+        st_col(C.type, i, (uint8_t)(id | (tail ? DRP_FRAME_PARTIAL : 0u)));
+        if (id == 1u) {
+          ChangeCols c;
+          c.change = c.from = c.to = 0;
+          if (!change_canon(buf, po, pl, lim, c)) {
+            ok = false;
+            break;
+          }
+          st_col(C.ko, i, c.key_off);
+          st_col(C.kl, i, c.key_len);
+          st_col(C.so, i, c.subset_off);
+          st_col(C.sl, i, c.subset_len);
+          st_col(C.vo, i, c.value_off);
+          st_col(C.vl, i, c.value_len);
+          st_col(C.ch, i, c.change);
+          st_col(C.fr, i, c.from);
+          st_col(C.to, i, c.to);
+          st_col(C.fl, i, (uint8_t)c.flags);
+        }
+      }
+      i++;
+      if (tail) break;
+      o += k + L;
+    }
+  }
+  if (!ok) defer = 1;
+  bsync();
+  if (defer && tid == 0) P.vlist[atomicAdd(P.vlist_n, 1u)] = (uint32_t)t;
 }
 
 // ==== segmented repair: exact claims for an unsettled stream range ==============================
@@ -2816,7 +3159,10 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
     } else {
       Q.tile_sparse = nullptr;
     }
-    hipLaunchKernelGGL(spec::emit_tiles<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+    if (DRP_EMIT_LEAN)
+      hipLaunchKernelGGL(spec::emit_lean, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+    else
+      hipLaunchKernelGGL(spec::emit_tiles<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
     hipLaunchKernelGGL(spec::emit_tiles<false>, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0,
                        st, Q);
   } else {
@@ -2827,6 +3173,28 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
   if (e != hipSuccess) return e;
   return drp_launch_stream_counts(Q.tile_prefix, nstreams, Q.tile_count, Q.tile_base, Q.tile_nch, Q.tile_nch_base,
                                   Q.scount, st, Q.counter + 3);
+}
+
+// Measurement hook (scripts/probe_overlap.py): the C2 claims kernel and the lean emit over every
+// tile of the last decode's parameters, alone and side by side on two streams (the claims kernel
+// rewrites the same records the emit reads, with the same values), each timed with events.
+extern "C" hipError_t drp_probe_overlap_launch(const DecodeParams *P, uint64_t nt_max, hipStream_t a, hipStream_t b,
+                                               hipEvent_t *ev) {
+  DecodeParams Q = *P;
+  Q.tile_stream = nullptr;
+  (void)hipEventRecord(ev[0], a);
+  hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, a, Q);
+  (void)hipEventRecord(ev[1], a);
+  hipLaunchKernelGGL(spec::emit_lean, dim3((uint32_t)nt_max), dim3(spec::NT), 0, a, Q);
+  (void)hipEventRecord(ev[2], a);
+  (void)hipStreamWaitEvent(b, ev[2], 0);
+  (void)hipEventRecord(ev[3], a);
+  hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, a, Q);
+  hipLaunchKernelGGL(spec::emit_lean, dim3((uint32_t)nt_max), dim3(spec::NT), 0, b, Q);
+  (void)hipEventRecord(ev[4], b);
+  (void)hipStreamWaitEvent(a, ev[4], 0);
+  (void)hipEventRecord(ev[5], a);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t drp_launch_blob_bytes(const uint8_t *type, const uint32_t *plen, uint64_t n, uint64_t *out,

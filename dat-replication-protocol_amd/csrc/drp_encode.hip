@@ -318,6 +318,39 @@ __device__ __forceinline__ uint32_t put_segs(uint8_t *o, uint32_t lane, const VS
 #ifndef DRP_ENC_MINW
 #define DRP_ENC_MINW 0  // > 0: min waves per SIMD for the write kernel (8: 64 VGPRs, a 28-byte spill)
 #endif
+// The bytes of frame i written by one wave (the header and field prefixes lane-parallel, the key /
+// subset / value bytes by WAVE_COPY).
+__device__ __forceinline__ void write_frame(const EncodeParams &P, uint64_t i, uint32_t lane) {
+  const drp_change_src &s = P.src;
+  uint8_t *o = P.out + P.frame_off[i];
+  const uint32_t fl = s.flags[i];
+  const uint64_t pl = payload_len(s, i);
+  const bool sub = (fl & DRP_F_SUBSET) != 0, val = (fl & DRP_F_VALUE) != 0;
+  uint64_t off;
+  {  // header (encode.js:124-137) + subset prefix
+    const VSeg g[4] = {vseg(pl + 1), vbyte1(DRP_TYPE_CHANGE), vbyte1(0x0a, sub),
+                       sub ? vseg(s.subset_len[i]) : VSeg{0ull, 0u, 0u}};
+    off = put_segs(o, lane, g);
+  }
+  if (sub) {
+    WAVE_COPY(o + off, P.heap + s.subset_off[i], s.subset_len[i], lane);
+    off += s.subset_len[i];
+  }
+  {
+    const VSeg g[2] = {vbyte1(0x12), vseg(s.key_len[i])};
+    off += put_segs(o + off, lane, g);
+    WAVE_COPY(o + off, P.heap + s.key_off[i], s.key_len[i], lane);
+    off += s.key_len[i];
+  }
+  {
+    const VSeg g[8] = {vbyte1(0x18), vseg(s.change[i]), vbyte1(0x20), vseg(s.from[i]), vbyte1(0x28), vseg(s.to[i]),
+                       vbyte1(0x32, val), val ? vseg(s.value_len[i]) : VSeg{0ull, 0u, 0u}};
+    off += put_segs(o + off, lane, g);
+  }
+  if (val) WAVE_COPY(o + off, P.heap + s.value_off[i], s.value_len[i], lane);
+}
+
+// one wave per frame (grid-stride over frames): every frame (DRP_ENC_OS=0, A/B)
 #if DRP_ENC_MINW
 __global__ __launch_bounds__(256, DRP_ENC_MINW) void enc_write_kernel(EncodeParams P) {
 #else
@@ -327,85 +360,264 @@ __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
   const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   if (P.frame_off[P.n] > P.cap) return;
-  const drp_change_src &s = P.src;
-  for (uint64_t i = wid; i < P.n; i += nw) {
-    uint8_t *o = P.out + P.frame_off[i];
-    const uint32_t fl = s.flags[i];
-    const uint64_t pl = payload_len(s, i);
-#if DRP_ENC_LANEPREFIX
-    const bool sub = (fl & DRP_F_SUBSET) != 0, val = (fl & DRP_F_VALUE) != 0;
-    uint64_t off;
-    {  // header (encode.js:124-137) + subset prefix
-      const VSeg g[4] = {vseg(pl + 1), vbyte1(DRP_TYPE_CHANGE), vbyte1(0x0a, sub),
-                         sub ? vseg(s.subset_len[i]) : VSeg{0ull, 0u, 0u}};
-      off = put_segs(o, lane, g);
-    }
-    if (sub) {
-      WAVE_COPY(o + off, P.heap + s.subset_off[i], s.subset_len[i], lane);
-      off += s.subset_len[i];
-    }
-    {
-      const VSeg g[2] = {vbyte1(0x12), vseg(s.key_len[i])};
-      off += put_segs(o + off, lane, g);
-      WAVE_COPY(o + off, P.heap + s.key_off[i], s.key_len[i], lane);
-      off += s.key_len[i];
-    }
-    {
-      const VSeg g[8] = {vbyte1(0x18), vseg(s.change[i]), vbyte1(0x20), vseg(s.from[i]), vbyte1(0x28), vseg(s.to[i]),
-                         vbyte1(0x32, val), val ? vseg(s.value_len[i]) : VSeg{0ull, 0u, 0u}};
-      off += put_segs(o + off, lane, g);
-    }
-    if (val) WAVE_COPY(o + off, P.heap + s.value_off[i], s.value_len[i], lane);
-#else
-    // header + subset prefix
-    uint8_t pre[32];
-    uint32_t h = venc(pl + 1, pre);
-    pre[h++] = DRP_TYPE_CHANGE;
-    uint64_t off = 0;
-    if (lane == 0)
-      for (uint32_t k = 0; k < h; k++) o[k] = pre[k];
-    off = h;
-    if (fl & DRP_F_SUBSET) {
-      uint8_t t[12];
-      uint32_t m = 0;
-      t[m++] = 0x0a;
-      m += venc(s.subset_len[i], t + m);
-      if (lane == 0)
-        for (uint32_t k = 0; k < m; k++) o[off + k] = t[k];
-      off += m;
-      wave_copy(o + off, P.heap + s.subset_off[i], s.subset_len[i], lane);
-      off += s.subset_len[i];
-    }
-    {
-      uint8_t t[12];
-      uint32_t m = 0;
-      t[m++] = 0x12;
-      m += venc(s.key_len[i], t + m);
-      if (lane == 0)
-        for (uint32_t k = 0; k < m; k++) o[off + k] = t[k];
-      off += m;
-      wave_copy(o + off, P.heap + s.key_off[i], s.key_len[i], lane);
-      off += s.key_len[i];
-    }
-    {
-      uint8_t t[48];  // 3 tags + 3 u64 varints (<= 10 B each) + value tag + u32 length varint = 39 B
-      uint32_t m = 0;
-      t[m++] = 0x18;
-      m += venc(s.change[i], t + m);
-      t[m++] = 0x20;
-      m += venc(s.from[i], t + m);
-      t[m++] = 0x28;
-      m += venc(s.to[i], t + m);
-      if (fl & DRP_F_VALUE) {
-        t[m++] = 0x32;
-        m += venc(s.value_len[i], t + m);
-      }
-      if (lane == 0)
-        for (uint32_t k = 0; k < m; k++) o[off + k] = t[k];
-      off += m;
-    }
-    if (fl & DRP_F_VALUE) wave_copy(o + off, P.heap + s.value_off[i], s.value_len[i], lane);
+  for (uint64_t i = wid; i < P.n; i += nw) write_frame(P, i, lane);
+}
+
+// ---- output-stationary write ------------------------------------------------------------------
+// The output is cut into 16 KiB blocks aligned in memory; a workgroup owns one block and each lane
+// fixed 16-byte chunks of it. The workgroup lays out the frames the block touches in LDS (their
+// starts, segment ends, heap offsets and prefix bytes), then every lane finds its chunk's frame and
+// segment: a chunk inside one key / subset / value copy (nearly all of a 4 KB value) is two aligned
+// heap loads, a funnel shift and one aligned 16-byte store, with no per-frame latency chain; a
+// chunk that mixes segments is assembled byte by byte. Blocks touching more than ENC_FMAX frames
+// (short frames) are left to the per-frame writer (enc_write_dense).
+#ifndef DRP_ENC_OS
+#define DRP_ENC_OS 1  // 0: the per-frame writer for every frame (A/B)
 #endif
+constexpr uint32_t ENC_BS = 16384, ENC_CPB = ENC_BS / 16, ENC_OS_T = 256, ENC_FMAX = 192;
+constexpr uint32_t LIT0 = 0, LIT2 = 24, LIT4 = 32, LITB = 72;  // prefix byte slots per frame
+constexpr uint32_t ENC_F_DENSE_FRAME = 1u << 31;               // (frame bytes that do not fit 31 bits)
+
+// wire offset of output block b's first byte (blocks are aligned in memory; out may not be)
+__device__ __forceinline__ int64_t oblk_start(uint64_t b, uint32_t g) { return (int64_t)(b * ENC_BS) - (int64_t)g; }
+
+// oblk_first[b] = the frame holding block b's first wire byte (block 0: byte 0)
+__global__ __launch_bounds__(256) void enc_oblk_kernel(EncodeParams P) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= P.n || P.frame_off[P.n] > P.cap) return;
+  const uint64_t g = (uintptr_t)P.out & 15;
+  const uint64_t lo = P.frame_off[i], hi = P.frame_off[i + 1];
+  const uint64_t b0 = i == 0 ? 0 : (lo + g + ENC_BS - 1) / ENC_BS, b1 = (hi + g + ENC_BS - 1) / ENC_BS;
+  for (uint64_t b = b0; b < b1 && b < P.nob; b++) P.oblk_first[b] = i;
+}
+
+__device__ __forceinline__ uint32_t put_lit(uint8_t *d, const VSeg &v) {
+  for (uint32_t k = 0; k < v.n; k++) d[k] = (uint8_t)(k < 8 ? v.lo >> (8 * k) : (uint64_t)(v.hi >> (8 * (k - 8))));
+  return v.n;
+}
+
+// bytes o .. o + 7 of an LDS byte array (three dword reads; any o)
+__device__ __forceinline__ uint64_t enc_lds_u64(const uint8_t *lds, uint32_t o) {
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(lds) + (o >> 2);
+  const uint32_t sh = (o & 3u) * 8u, a0 = q[0], a1 = q[1], a2 = q[2];
+  return (uint64_t)__builtin_amdgcn_alignbit(a1, a0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, sh) << 32);
+}
+
+struct EncLds {
+  int64_t fst[ENC_FMAX + 1];  // frame starts (wire offsets); [nf] = the last frame's end
+  uint32_t e[5][ENC_FMAX];    // segment ends relative to the frame start: L0 | subset | L2 | key | L4 (| value)
+  uint64_t src[3][ENC_FMAX];  // heap offsets of subset, key, value
+  __attribute__((aligned(4))) uint8_t lit[ENC_FMAX][LITB];
+  uint8_t slack[32];  // (16-byte windows read past the last prefix slot)
+};
+
+__global__ __launch_bounds__(ENC_OS_T) void enc_write_os(EncodeParams P) {
+  __shared__ EncLds S;
+  const uint64_t W = P.frame_off[P.n];
+  if (W > P.cap) return;
+  const uint32_t g = (uint32_t)((uintptr_t)P.out & 15);
+  const uint64_t b = blockIdx.x;
+  const int64_t bs = oblk_start(b, g);
+  if (bs >= (int64_t)W) return;  // (whole workgroup)
+  const int64_t be = bs + (int64_t)ENC_BS;
+  const uint64_t f0 = P.oblk_first[b];
+  uint64_t f1 = P.n;  // frames [f0, f1) touch the block
+  if (be < (int64_t)W) {
+    const uint64_t nb = P.oblk_first[b + 1];
+    f1 = P.frame_off[nb] < (uint64_t)be ? nb + 1 : nb;
+  }
+  const uint32_t t = threadIdx.x;
+  if (f1 - f0 > ENC_FMAX) {
+    if (t == 0) P.dense[atomicAdd(P.dense_n, 1u)] = (uint32_t)b;
+    return;
+  }
+  const uint32_t nf = (uint32_t)(f1 - f0);
+  bool big = false;
+  if (t < nf) {
+    const drp_change_src &s = P.src;
+    const uint64_t i = f0 + t;
+    const uint32_t fl = s.flags[i];
+    const bool sub = (fl & DRP_F_SUBSET) != 0, val = (fl & DRP_F_VALUE) != 0;
+    const uint32_t sl = sub ? s.subset_len[i] : 0u, kl = s.key_len[i], vl = val ? s.value_len[i] : 0u;
+    const uint64_t pl = payload_len(s, i);
+    uint8_t *l = S.lit[t];
+    uint32_t x = put_lit(l + LIT0, vseg(pl + 1));
+    l[LIT0 + x++] = DRP_TYPE_CHANGE;
+    if (sub) {
+      l[LIT0 + x++] = 0x0a;
+      x += put_lit(l + LIT0 + x, vseg(sl));
+    }
+    uint32_t y = 0;
+    l[LIT2 + y++] = 0x12;
+    y += put_lit(l + LIT2 + y, vseg(kl));
+    uint32_t z = 0;
+    l[LIT4 + z++] = 0x18;
+    z += put_lit(l + LIT4 + z, vseg(s.change[i]));
+    l[LIT4 + z++] = 0x20;
+    z += put_lit(l + LIT4 + z, vseg(s.from[i]));
+    l[LIT4 + z++] = 0x28;
+    z += put_lit(l + LIT4 + z, vseg(s.to[i]));
+    if (val) {
+      l[LIT4 + z++] = 0x32;
+      z += put_lit(l + LIT4 + z, vseg(vl));
+    }
+    const uint64_t fs = P.frame_off[i];
+    const uint64_t e0 = x, e1 = e0 + sl, e2 = e1 + y, e3 = e2 + kl, e4 = e3 + z, e5 = e4 + vl;
+    big = e5 >= ENC_F_DENSE_FRAME;
+    S.fst[t] = (int64_t)fs;
+    S.e[0][t] = (uint32_t)e0;
+    S.e[1][t] = (uint32_t)e1;
+    S.e[2][t] = (uint32_t)e2;
+    S.e[3][t] = (uint32_t)e3;
+    S.e[4][t] = (uint32_t)e4;
+    S.src[0][t] = s.subset_off[i] * (sub ? 1u : 0u);
+    S.src[1][t] = s.key_off[i];
+    S.src[2][t] = val ? s.value_off[i] : 0ull;
+  }
+  if (t == 0) S.fst[nf] = (int64_t)P.frame_off[f1];
+  if (__syncthreads_or(big)) {  // (a frame of 2^31 bytes or more: the per-frame writer)
+    if (t == 0) P.dense[atomicAdd(P.dense_n, 1u)] = (uint32_t)b;
+    return;
+  }
+  // ENC_CPB / ENC_OS_T chunks per lane, strided by the workgroup (each pass of the workgroup stores
+  // 4 KiB contiguous). Every chunk's frame and segment are looked up first, then every heap load
+  // of the lane's whole-copy chunks is issued, then the stores: a lane keeps 8 loads in flight.
+  constexpr uint32_t U = ENC_CPB / ENC_OS_T;
+  const uint4 *sa[U];
+  uint32_t shv[U];
+  bool fast[U];
+#pragma unroll
+  for (uint32_t u = 0; u < U; u++) {
+    const int64_t c0 = bs + 16 * (int64_t)(t + u * ENC_OS_T);
+    fast[u] = false;
+    sa[u] = nullptr;
+    shv[u] = 0;
+    if (c0 >= 0 && c0 + 16 <= (int64_t)W) {
+      uint32_t lo = 0, hi = nf;  // fst[lo] <= c0 < fst[hi]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (S.fst[mid] <= c0) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t r = (uint32_t)(c0 - S.fst[lo]);
+      const uint32_t fe = (uint32_t)(S.fst[lo + 1] - S.fst[lo]);
+      const uint32_t e0 = S.e[0][lo], e1 = S.e[1][lo], e2 = S.e[2][lo], e3 = S.e[3][lo], e4 = S.e[4][lo];
+      // a copy segment holding the whole chunk: subset [e0, e1), key [e2, e3), value [e4, end)
+      uint32_t a = 0xFFFFFFFFu, seg = 0;
+      if (r >= e4 && r + 16 <= fe) a = e4, seg = 2;
+      else if (r >= e2 && r + 16 <= e3) a = e2, seg = 1;
+      else if (r >= e0 && r + 16 <= e1) a = e0, seg = 0;
+      if (a != 0xFFFFFFFFu) {
+        const uint8_t *sp = P.heap + S.src[seg][lo] + (r - a);
+        shv[u] = (uint32_t)((uintptr_t)sp & 15);
+        sa[u] = reinterpret_cast<const uint4 *>(sp - shv[u]);
+        fast[u] = true;
+      }
+    }
+  }
+  uint4 v0[U], v1[U];
+#pragma unroll
+  for (uint32_t u = 0; u < U; u++) {
+    v0[u] = v1[u] = make_uint4(0, 0, 0, 0);
+    if (fast[u]) {
+      v0[u] = sa[u][0];
+      if (shv[u]) v1[u] = sa[u][1];
+    }
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < U; u++)
+    if (fast[u])
+      *reinterpret_cast<uint4 *>(P.out + bs + 16 * (int64_t)(t + u * ENC_OS_T)) =
+          shv[u] ? enc_shift(v0[u], v1[u], shv[u]) : v0[u];
+  // chunks that mix segments (and the output's first / last chunk): piece by piece (a piece = the
+  // chunk bytes of one segment of one frame), each piece as one 16-byte window shifted into place
+  // and masked: two aligned loads for heap bytes, LDS reads for prefix bytes, no byte loops
+#pragma unroll 1
+  for (uint32_t u = 0; u < U; u++) {
+    const int64_t c0 = bs + 16 * (int64_t)(t + u * ENC_OS_T);
+    if (fast[u] || c0 >= (int64_t)W) continue;
+    const int64_t p0 = c0 < 0 ? 0 : c0;
+    uint32_t j = 0, hi = nf;
+    while (hi - j > 1) {
+      const uint32_t mid = (j + hi) >> 1;
+      if (S.fst[mid] <= p0) j = mid;
+      else hi = mid;
+    }
+    const int64_t ce = c0 + 16 < (int64_t)W ? c0 + 16 : (int64_t)W;
+    uint64_t acc0 = 0, acc1 = 0;  // the chunk's bytes 0..7, 8..15
+    int64_t w = p0;
+    while (w < ce) {
+      while (w >= S.fst[j + 1]) j++;
+      const int64_t fs = S.fst[j];
+      const uint32_t r = (uint32_t)(w - fs);
+      const uint32_t ends[6] = {S.e[0][j], S.e[1][j], S.e[2][j], S.e[3][j], S.e[4][j],
+                                (uint32_t)(S.fst[j + 1] - fs)};
+      uint32_t sg = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 5; q++) sg += r >= ends[q] ? 1u : 0u;
+      const uint32_t a = sg ? ends[sg - 1] : 0u;
+      const int64_t pe = fs + ends[sg] < ce ? fs + ends[sg] : ce;  // this piece: wire bytes [w, pe)
+      const uint32_t q0 = (uint32_t)(w - c0), q1 = (uint32_t)(pe - c0);
+      uint64_t v0, v1;  // 16 bytes from the piece's first byte on
+      if (sg & 1u) {
+        const uint8_t *sp = P.heap + S.src[sg >> 1][j] + (r - a);
+        const uint32_t sh = (uint32_t)((uintptr_t)sp & 15);
+        const uint4 *ab = reinterpret_cast<const uint4 *>(sp - sh);
+        const uint4 b0 = ab[0];
+        const uint4 b1 = sh + (q1 - q0) > 16u ? ab[1] : b0;  // (only blocks holding piece bytes)
+        const uint4 x = enc_shift(b0, b1, sh);
+        v0 = ((uint64_t)x.y << 32) | x.x;
+        v1 = ((uint64_t)x.w << 32) | x.z;
+      } else {
+        const uint32_t lo = (uint32_t)(&S.lit[j][sg == 0 ? LIT0 : sg == 2 ? LIT2 : LIT4] - &S.lit[0][0]) + (r - a);
+        v0 = enc_lds_u64(&S.lit[0][0], lo);
+        v1 = enc_lds_u64(&S.lit[0][0], lo + 8u);
+      }
+      // shift left by q0 bytes, keep bytes [q0, q1)
+      const uint32_t b = 8u * q0;
+      uint64_t s0, s1;
+      if (b == 0) s0 = v0, s1 = v1;
+      else if (b < 64) s0 = v0 << b, s1 = (v1 << b) | (v0 >> (64u - b));
+      else s0 = 0, s1 = v0 << (b - 64u);
+      const uint32_t e = 8u * q1;
+      const uint64_t m0 = (e >= 64 ? ~0ull : (1ull << e) - 1ull) & (b >= 64 ? 0ull : ~0ull << b);
+      const uint64_t m1 = (e <= 64 ? 0ull : (e >= 128 ? ~0ull : (1ull << (e - 64u)) - 1ull)) &
+                          (b <= 64 ? ~0ull : ~0ull << (b - 64u));
+      acc0 |= s0 & m0;
+      acc1 |= s1 & m1;
+      w = pe;
+    }
+    if (c0 >= 0 && c0 + 16 <= (int64_t)W) {
+      *reinterpret_cast<uint4 *>(P.out + c0) =
+          make_uint4((uint32_t)acc0, (uint32_t)(acc0 >> 32), (uint32_t)acc1, (uint32_t)(acc1 >> 32));
+    } else {  // the output's first or last chunk: only its own bytes
+      for (int64_t x = p0; x < ce; x++) {
+        const uint32_t q = (uint32_t)(x - c0);
+        P.out[x] = (uint8_t)((q < 8 ? acc0 >> (8 * q) : acc1 >> (8 * (q - 8))) & 0xFF);
+      }
+    }
+  }
+}
+
+// The frames of the blocks enc_write_os left (more than ENC_FMAX frames, or a frame of 2^31 bytes
+// or more), one wave per frame; a frame shared with a neighbouring block is rewritten with the
+// same bytes.
+__global__ __launch_bounds__(256) void enc_write_dense(EncodeParams P) {
+  const uint64_t W = P.frame_off[P.n];
+  if (W > P.cap) return;
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  const uint32_t nd = *P.dense_n;
+  const uint32_t g = (uint32_t)((uintptr_t)P.out & 15);
+  for (uint32_t d = blockIdx.x; d < nd; d += gridDim.x) {
+    const uint64_t b = P.dense[d];
+    const int64_t be = oblk_start(b, g) + (int64_t)ENC_BS;
+    const uint64_t f0 = P.oblk_first[b];
+    uint64_t f1 = P.n;
+    if (be < (int64_t)W) {
+      const uint64_t nb = P.oblk_first[b + 1];
+      f1 = P.frame_off[nb] < (uint64_t)be ? nb + 1 : nb;
+    }
+    for (uint64_t i = f0 + wv; i < f1; i += 4) write_frame(P, i, lane);
   }
 }
 
@@ -451,6 +663,10 @@ __global__ void stats_kernel(const drp_stream_result *res, const uint64_t *strea
 
 using namespace drp;
 
+// output blocks of the write for an output of capacity cap (the grid covers the largest output
+// the capacity allows; blocks past the real end exit at once)
+extern "C" uint64_t drp_encode_out_blocks(uint64_t cap) { return (cap + 15) / ENC_BS + 2; }
+
 extern "C" hipError_t drp_launch_encode(const EncodeParams *Pp, hipStream_t st) {
   EncodeParams P = *Pp;
   if (P.n == 0) return hipSuccess;
@@ -458,7 +674,13 @@ extern "C" hipError_t drp_launch_encode(const EncodeParams *Pp, hipStream_t st) 
   hipLaunchKernelGGL(enc_size_kernel, dim3((uint32_t)nblk), dim3(SCAN_BLK), 0, st, P);
   hipLaunchKernelGGL(enc_blocksum_kernel, dim3(1), dim3(SCAN_BLK), 0, st, P, nblk);
   hipLaunchKernelGGL(enc_addbase_kernel, dim3((uint32_t)nblk), dim3(SCAN_BLK), 0, st, P);
-  if (P.out) {
+  if (P.out && DRP_ENC_OS && P.nob && P.nob < (1ull << 31)) {
+    hipLaunchKernelGGL(enc_oblk_kernel, dim3((uint32_t)((P.n + 255) / 256)), dim3(256), 0, st, P);
+    hipError_t e = hipMemsetAsync(P.dense_n, 0, 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(enc_write_os, dim3((uint32_t)P.nob), dim3(ENC_OS_T), 0, st, P);
+    hipLaunchKernelGGL(enc_write_dense, dim3(2048), dim3(256), 0, st, P);
+  } else if (P.out) {
     uint64_t waves = P.n < DRP_ENC_WAVES ? P.n : DRP_ENC_WAVES;  // one frame per wave at a time
     uint32_t grid = (uint32_t)((waves * 64 + 255) / 256);
     hipLaunchKernelGGL(enc_write_kernel, dim3(grid), dim3(256), 0, st, P);

@@ -85,6 +85,12 @@ struct EncodeParams {
   uint64_t cap;
   uint64_t *block_sum;  // per-block partial sums (scan scratch)
   uint32_t *overflow;  // bit 0 output capacity, bit 1 a row's heap range is out of bounds
+  // output-stationary write (enc_write_os): per output block of ENC_BS bytes the first frame whose
+  // bytes it holds, the blocks left to the per-frame writer (more frames than fit its LDS), count
+  uint64_t *oblk_first;
+  uint32_t *dense;
+  uint32_t *dense_n;
+  uint64_t nob;  // output blocks the grid covers (from cap)
 };
 
 }  // namespace drp
@@ -121,12 +127,17 @@ hipError_t drp_launch_finalize(const uint8_t *bytes, const uint64_t *stream_off,
                                const uint64_t *tile_base, const uint64_t *tile_count,
                                const uint64_t *payload_err, const uint64_t *scount,
                                const uint8_t *type, const uint8_t *flags, uint64_t cap,
-                               drp_stream_result *res, hipStream_t st);
+                               drp_stream_result *res, const uint32_t *abort_flag,
+                               uint32_t abort_mask, hipStream_t st);
 hipError_t drp_launch_encode(const drp::EncodeParams *P, hipStream_t st);
+uint64_t drp_encode_out_blocks(uint64_t cap);
+hipError_t drp_probe_overlap_launch(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t a, hipStream_t b,
+                                    hipEvent_t *ev);
 // key hash + key flags for every change frame written (no-op when co->key_hash is NULL)
 hipError_t drp_launch_key_post(const uint8_t *bytes, const uint64_t *tile_prefix, uint64_t nstreams,
                                const uint64_t *tile_base, const uint64_t *tile_count, uint64_t cap,
-                               const drp_frames *fr, const drp_changes *co, int flags_only, hipStream_t st);
+                               const drp_frames *fr, const drp_changes *co, int flags_only, const uint32_t *abort_flag,
+                               uint32_t abort_mask, hipStream_t st);
 hipError_t drp_launch_index_scan(const drp_stream_stats *stats, uint64_t count, uint64_t *base,
                                  hipStream_t st);
 hipError_t drp_launch_stats_from_results(const drp_stream_result *res, const uint64_t *stream_off,

@@ -119,7 +119,9 @@ __global__ __launch_bounds__(256) void key_post_kernel(const uint8_t *bytes, con
                                                        const uint64_t *tile_count, uint64_t cap,
                                                        const uint64_t *payload_off, const uint8_t *type,
                                                        const uint32_t *key_off, const uint32_t *key_len,
-                                                       uint8_t *flags, uint64_t *key_hash) {
+                                                       uint8_t *flags, uint64_t *key_hash,
+                                                       const uint32_t *abort_flag, uint32_t abort_mask) {
+  if (abort_flag && (*abort_flag & abort_mask)) return;  // (a failed prediction: run again after its repair)
   const uint64_t nt = tile_prefix[nstreams];
   uint64_t total = nt ? tile_base[nt - 1] + tile_count[nt - 1] : 0;
   if (total > cap) total = cap;
@@ -144,13 +146,13 @@ __global__ __launch_bounds__(256) void key_post_kernel(const uint8_t *bytes, con
 extern "C" hipError_t drp_launch_key_post(const uint8_t *bytes, const uint64_t *tile_prefix, uint64_t nstreams,
                                           const uint64_t *tile_base, const uint64_t *tile_count, uint64_t cap,
                                           const drp_frames *fr, const drp_changes *co, int flags_only,
-                                          hipStream_t st) {
+                                          const uint32_t *abort_flag, uint32_t abort_mask, hipStream_t st) {
   // the hash when the caller gave a column for it; the key flags also without one (flags_only)
   if ((!co->key_hash && !flags_only) || cap == 0) return hipSuccess;
   uint64_t blocks = (cap + 255) / 256;
   if (blocks > 65536) blocks = 65536;  // grid-stride beyond
   hipLaunchKernelGGL(drp::keys::key_post_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, bytes, tile_prefix,
                      nstreams, tile_base, tile_count, cap, fr->payload_off, fr->type, co->key_off, co->key_len,
-                     co->flags, co->key_hash);
+                     co->flags, co->key_hash, abort_flag, abort_mask);
   return hipGetLastError();
 }

@@ -448,6 +448,58 @@ static napi_value js_encode(napi_env env, napi_callback_info info) {
   return NULL;
 }
 
+/* ---- pinned staging blocks ---------------------------------------------------------------
+ * pinnedBuffer(bytes) -> a Buffer over page-locked host memory (drp_host_alloc), or null. The
+ * decoder coalesces small writes into it, so the batch is copied into HBM by DMA instead of
+ * through the runtime's pageable bounce buffer. Blocks are PIN_BLOCK bytes and recycled: a
+ * block returns to the free list when its Buffer and every slice of it (the change values handed
+ * to callbacks) have been collected, so no live slice ever sees a later batch's bytes. At most
+ * PIN_MAX blocks exist; past that (or for a larger batch) the caller copies into ordinary memory. */
+#define PIN_BLOCK ((size_t)16 << 20 | (size_t)1 << 16)
+#define PIN_MAX 24
+static void *pin_free[PIN_MAX];
+static int pin_nfree, pin_total;
+
+static void pin_release(napi_env env, void *data, void *hint) {
+  (void)hint;
+  int64_t adj;
+  if (pin_nfree < PIN_MAX) pin_free[pin_nfree++] = data;
+  else drp_host_free(data);
+  napi_adjust_external_memory(env, -(int64_t)PIN_BLOCK, &adj);
+}
+
+static void pin_cleanup(void *arg) {
+  (void)arg;
+  while (pin_nfree) drp_host_free(pin_free[--pin_nfree]);
+}
+
+static napi_value js_pinned_buffer(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], out;
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  double want = 0;
+  if (argc < 1 || napi_get_value_double(env, argv[0], &want) != napi_ok || !(want > 0) || want > (double)PIN_BLOCK) {
+    NAPI_CALL(env, napi_get_null(env, &out));
+    return out;
+  }
+  void *p = NULL;
+  if (pin_nfree) {
+    p = pin_free[--pin_nfree];
+  } else if (pin_total < PIN_MAX && drp_host_alloc(PIN_BLOCK, &p) == DRP_OK) {
+    pin_total++;
+  } else {
+    NAPI_CALL(env, napi_get_null(env, &out));
+    return out;
+  }
+  int64_t adj;
+  napi_adjust_external_memory(env, (int64_t)PIN_BLOCK, &adj); /* (so V8 collects spent batches early) */
+  if (napi_create_external_buffer(env, (size_t)want, p, pin_release, NULL, &out) != napi_ok) {
+    pin_free[pin_nfree++] = p;
+    NAPI_CALL(env, napi_get_null(env, &out));
+  }
+  return out;
+}
+
 /* ---- devices and the multi-GPU global index ---------------------------------------------- */
 
 static napi_value js_device_count(napi_env env, napi_callback_info info) {
@@ -606,9 +658,11 @@ static napi_value init(napi_env env, napi_value exports) {
       {"encode", NULL, js_encode, NULL, NULL, NULL, napi_enumerable, NULL},
       {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_enumerable, NULL},
       {"indexAllgather", NULL, js_index_allgather, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"pinnedBuffer", NULL, js_pinned_buffer, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   napi_add_env_cleanup_hook(env, comm_cache_clear, NULL);
+  napi_add_env_cleanup_hook(env, pin_cleanup, NULL);
   napi_value v;
   napi_create_int32(env, drp_abi_version(), &v);
   napi_set_named_property(env, exports, "abiVersion", v);

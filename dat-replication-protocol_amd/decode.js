@@ -70,6 +70,18 @@ BlobStream.prototype._read = function () {
   if (fn) fn()
 }
 
+// The chunks of a batch in one buffer: a page-locked staging block from the addon when one is
+// free (the GPU copy then runs by DMA at the PCIe rate), else ordinary memory. The block is not
+// reused while any slice of this batch is alive (native.js / drp_napi.c pinnedBuffer).
+function coalesce (chunks) {
+  var total = 0
+  for (var i = 0; i < chunks.length; i++) total += chunks[i].length
+  var out = native.pinnedBuffer ? native.pinnedBuffer(total) : null
+  if (out === null) return Buffer.concat(chunks, total)
+  for (var j = 0, at = 0; j < chunks.length; j++) at += chunks[j].copy(out, at)
+  return out
+}
+
 // --- default handlers (decode.js:50-61) -------------------------------------------
 function noopFinalize (cb) { cb() }
 function noopChange (change, cb) { cb() }
@@ -244,7 +256,7 @@ Decoder.prototype._kick = function () {
     chunks.unshift(this._carry)
     this._carry = null
   }
-  var batch = chunks.length === 1 ? chunks[0] : Buffer.concat(chunks)
+  var batch = chunks.length === 1 ? chunks[0] : coalesce(chunks)
   // where each chunk starts in the batch: blob payloads are delivered as slices of the written
   // chunks themselves (decode.js:179-202 slices the chunk it was given), not of the batch copy
   var starts = new Array(chunks.length)

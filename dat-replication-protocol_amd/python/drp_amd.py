@@ -28,6 +28,7 @@ EXPORTS = [
     "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results", "drp_device",
     "drp_comm_id", "drp_comm_init_rank", "drp_comm_init_all", "drp_comm_destroy",
     "drp_index_allgather", "drp_index_allgather_multi", "drp_index_allgather_host", "drp_device_count",
+    "drp_host_alloc", "drp_host_free",
 ]
 KEY_POST_OFF, KEY_POST_HASH, KEY_POST_FLAGS = 0, 1, 2
 BLOB_SKIP_OFF, BLOB_SKIP_AUTO, BLOB_SKIP_ALWAYS = 0, 1, 2

@@ -207,6 +207,12 @@ int drp_set_blob_skip(drp_ctx *ctx, int mode);
 /* Device scratch bytes needed to decode `n` bytes split into `nstreams` streams. */
 uint64_t drp_decode_scratch_bytes(drp_ctx *ctx, uint64_t n, uint64_t nstreams);
 
+/* Page-locked host memory (hipHostMalloc) for staging host batches: a batch the caller assembles
+ * there is copied into HBM by DMA at the full PCIe rate instead of through the runtime's pageable
+ * bounce buffer (the N-API addon coalesces small writes into such blocks). */
+int drp_host_alloc(uint64_t bytes, void **out);
+void drp_host_free(void *p);
+
 /* ---- decode -------------------------------------------------------------- */
 /* Decode `nstreams` independent streams laid end to end in `bytes` (device ptr, 16-byte
  * aligned, `nbytes` long).

@@ -6,6 +6,8 @@
 //   mode "digest": events carry sha256 of keys/values/blob data instead of hex
 //   mode "keyhash": decode({keyHash: true}); change events also carry keyHash (decimal)
 //   mode "ticks": one write per event-loop turn (synchronous acks)
+//   mode "hold": digest events, each change's value digested only at 'finish' (the value buffers are
+//               held across every later batch: a staging block reused too early would show)
 //   mode "h2d": digest events, then one {t: 'timing'} record with the decoder's byte counters and
 //               how many blob pieces were slices of the written chunks
 // DRP_MAX_BATCH in the environment sets the decoder's batch threshold
@@ -24,17 +26,19 @@ var mode = process.argv[4] || ''
 var nth = Number(process.argv[5] || 0)
 var asyncAck = mode === 'async' || mode === 'destroy'
 var ticks = mode === 'ticks'
-var digest = mode === 'digest' || mode === 'h2d'
+var digest = mode === 'digest' || mode === 'h2d' || mode === 'hold'
 function enc (b) {
   return digest ? crypto.createHash('sha256').update(b).digest('hex').slice(0, 16) : b.toString('hex')
 }
 var out = []
+var held = []
 var d = protocol.decode(mode === 'keyhash' ? { keyHash: true } : undefined)
 var seen = 0
 d.change(function (c, cb) {
   var ev = { t: 'change', subset: enc(Buffer.from(c.subset, 'utf8')), key: enc(Buffer.from(c.key, 'utf8')),
     change: c.change, from: c.from, to: c.to, value: c.value === null ? null : enc(c.value) }
   if (mode === 'keyhash') ev.keyHash = c.keyHash.toString()
+  if (mode === 'hold') held.push([ev, c.value])
   out.push(ev)
   if (mode === 'destroy' && ++seen === nth) {
     d.destroy()
@@ -61,6 +65,7 @@ d.blob(function (b, cb) {
 d.on('error', function (e) { out.push({ t: 'error', message: e.message }); done() })
 d.on('close', function () { out.push({ t: 'close' }) })
 d.on('finish', function () {
+  held.forEach(function (h) { h[0].value = h[1] === null ? null : enc(h[1]) })
   out.push({ t: 'finish', changes: d.changes, blobs: d.blobs, bytes: d.bytes })
   if (mode === 'h2d') {
     out.push({ t: 'timing', h2dBytes: d.timing.h2dBytes, h2dSkipped: d.timing.h2dSkipped,

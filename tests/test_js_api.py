@@ -31,7 +31,7 @@ def test_package_loads_without_gpu_use():
                os.path.join(ROOT, "dat-replication-protocol_amd", "lib", "drp.node")))
     out = json.loads(subprocess.check_output([NODE, "-e", code], text=True, timeout=60))
     assert out == ["function", "function", ["abiVersion", "decode", "decodeSync", "deviceCount", "encode",
-                                            "indexAllgather", "open"], 4]
+                                            "indexAllgather", "open", "pinnedBuffer"], 4]
 
 
 def _enc(b, digest):
@@ -252,6 +252,19 @@ def test_c3_blob_payloads_stay_in_host_memory():
           f"skipped {tm['h2dSkipped']} B")
     assert tm["h2dBytes"] <= len(wire) // 4, tm
     assert tm["blobPieces"] >= r["blobs"] and tm["blobPiecesShared"] == tm["blobPieces"], tm
+
+
+@pytest.mark.gpu
+@needs_node
+def test_held_values_survive_later_batches():
+    """Small writes are coalesced into page-locked staging blocks (drp_napi.c pinnedBuffer) that
+    the addon recycles; change values are slices of them. Values held until the end of the
+    stream (digested only at 'finish', ~40 batches later) must still hold their own bytes."""
+    wire = S.c2_stream(600_000, seed=21).tobytes()
+    r, exp = oracle_events(wire, digest=True)
+    got = [e for e in run_js(wire, "65536", "hold", batch=1 << 20) if e["t"] != "close"]
+    assert got[:-1] == exp
+    assert got[-1] == {"t": "finish", "changes": r["changes"], "blobs": r["blobs"], "bytes": len(wire)}
 
 
 @pytest.mark.gpu
