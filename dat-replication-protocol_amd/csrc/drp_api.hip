@@ -276,12 +276,13 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
 }
 
 // Measurement hook, not part of the product path (scripts/probe_overlap.py): after a
-// single-stream decode on the ctx, times its claims kernel alone, its emit kernel alone and both
-// side by side on two streams: ms[0..2].
+// single-stream decode on the ctx, times its claims kernel alone, its emit kernel alone, both side
+// by side on two streams, and both roles in one launch with the emit 0 / 64 / 1024 tiles behind
+// the claims on the same XCD: ms[0..5].
 int drp_probe_overlap(drp_ctx *c, float *ms) {
   if (!c || !ms || !c->lastNT) return DRP_E_INVAL;
   hipStream_t b = nullptr;
-  hipEvent_t ev[6];
+  hipEvent_t ev[10];
   CHK(hipStreamCreateWithFlags(&b, hipStreamNonBlocking));
   for (auto &e : ev) CHK(hipEventCreate(&e));
   CHK(drp_probe_overlap_launch(&c->lastP, c->lastNT, c->st, b, ev));
@@ -290,6 +291,7 @@ int drp_probe_overlap(drp_ctx *c, float *ms) {
   (void)hipEventElapsedTime(&ms[0], ev[0], ev[1]);
   (void)hipEventElapsedTime(&ms[1], ev[1], ev[2]);
   (void)hipEventElapsedTime(&ms[2], ev[3], ev[5]);
+  for (int v = 0; v < 3; v++) (void)hipEventElapsedTime(&ms[3 + v], ev[6 + v], ev[7 + v]);
   for (auto &e : ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(b);
   return DRP_OK;

@@ -1098,129 +1098,12 @@ struct FastLds {
   uint32_t xw[8];
   uint32_t xf[2 * NT / WAVE], wl[NT / WAVE], fl[NT / WAVE];
   uint64_t xm[4];  // candidate masks (two waves): [w] strong, [2 + w] strong and far
-  uint8_t sp_eb[NT], sp_en[NT], sp_ec[NT];  // the sparse form's records (sparse_claims)
-  uint64_t sp_claim;
-  uint32_t sp_ok;
 #ifdef DRP_K1_PAD
   uint8_t pad[DRP_K1_PAD];  // (A/B only: caps the workgroups per CU through LDS)
 #endif
 };
 enum : uint32_t { FC_OK = 0, FC_DENSE = 1, FC_ABLATE = 2 };
 
-__device__ __forceinline__ void sparse_claims(const DecodeParams &P, const TileGeo &G, FastLds &S, uint32_t total,
-                                              uint32_t se_rel) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const bool live = lane < total;
-  const uint32_t nd = live ? S.lnd[lane] : (NX_DEAD | (3u << 30));
-  const uint32_t pos = live ? S.lpos[lane] : 0xFFFFu;
-  const uint32_t c = nd & 0xFFFFu, id = nd >> 30, q = (nd >> 16) & 0x3FFFu;
-  uint32_t a = live ? S.lal[lane] : 0u;
-  // survival: KSTRONG - 1 rounds of "my successor's state", from one snapshot per round
-#pragma unroll
-  for (int r = 1; r < KSTRONG; r++) {
-    const uint32_t b = (uint32_t)__shfl((int)a, (int)(c < WAVE ? c : lane), WAVE);
-    if (a == 1u && c < NX_NEAR && b != 1u) a = b;
-  }
-  const bool tile_node = live && pos < TILE;
-  const uint64_t strong = __ballot(tile_node && a == 1u);
-  const uint64_t und = __ballot(tile_node && a == 2u);
-  if (lane < NT / 2) {  // (records default: no entry)
-    S.sp_eb[lane] = 0xFF;
-    S.sp_eb[lane + NT / 2] = 0xFF;
-    S.sp_en[lane] = S.sp_en[lane + NT / 2] = 0;
-    S.sp_ec[lane] = S.sp_ec[lane + NT / 2] = 0;
-  }
-  uint32_t ok = 1;
-  uint64_t claim = C_ID;
-  if (!strong) {
-    ok = und == 0;  // (undecided nodes: the general phases check them in HBM)
-  } else {
-    const uint32_t g0 = (uint32_t)__builtin_ctzll(strong);
-    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)g0);
-    if ((c0 == NX_FAR || c0 == NX_NEAR) && (strong & (strong - 1))) ok = 0;  // (rule 2's case)
-    // the chain from g0 (a uniform walk over the lanes' successor codes)
-    uint64_t chain = 0;
-    uint32_t j = g0, last = g0, exitn = 0xFFFFFFFFu;
-#pragma unroll 1
-    for (uint32_t step = 0; ok && step < WAVE; step++) {
-      const uint32_t pj = (uint32_t)__builtin_amdgcn_readlane((int)pos, (int)j);
-      if (pj >= TILE) {  // the first chain position past the tile: the claim
-        exitn = j;
-        break;
-      }
-      chain |= 1ull << j;
-      last = j;
-      const uint32_t nj = (uint32_t)__builtin_amdgcn_readlane((int)nd, (int)j);
-      if ((nj >> 30) == 3u) ok = 0;  // (an invalid header on the chain)
-      const uint32_t cj = nj & 0xFFFFu;
-      if (cj < WAVE) {
-        j = cj;
-        continue;
-      }
-      if (cj == NX_DEAD) ok = 0;  // (the chain dies: ambiguous)
-      break;
-    }
-    if (ok && (strong & ~chain)) ok = 0;  // a strong node off the chain
-    if (ok && exitn == 0xFFFFFFFFu) {
-      // the chain ends inside the tile: past its last node only decided (dead) nodes may follow
-      const uint32_t pl = (uint32_t)__builtin_amdgcn_readlane((int)pos, (int)last);
-      const uint64_t after = und & ~((2ull << last) - 1ull);
-      if (after) ok = 0;
-      const uint32_t nl = (uint32_t)__builtin_amdgcn_readlane((int)nd, (int)last);
-      const uint32_t cl = nl & 0xFFFFu, ql = (nl >> 16) & 0x3FFFu;
-      if (cl == NX_TAILB || cl == NX_TAILC) {
-        claim = MARK_TERM | (G.A + pl);  // a tail ends the chain
-      } else if ((cl == NX_FAR || cl == NX_NEAR) && ql < 0x3FFFu) {
-        claim = G.A + ql;  // its frame leaves the listed positions: the successor it declares
-      } else {
-        ok = 0;
-      }
-    } else if (ok) {
-      claim = G.A + (uint32_t)__builtin_amdgcn_readlane((int)pos, (int)exitn);
-    }
-    if (ok) {  // the records: each thread's first chain node, its delivered frames and changes
-      // (chain nodes are in position order: a thread's chain nodes are consecutive chain lanes)
-      const bool on = ((chain >> lane) & 1ull) != 0;
-      const uint32_t th = pos / SEGB;
-      const uint64_t below = chain & ((1ull << lane) - 1ull);
-      const uint32_t prev = below ? 63u - (uint32_t)__builtin_clzll(below) : lane;
-      const uint32_t pth = (uint32_t)__shfl((int)pos, (int)prev, WAVE) / SEGB;
-      const bool first = on && (!below || pth != th);
-      const bool delivered = on && c != NX_TAILC && id != 3u;
-      const uint64_t dm = __ballot(delivered && id != 0u), cm = __ballot(delivered && id == 1u);
-      const uint64_t firsts = __ballot(first);
-      if (first) {
-        const uint64_t later = firsts & ~((2ull << lane) - 1ull);  // (lane 63: none)
-        const uint64_t mine = (later ? ((1ull << __builtin_ctzll(later)) - 1ull) : ~0ull) & ~((1ull << lane) - 1ull);
-        S.sp_eb[th] = (uint8_t)((pos % SEGB) | (lane == g0 ? 0x40u : 0u));
-        S.sp_en[th] = (uint8_t)__builtin_popcountll(dm & mine);
-        S.sp_ec[th] = (uint8_t)__builtin_popcountll(cm & mine);
-      }
-    }
-  }
-  if (lane == 0) {
-    S.sp_ok = ok;
-    S.sp_claim = claim;
-  }
-  (void)se_rel;
-}
-
-// The sparse form of fast_claims' prediction (wave 0 of the workgroup; at most 64 nodes, lane i =
-// node i in position order, parsed into lnd / lal by the caller). Survival is propagated along the
-// successor links with lane shuffles; the prediction is the chain from the first strong tile node,
-// taken only when it is unambiguous: that node does not jump past the tile while another strong
-// node follows, every strong tile node lies on its chain, the chain does not die, and no undecided
-// node (a frame leaving the image that the structural check did not prove) follows the chain's last
-// tile node. Then the records are the chain's: each thread's first chain node (the first carrier
-// flagged as a restart, as the general link rounds flag it), its delivered frames and Change frames,
-// and the claim is the first chain position past the tile (or the chain's end). S.sp_ok = 0 sends
-// the tile to the general phases. No strong node and no undecided one: an identity claim.
-#ifndef DRP_SPARSE_CLAIMS
-#define DRP_SPARSE_CLAIMS 1  // 0: every tile through the general phases (A/B)
-#endif
-struct FastLds;
-__device__ __forceinline__ void sparse_claims(const DecodeParams &P, const TileGeo &G, FastLds &S, uint32_t total,
-                                              uint32_t se_rel);
 // The fast claims of interior tile t: writes the per-thread records (P.ent*) and P.claim[t], and
 // returns this thread's record (eb, en, ecn) and, in thread NT - 1, the claim. FC_DENSE: more than
 // FCAP live positions (the tile went to the general kernel's work list; nothing written).
@@ -1443,28 +1326,6 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   abl_out(P, t, (uint64_t)(ncode[0] + na[1]));
   return FC_ABLATE;
 #endif
-  // Sparse tiles (at most 64 nodes with the halo's: C5's long frames, blob payloads): one wave
-  // decides the prediction with one node per lane and no further barriers, when it is
-  // unambiguous; anything else takes the general phases below (lnd / lal are left as they are).
-  if (DRP_SPARSE_CLAIMS && total <= WAVE) {
-    if (wid == 0) sparse_claims(P, G, S, total, se_rel);
-    bsync();
-    if (S.sp_ok) {
-      const uint64_t ix = t * NT + tid;
-      eb_o = S.sp_eb[tid];
-      en_o = S.sp_en[tid];
-      ecn_o = S.sp_ec[tid];
-      P.ent[ix] = (uint8_t)eb_o;
-      P.ent_n[ix] = (uint8_t)en_o;
-      P.ent_c[ix] = (uint8_t)ecn_o;
-      cl_o = 0;
-      if (tid == NT - 1) {
-        P.claim[t] = S.sp_claim;
-        cl_o = S.sp_claim;
-      }
-      return FC_OK;
-    }
-  }
   lmw[tid] = 0;  // (now the strong masks)
   dmw[tid] = 0;
   // ---- survival: KSTRONG - 1 rounds propagate death / undecided back along the chains ------------
@@ -2608,18 +2469,30 @@ __device__ __forceinline__ void st_col(T *base, uint32_t i, T v) {
   *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (uint32_t)(i * (uint32_t)sizeof(T))) = v;
 }
 
+struct LeanLds {
+  __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+  uint32_t wsum[NT / WAVE];
+  uint32_t defer;
+};
+__device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t, LeanLds &L);
+
 __global__ __launch_bounds__(NT, DRP_EMIT_LEAN_WAVES) void emit_lean(DecodeParams P) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
-  __shared__ uint32_t wsum[NT / WAVE];
-  __shared__ uint32_t defer;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  __shared__ LeanLds L;
   if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
-  const uint64_t ntiles = P.tile_prefix[P.nstreams];
   uint64_t t;
   {  // XCD-contiguous tile order, as the fast emit_tiles
     const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = blockIdx.x % 8u;
     t = (uint64_t)x * q + min(x, r) + blockIdx.x / 8u;
   }
+  emit_lean_tile(P, t, L);
+}
+
+__device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t, LeanLds &L) {
+  uint8_t *buf = L.buf;
+  uint32_t *wsum = L.wsum;
+  uint32_t &defer = L.defer;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  const uint64_t ntiles = P.tile_prefix[P.nstreams];
   const TileGeo G = tile_geo(P, t);
   if (t >= ntiles) return;  // (whole workgroup)
   if (P.tile_sparse && P.tile_sparse[t]) return;  // emit_sparse wrote it
@@ -3175,6 +3048,38 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
                                   Q.scount, st, Q.counter + 3);
 }
 
+// Measurement only (drp_probe_overlap): one launch in which workgroup 16 k + r (r < 8) runs the
+// claims of tile 8 k + r and workgroup 16 k + 8 + r the lean emit of tile 8 (k - lag / 8) + r: on the
+// round-robin XCD placement both of a tile's workgroups share one XCD, the emit `lag` tiles behind
+// the claims, so the emit may read the tile from that XCD's L2 / the Infinity Cache. This is the
+// schedule a single-pass decode would have (timing only: the records and bases are the previous
+// decode's, rewritten with the same values).
+namespace drp {
+namespace spec {
+union DualLds {
+  FastLds c;
+  LeanLds e;
+};
+__global__ __launch_bounds__(NT, DRP_K1_WAVES) void probe_dual(DecodeParams P, uint64_t nt, uint32_t lag) {
+  __shared__ DualLds U;
+  const uint64_t b = blockIdx.x, k = b >> 4, r = b & 15u;
+  if (r < 8) {
+    const uint64_t t = 8 * k + r;
+    if (t >= nt) return;
+    const TileGeo G = tile_geo(P, t);
+    if (G.A < G.so || G.A + IMG > G.se) return;
+    uint32_t eb, en, ecn;
+    uint64_t cl;
+    (void)fast_claims<false>(P, G, t, U.c, eb, en, ecn, cl);
+  } else {
+    const int64_t t = (int64_t)(8 * k + (r - 8)) - (int64_t)lag;
+    if (t < 0) return;
+    emit_lean_tile(P, (uint64_t)t, U.e);
+  }
+}
+}  // namespace spec
+}  // namespace drp
+
 // Measurement hook (scripts/probe_overlap.py): the C2 claims kernel and the lean emit over every
 // tile of the last decode's parameters, alone and side by side on two streams (the claims kernel
 // rewrites the same records the emit reads, with the same values), each timed with events.
@@ -3194,6 +3099,14 @@ extern "C" hipError_t drp_probe_overlap_launch(const DecodeParams *P, uint64_t n
   (void)hipEventRecord(ev[4], b);
   (void)hipStreamWaitEvent(a, ev[4], 0);
   (void)hipEventRecord(ev[5], a);
+  // one launch, both roles, emit lagging by `lag` tiles: the tail past nt covers the last tiles' emit
+  for (int v = 0; v < 3; v++) {
+    const uint32_t lag = v == 0 ? 0u : v == 1 ? 64u : 1024u;
+    const uint64_t groups = (nt_max + lag + 7) / 8;
+    (void)hipEventRecord(ev[6 + v], a);
+    hipLaunchKernelGGL(spec::probe_dual, dim3((uint32_t)(groups * 16)), dim3(spec::NT), 0, a, Q, nt_max, lag);
+  }
+  (void)hipEventRecord(ev[9], a);
   return hipGetLastError();
 }
 

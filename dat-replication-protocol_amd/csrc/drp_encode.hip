@@ -364,18 +364,30 @@ __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
 }
 
 // ---- output-stationary write ------------------------------------------------------------------
-// The output is cut into 16 KiB blocks aligned in memory; a workgroup owns one block and each lane
-// fixed 16-byte chunks of it. The workgroup lays out the frames the block touches in LDS (their
+// The output is cut into ENC_BS-byte blocks aligned in memory; a workgroup owns one block and each
+// lane fixed 16-byte chunks of it. The workgroup lays out the frames the block touches in LDS (their
 // starts, segment ends, heap offsets and prefix bytes), then every lane finds its chunk's frame and
 // segment: a chunk inside one key / subset / value copy (nearly all of a 4 KB value) is two aligned
 // heap loads, a funnel shift and one aligned 16-byte store, with no per-frame latency chain; a
-// chunk that mixes segments is assembled byte by byte. Blocks touching more than ENC_FMAX frames
-// (short frames) are left to the per-frame writer (enc_write_dense).
+// chunk that mixes segments is assembled piece by piece. Blocks touching more than ENC_FMAX frames
+// (short frames) are left to the per-frame writer (enc_write_dense). 32 KiB blocks and a 16 KB
+// LDS layout keep 8 workgroups on a CU, so the descriptor phase's latency (three dependent global
+// rounds) is spread over 32 KiB of copies and hidden behind 7 other workgroups.
 #ifndef DRP_ENC_OS
 #define DRP_ENC_OS 1  // 0: the per-frame writer for every frame (A/B)
 #endif
-constexpr uint32_t ENC_BS = 16384, ENC_CPB = ENC_BS / 16, ENC_OS_T = 256, ENC_FMAX = 192;
+#ifndef DRP_ENC_BS
+#define DRP_ENC_BS 65536  // output block bytes (a multiple of 16 KiB, at most 1 MiB)
+#endif
+constexpr uint32_t ENC_BS = DRP_ENC_BS, ENC_CPB = ENC_BS / 16, ENC_OS_T = 256, ENC_FMAX = 128;
+constexpr uint32_t ENC_U = 4, ENC_NB = ENC_CPB / (ENC_OS_T * ENC_U);  // chunks per lane: ENC_NB batches of ENC_U
+static_assert(ENC_NB >= 1 && ENC_NB * ENC_U <= 32 && ENC_CPB % (ENC_OS_T * ENC_U) == 0, "ENC_BS");
 constexpr uint32_t LIT0 = 0, LIT2 = 24, LIT4 = 32, LITB = 72;  // prefix byte slots per frame
+// Mixed chunks (not inside one copy segment) per block: at most 3 + 2 + 4 per frame (the chunks the
+// prefix runs L0 <= 24 B, L2 <= 8 B, L4 <= 40 B overlap; a chunk across a copy's end overlaps the
+// next prefix run) plus the output's first and last chunk.
+constexpr uint32_t ENC_MIXCAP = 9 * ENC_FMAX + 8;
+static_assert(ENC_CPB <= 65536, "chunk index in 16 bits");
 constexpr uint32_t ENC_F_DENSE_FRAME = 1u << 31;               // (frame bytes that do not fit 31 bits)
 
 // wire offset of output block b's first byte (blocks are aligned in memory; out may not be)
@@ -409,7 +421,76 @@ struct EncLds {
   uint64_t src[3][ENC_FMAX];  // heap offsets of subset, key, value
   __attribute__((aligned(4))) uint8_t lit[ENC_FMAX][LITB];
   uint8_t slack[32];  // (16-byte windows read past the last prefix slot)
+  uint32_t nmix;
+  uint16_t mix[ENC_MIXCAP];  // the block's mixed chunks (chunk index in the block)
 };
+
+// One chunk that mixes segments (or the output's first / last chunk), piece by piece (a piece = the
+// chunk bytes of one segment of one frame), each piece as one 16-byte window shifted into place and
+// masked: two aligned loads for heap bytes, LDS reads for prefix bytes, no byte loops.
+__device__ __forceinline__ void enc_mixed_chunk(const EncodeParams &P, const EncLds &S, uint32_t nf,
+                                                uint64_t W, int64_t c0) {
+  const int64_t p0 = c0 < 0 ? 0 : c0;
+  uint32_t j = 0, hi = nf;
+  while (hi - j > 1) {
+    const uint32_t mid = (j + hi) >> 1;
+    if (S.fst[mid] <= p0) j = mid;
+    else hi = mid;
+  }
+  const int64_t ce = c0 + 16 < (int64_t)W ? c0 + 16 : (int64_t)W;
+  uint64_t acc0 = 0, acc1 = 0;  // the chunk's bytes 0..7, 8..15
+  int64_t w = p0;
+  while (w < ce) {
+    while (w >= S.fst[j + 1]) j++;
+    const int64_t fs = S.fst[j];
+    const uint32_t r = (uint32_t)(w - fs);
+    const uint32_t ends[6] = {S.e[0][j], S.e[1][j], S.e[2][j], S.e[3][j], S.e[4][j],
+                              (uint32_t)(S.fst[j + 1] - fs)};
+    uint32_t sg = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 5; q++) sg += r >= ends[q] ? 1u : 0u;
+    const uint32_t a = sg ? ends[sg - 1] : 0u;
+    const int64_t pe = fs + ends[sg] < ce ? fs + ends[sg] : ce;  // this piece: wire bytes [w, pe)
+    const uint32_t q0 = (uint32_t)(w - c0), q1 = (uint32_t)(pe - c0);
+    uint64_t v0, v1;  // 16 bytes from the piece's first byte on
+    if (sg & 1u) {
+      const uint8_t *sp = P.heap + S.src[sg >> 1][j] + (r - a);
+      const uint32_t sh = (uint32_t)((uintptr_t)sp & 15);
+      const uint4 *ab = reinterpret_cast<const uint4 *>(sp - sh);
+      const uint4 b0 = ab[0];
+      const uint4 b1 = sh + (q1 - q0) > 16u ? ab[1] : b0;  // (only blocks holding piece bytes)
+      const uint4 x = enc_shift(b0, b1, sh);
+      v0 = ((uint64_t)x.y << 32) | x.x;
+      v1 = ((uint64_t)x.w << 32) | x.z;
+    } else {
+      const uint32_t lo = (uint32_t)(&S.lit[j][sg == 0 ? LIT0 : sg == 2 ? LIT2 : LIT4] - &S.lit[0][0]) + (r - a);
+      v0 = enc_lds_u64(&S.lit[0][0], lo);
+      v1 = enc_lds_u64(&S.lit[0][0], lo + 8u);
+    }
+    // shift left by q0 bytes, keep bytes [q0, q1)
+    const uint32_t b = 8u * q0;
+    uint64_t s0, s1;
+    if (b == 0) s0 = v0, s1 = v1;
+    else if (b < 64) s0 = v0 << b, s1 = (v1 << b) | (v0 >> (64u - b));
+    else s0 = 0, s1 = v0 << (b - 64u);
+    const uint32_t e = 8u * q1;
+    const uint64_t m0 = (e >= 64 ? ~0ull : (1ull << e) - 1ull) & (b >= 64 ? 0ull : ~0ull << b);
+    const uint64_t m1 = (e <= 64 ? 0ull : (e >= 128 ? ~0ull : (1ull << (e - 64u)) - 1ull)) &
+                        (b <= 64 ? ~0ull : ~0ull << (b - 64u));
+    acc0 |= s0 & m0;
+    acc1 |= s1 & m1;
+    w = pe;
+  }
+  if (c0 >= 0 && c0 + 16 <= (int64_t)W) {
+    *reinterpret_cast<uint4 *>(P.out + c0) =
+        make_uint4((uint32_t)acc0, (uint32_t)(acc0 >> 32), (uint32_t)acc1, (uint32_t)(acc1 >> 32));
+  } else {  // the output's first or last chunk: only its own bytes
+    for (int64_t x = p0; x < ce; x++) {
+      const uint32_t q = (uint32_t)(x - c0);
+      P.out[x] = (uint8_t)((q < 8 ? acc0 >> (8 * q) : acc1 >> (8 * (q - 8))) & 0xFF);
+    }
+  }
+}
 
 __global__ __launch_bounds__(ENC_OS_T) void enc_write_os(EncodeParams P) {
   __shared__ EncLds S;
@@ -421,11 +502,9 @@ __global__ __launch_bounds__(ENC_OS_T) void enc_write_os(EncodeParams P) {
   if (bs >= (int64_t)W) return;  // (whole workgroup)
   const int64_t be = bs + (int64_t)ENC_BS;
   const uint64_t f0 = P.oblk_first[b];
-  uint64_t f1 = P.n;  // frames [f0, f1) touch the block
-  if (be < (int64_t)W) {
-    const uint64_t nb = P.oblk_first[b + 1];
-    f1 = P.frame_off[nb] < (uint64_t)be ? nb + 1 : nb;
-  }
+  // frames [f0, f1) touch the block (the frame holding the next block's first byte may start at be
+  // exactly: laid out, never looked up)
+  const uint64_t f1 = be < (int64_t)W ? min(P.oblk_first[b + 1] + 1, P.n) : P.n;
   const uint32_t t = threadIdx.x;
   if (f1 - f0 > ENC_FMAX) {
     if (t == 0) P.dense[atomicAdd(P.dense_n, 1u)] = (uint32_t)b;
@@ -465,6 +544,7 @@ __global__ __launch_bounds__(ENC_OS_T) void enc_write_os(EncodeParams P) {
     const uint64_t e0 = x, e1 = e0 + sl, e2 = e1 + y, e3 = e2 + kl, e4 = e3 + z, e5 = e4 + vl;
     big = e5 >= ENC_F_DENSE_FRAME;
     S.fst[t] = (int64_t)fs;
+    if (t == nf - 1) S.fst[nf] = (int64_t)(fs + e5);
     S.e[0][t] = (uint32_t)e0;
     S.e[1][t] = (uint32_t)e1;
     S.e[2][t] = (uint32_t)e2;
@@ -474,129 +554,81 @@ __global__ __launch_bounds__(ENC_OS_T) void enc_write_os(EncodeParams P) {
     S.src[1][t] = s.key_off[i];
     S.src[2][t] = val ? s.value_off[i] : 0ull;
   }
-  if (t == 0) S.fst[nf] = (int64_t)P.frame_off[f1];
+  if (t == 0) S.nmix = 0;
   if (__syncthreads_or(big)) {  // (a frame of 2^31 bytes or more: the per-frame writer)
     if (t == 0) P.dense[atomicAdd(P.dense_n, 1u)] = (uint32_t)b;
     return;
   }
-  // ENC_CPB / ENC_OS_T chunks per lane, strided by the workgroup (each pass of the workgroup stores
-  // 4 KiB contiguous). Every chunk's frame and segment are looked up first, then every heap load
-  // of the lane's whole-copy chunks is issued, then the stores: a lane keeps 8 loads in flight.
-  constexpr uint32_t U = ENC_CPB / ENC_OS_T;
-  const uint4 *sa[U];
-  uint32_t shv[U];
-  bool fast[U];
-#pragma unroll
-  for (uint32_t u = 0; u < U; u++) {
-    const int64_t c0 = bs + 16 * (int64_t)(t + u * ENC_OS_T);
-    fast[u] = false;
-    sa[u] = nullptr;
-    shv[u] = 0;
-    if (c0 >= 0 && c0 + 16 <= (int64_t)W) {
-      uint32_t lo = 0, hi = nf;  // fst[lo] <= c0 < fst[hi]
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (S.fst[mid] <= c0) lo = mid;
-        else hi = mid;
-      }
-      const uint32_t r = (uint32_t)(c0 - S.fst[lo]);
-      const uint32_t fe = (uint32_t)(S.fst[lo + 1] - S.fst[lo]);
-      const uint32_t e0 = S.e[0][lo], e1 = S.e[1][lo], e2 = S.e[2][lo], e3 = S.e[3][lo], e4 = S.e[4][lo];
-      // a copy segment holding the whole chunk: subset [e0, e1), key [e2, e3), value [e4, end)
-      uint32_t a = 0xFFFFFFFFu, seg = 0;
-      if (r >= e4 && r + 16 <= fe) a = e4, seg = 2;
-      else if (r >= e2 && r + 16 <= e3) a = e2, seg = 1;
-      else if (r >= e0 && r + 16 <= e1) a = e0, seg = 0;
-      if (a != 0xFFFFFFFFu) {
-        const uint8_t *sp = P.heap + S.src[seg][lo] + (r - a);
-        shv[u] = (uint32_t)((uintptr_t)sp & 15);
-        sa[u] = reinterpret_cast<const uint4 *>(sp - shv[u]);
-        fast[u] = true;
-      }
-    }
-  }
-  uint4 v0[U], v1[U];
-#pragma unroll
-  for (uint32_t u = 0; u < U; u++) {
-    v0[u] = v1[u] = make_uint4(0, 0, 0, 0);
-    if (fast[u]) {
-      v0[u] = sa[u][0];
-      if (shv[u]) v1[u] = sa[u][1];
-    }
-  }
-#pragma unroll
-  for (uint32_t u = 0; u < U; u++)
-    if (fast[u])
-      *reinterpret_cast<uint4 *>(P.out + bs + 16 * (int64_t)(t + u * ENC_OS_T)) =
-          shv[u] ? enc_shift(v0[u], v1[u], shv[u]) : v0[u];
-  // chunks that mix segments (and the output's first / last chunk): piece by piece (a piece = the
-  // chunk bytes of one segment of one frame), each piece as one 16-byte window shifted into place
-  // and masked: two aligned loads for heap bytes, LDS reads for prefix bytes, no byte loops
+  // ENC_NB batches of ENC_U chunks per lane, strided by the workgroup (each pass of the workgroup
+  // stores 4 KiB contiguous). In a batch every chunk's frame and segment are looked up first, then
+  // every heap load of the lane's whole-copy chunks is issued, then the stores: a lane keeps up to
+  // 2 * ENC_U loads in flight. fm: the lane's chunks written here (the rest: the piece loop below).
+  uint32_t fm = 0;
 #pragma unroll 1
-  for (uint32_t u = 0; u < U; u++) {
-    const int64_t c0 = bs + 16 * (int64_t)(t + u * ENC_OS_T);
-    if (fast[u] || c0 >= (int64_t)W) continue;
-    const int64_t p0 = c0 < 0 ? 0 : c0;
-    uint32_t j = 0, hi = nf;
-    while (hi - j > 1) {
-      const uint32_t mid = (j + hi) >> 1;
-      if (S.fst[mid] <= p0) j = mid;
-      else hi = mid;
-    }
-    const int64_t ce = c0 + 16 < (int64_t)W ? c0 + 16 : (int64_t)W;
-    uint64_t acc0 = 0, acc1 = 0;  // the chunk's bytes 0..7, 8..15
-    int64_t w = p0;
-    while (w < ce) {
-      while (w >= S.fst[j + 1]) j++;
-      const int64_t fs = S.fst[j];
-      const uint32_t r = (uint32_t)(w - fs);
-      const uint32_t ends[6] = {S.e[0][j], S.e[1][j], S.e[2][j], S.e[3][j], S.e[4][j],
-                                (uint32_t)(S.fst[j + 1] - fs)};
-      uint32_t sg = 0;
+  for (uint32_t k = 0; k < ENC_NB; k++) {
+    const uint4 *sa[ENC_U];
+    uint32_t shv[ENC_U];
+    bool fast[ENC_U];
 #pragma unroll
-      for (uint32_t q = 0; q < 5; q++) sg += r >= ends[q] ? 1u : 0u;
-      const uint32_t a = sg ? ends[sg - 1] : 0u;
-      const int64_t pe = fs + ends[sg] < ce ? fs + ends[sg] : ce;  // this piece: wire bytes [w, pe)
-      const uint32_t q0 = (uint32_t)(w - c0), q1 = (uint32_t)(pe - c0);
-      uint64_t v0, v1;  // 16 bytes from the piece's first byte on
-      if (sg & 1u) {
-        const uint8_t *sp = P.heap + S.src[sg >> 1][j] + (r - a);
-        const uint32_t sh = (uint32_t)((uintptr_t)sp & 15);
-        const uint4 *ab = reinterpret_cast<const uint4 *>(sp - sh);
-        const uint4 b0 = ab[0];
-        const uint4 b1 = sh + (q1 - q0) > 16u ? ab[1] : b0;  // (only blocks holding piece bytes)
-        const uint4 x = enc_shift(b0, b1, sh);
-        v0 = ((uint64_t)x.y << 32) | x.x;
-        v1 = ((uint64_t)x.w << 32) | x.z;
-      } else {
-        const uint32_t lo = (uint32_t)(&S.lit[j][sg == 0 ? LIT0 : sg == 2 ? LIT2 : LIT4] - &S.lit[0][0]) + (r - a);
-        v0 = enc_lds_u64(&S.lit[0][0], lo);
-        v1 = enc_lds_u64(&S.lit[0][0], lo + 8u);
-      }
-      // shift left by q0 bytes, keep bytes [q0, q1)
-      const uint32_t b = 8u * q0;
-      uint64_t s0, s1;
-      if (b == 0) s0 = v0, s1 = v1;
-      else if (b < 64) s0 = v0 << b, s1 = (v1 << b) | (v0 >> (64u - b));
-      else s0 = 0, s1 = v0 << (b - 64u);
-      const uint32_t e = 8u * q1;
-      const uint64_t m0 = (e >= 64 ? ~0ull : (1ull << e) - 1ull) & (b >= 64 ? 0ull : ~0ull << b);
-      const uint64_t m1 = (e <= 64 ? 0ull : (e >= 128 ? ~0ull : (1ull << (e - 64u)) - 1ull)) &
-                          (b <= 64 ? ~0ull : ~0ull << (b - 64u));
-      acc0 |= s0 & m0;
-      acc1 |= s1 & m1;
-      w = pe;
-    }
-    if (c0 >= 0 && c0 + 16 <= (int64_t)W) {
-      *reinterpret_cast<uint4 *>(P.out + c0) =
-          make_uint4((uint32_t)acc0, (uint32_t)(acc0 >> 32), (uint32_t)acc1, (uint32_t)(acc1 >> 32));
-    } else {  // the output's first or last chunk: only its own bytes
-      for (int64_t x = p0; x < ce; x++) {
-        const uint32_t q = (uint32_t)(x - c0);
-        P.out[x] = (uint8_t)((q < 8 ? acc0 >> (8 * q) : acc1 >> (8 * (q - 8))) & 0xFF);
+    for (uint32_t u = 0; u < ENC_U; u++) {
+      const int64_t c0 = bs + 16 * (int64_t)(t + (k * ENC_U + u) * ENC_OS_T);
+      fast[u] = false;
+      sa[u] = nullptr;
+      shv[u] = 0;
+      if (c0 >= 0 && c0 + 16 <= (int64_t)W) {
+        uint32_t lo = 0, hi = nf;  // fst[lo] <= c0 < fst[hi]
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (S.fst[mid] <= c0) lo = mid;
+          else hi = mid;
+        }
+        const uint32_t r = (uint32_t)(c0 - S.fst[lo]);
+        const uint32_t fe = (uint32_t)(S.fst[lo + 1] - S.fst[lo]);
+        const uint32_t e0 = S.e[0][lo], e1 = S.e[1][lo], e2 = S.e[2][lo], e3 = S.e[3][lo], e4 = S.e[4][lo];
+        // a copy segment holding the whole chunk: subset [e0, e1), key [e2, e3), value [e4, end)
+        uint32_t a = 0xFFFFFFFFu, seg = 0;
+        if (r >= e4 && r + 16 <= fe) a = e4, seg = 2;
+        else if (r >= e2 && r + 16 <= e3) a = e2, seg = 1;
+        else if (r >= e0 && r + 16 <= e1) a = e0, seg = 0;
+        if (a != 0xFFFFFFFFu) {
+          const uint8_t *sp = P.heap + S.src[seg][lo] + (r - a);
+          shv[u] = (uint32_t)((uintptr_t)sp & 15);
+          sa[u] = reinterpret_cast<const uint4 *>(sp - shv[u]);
+          fast[u] = true;
+        }
       }
     }
+    uint4 v0[ENC_U], v1[ENC_U];
+#pragma unroll
+    for (uint32_t u = 0; u < ENC_U; u++) {
+      v0[u] = v1[u] = make_uint4(0, 0, 0, 0);
+      if (fast[u]) {
+        v0[u] = sa[u][0];
+        if (shv[u]) v1[u] = sa[u][1];
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < ENC_U; u++)
+      if (fast[u]) {
+        *reinterpret_cast<uint4 *>(P.out + bs + 16 * (int64_t)(t + (k * ENC_U + u) * ENC_OS_T)) =
+            shv[u] ? enc_shift(v0[u], v1[u], shv[u]) : v0[u];
+        fm |= 1u << (k * ENC_U + u);
+      }
   }
+  // the mixed chunks, listed in LDS and spread one per lane (a lane's own mixed chunks would run
+  // one after another, each a chain of dependent piece loads)
+#pragma unroll 1
+  for (uint32_t u = 0; u < ENC_NB * ENC_U; u++) {
+    const int64_t c0 = bs + 16 * (int64_t)(t + u * ENC_OS_T);
+    if (((fm >> u) & 1u) || c0 >= (int64_t)W) continue;
+    const uint32_t slot = atomicAdd(&S.nmix, 1u);
+    if (slot < ENC_MIXCAP) S.mix[slot] = (uint16_t)(t + u * ENC_OS_T);
+    else enc_mixed_chunk(P, S, nf, W, c0);  // (not reached: ENC_MIXCAP bounds the count)
+  }
+  __syncthreads();
+  const uint32_t nm = min(S.nmix, ENC_MIXCAP);
+#pragma unroll 1
+  for (uint32_t x = t; x < nm; x += ENC_OS_T) enc_mixed_chunk(P, S, nf, W, bs + 16 * (int64_t)S.mix[x]);
 }
 
 // The frames of the blocks enc_write_os left (more than ENC_FMAX frames, or a frame of 2^31 bytes

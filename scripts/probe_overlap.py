@@ -27,8 +27,9 @@ bench.verify_c2(outs, res, n, dev)
 L = drp_amd.lib()
 L.drp_probe_overlap.argtypes = [C.c_void_p, C.POINTER(C.c_float)]
 for rep in range(4):
-    ms = (C.c_float * 3)()
+    ms = (C.c_float * 6)()
     assert L.drp_probe_overlap(ctx.h, ms) == 0
     print(f"claims alone {ms[0]:.3f} ms, emit alone {ms[1]:.3f} ms, sum {ms[0] + ms[1]:.3f} ms, "
-          f"side by side {ms[2]:.3f} ms", flush=True)
+          f"side by side {ms[2]:.3f} ms, one launch (emit lag 0 / 64 / 1024 tiles) "
+          f"{ms[3]:.3f} / {ms[4]:.3f} / {ms[5]:.3f} ms", flush=True)
 ctx.close()

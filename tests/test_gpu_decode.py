@@ -325,32 +325,35 @@ def test_encode_max_width_varints(ctx):
     assert ctx.encode_batch(heap, c) == O.encode_changes(heap, c)
 
 
-@pytest.mark.parametrize("shape", ["tiny", "c1", "c5", "mixed"])
+@pytest.mark.parametrize("shape", ["tiny", "c1", "c5", "mixed", "edge"])
 def test_encode_write_paths_match_oracle(ctx, shape):
-    """The encode write covers the output with 16 KiB blocks (drp_encode.hip): a block touching
+    """The encode write covers the output with 64 KiB blocks (drp_encode.hip): a block touching
     at most ENC_FMAX frames is written chunk by chunk (16-byte copies out of the heap, chunks that
-    mix segments byte by byte), a denser one frame by frame. Frames of ~10 bytes (dense blocks),
-    C1-sized ones (mostly mixed chunks), 4 KB values (whole copies), and all of them interleaved
-    with subsets and 10-byte varints, written at every alignment of the output pointer: the wire
+    mix segments piece by piece, listed in LDS), a denser one frame by frame. Frames of ~10 bytes
+    (dense blocks), C1-sized ones (dense at 64 KiB), 4 KB values (whole copies), ~500-byte frames
+    with short keys, subsets and long varints (the most mixed chunks a block can hold, around
+    ENC_FMAX frames a block), and all of them interleaved, written at every alignment of the
+    output pointer: the wire
     equals the oracle's encode.js + protocol-buffers@2 restatement byte for byte, and the bytes
     around it are untouched."""
     import torch
-    rng = np.random.default_rng({"tiny": 1, "c1": 2, "c5": 3, "mixed": 4}[shape])
-    n = {"tiny": 40_000, "c1": 20_000, "c5": 2_000, "mixed": 30_000}[shape]
+    rng = np.random.default_rng({"tiny": 1, "c1": 2, "c5": 3, "mixed": 4, "edge": 5}[shape])
+    n = {"tiny": 40_000, "c1": 20_000, "c5": 2_000, "mixed": 30_000, "edge": 20_000}[shape]
     kind = {"tiny": np.zeros(n, int), "c1": np.ones(n, int), "c5": np.full(n, 2),
-            "mixed": rng.integers(0, 3, n)}[shape]
+            "mixed": rng.integers(0, 3, n), "edge": np.full(n, 3)}[shape]
     if shape == "mixed":  # runs of each kind, so dense and sparse blocks alternate
         kind = np.repeat(rng.integers(0, 3, n // 500 + 1), 500)[:n]
-    kl = np.where(kind == 0, rng.integers(0, 3, n), np.where(kind == 1, 32, rng.integers(1, 257, n))).astype(np.uint32)
-    vl = np.where(kind == 0, 0, np.where(kind == 1, 64, 4096)).astype(np.uint32)
-    sub = (rng.random(n) < (0.3 if shape == "mixed" else 0.0))
-    sl = np.where(sub, rng.integers(0, 200, n), 0).astype(np.uint32)
+    kl = np.select([kind == 0, kind == 1, kind == 2], [rng.integers(0, 3, n), 32, rng.integers(1, 257, n)],
+                   rng.integers(0, 40, n)).astype(np.uint32)
+    vl = np.select([kind == 0, kind == 1, kind == 2], [0, 64, 4096], rng.integers(380, 460, n)).astype(np.uint32)
+    sub = (rng.random(n) < {"mixed": 0.3, "edge": 0.5}.get(shape, 0.0))
+    sl = np.where(sub, rng.integers(0, 200 if shape == "mixed" else 40, n), 0).astype(np.uint32)
     flags = (sub.astype(np.uint8) | np.where((kind > 0) | (rng.random(n) < 0.5), 2, 0).astype(np.uint8))
     row = kl.astype(np.uint64) + sl + vl
     base = np.cumsum(row) - row
     heap = rng.integers(0, 256, int(row.sum()) + 16, dtype=np.uint8)
     nums = rng.integers(0, 1 << 40, (3, n), dtype=np.uint64)
-    if shape == "mixed":
+    if shape in ("mixed", "edge"):
         nums[:, ::7] = np.uint64(2**64 - 1)
     cols = {"key_off": base, "key_len": kl, "subset_off": base + kl, "subset_len": sl,
             "value_off": base + kl + sl, "value_len": vl, "change": nums[0], "from": nums[1], "to": nums[2],
@@ -362,7 +365,7 @@ def test_encode_write_paths_match_oracle(ctx, shape):
     ht = torch.from_numpy(heap).to(dev)
     foff = torch.empty(n + 1, dtype=torch.int64, device=dev)
     W = len(exp)
-    for shift in ([0, 1, 7, 15] if shape != "mixed" else range(16)):
+    for shift in ([0, 1, 7, 15] if shape not in ("mixed", "edge") else range(16)):
         buf = torch.full((W + 64,), 0xA5, dtype=torch.uint8, device=dev)
         ctx.encode_device(ct, ht, n, foff, buf[16 + shift:], W + 32)
         torch.cuda.synchronize(dev)
