@@ -610,6 +610,9 @@ def main():
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse "
                     "several ranks on one GPU")
     args = ap.parse_args()
+    if os.environ.get("DRP_BENCH_WATCHDOG"):  # (hang finding: every thread's Python stack, then exit)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["DRP_BENCH_WATCHDOG"]), exit=True)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # one process per GPU: re-launch under torch.distributed.run before anything touches

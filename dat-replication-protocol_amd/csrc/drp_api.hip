@@ -10,6 +10,9 @@
 #include <cstring>
 #include <ctime>
 #include <algorithm>
+#include <chrono>
+#include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/drp.h"
@@ -33,6 +36,49 @@ bool trace_on() {
       fflush(stderr);                             \
     }                                             \
   } while (0)
+
+// Hang finding (DRP_WATCHDOG=<seconds>, off by default): the speculative decode's launches record
+// named events (drp_dbg_mark), and a host wait that runs past the limit prints which of them have
+// completed, then ends the process (a measurement aid: the default path records nothing).
+struct DbgMarks {
+  int on = -1;
+  double limit_s = 0;
+  hipEvent_t ev[64] = {};
+  const char *name[64] = {};
+  int n = 0;
+};
+DbgMarks g_dbg;
+bool dbg_on() {
+  if (g_dbg.on < 0) {
+    const char *w = getenv("DRP_WATCHDOG");
+    g_dbg.limit_s = w ? atof(w) : 0;
+    g_dbg.on = g_dbg.limit_s > 0 ? 1 : 0;
+    if (g_dbg.on)
+      for (auto &e : g_dbg.ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  }
+  return g_dbg.on == 1;
+}
+// a stream synchronisation that, under DRP_WATCHDOG, gives up after the limit and names the
+// first marked launch that has not completed
+hipError_t sync_watch(hipStream_t st, const char *where) {
+  if (!dbg_on()) return hipStreamSynchronize(st);
+  const auto t0 = std::chrono::steady_clock::now();
+  hipError_t e;
+  while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (s > g_dbg.limit_s) {
+      fprintf(stderr, "[drp] watchdog: %s still running after %.1f s; marks:", where, s);
+      for (int k = g_dbg.n > 64 ? g_dbg.n - 64 : 0; k < g_dbg.n; k++)  // (a ring of the last 64)
+        fprintf(stderr, " %s=%s", g_dbg.name[k % 64], hipEventQuery(g_dbg.ev[k % 64]) == hipSuccess ? "done" : "PENDING");
+      fputc('\n', stderr);
+      fflush(stderr);
+      _exit(3);
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+  g_dbg.n = 0;
+  return e;
+}
 
 struct DevBuf {
   void *p = nullptr;
@@ -597,7 +643,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
                             c->key_post == DRP_KEY_POST_FLAGS, abort_flag, drp_spec_retry_mask(), st));
     CHK(hipEventRecord(c->ev[3], st));
     CHK(hipMemcpyAsync(h, ctrl, 64, hipMemcpyDeviceToHost, st));
-    CHK(hipStreamSynchronize(st));
+    CHK(sync_watch(st, "decode (claims .. key_post)"));
     return DRP_OK;
   };
   if (const int rt = launch_tail()) return rt;
@@ -657,7 +703,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
         k = kn;
       }
       CHK(hipMemcpyAsync(h, ctrl, 64, hipMemcpyDeviceToHost, st));
-      CHK(hipStreamSynchronize(st));
+      CHK(sync_watch(st, "repair passes"));
       TRACE("decode_spec: passes %d-%d over %s, %u listed next", pass + 1, pass + chain,
             full ? "every tile" : "dirty lists", h[8 + k]);
       pass += chain - 1;
@@ -1368,3 +1414,9 @@ int drp_stream_stats_from_results(drp_ctx *c, const drp_stream_result *results, 
 }
 
 }  // extern "C"
+
+extern "C" void drp_dbg_mark(const char *name, hipStream_t st) {
+  if (!dbg_on()) return;
+  g_dbg.name[g_dbg.n % 64] = name;
+  (void)hipEventRecord(g_dbg.ev[g_dbg.n++ % 64], st);
+}

@@ -337,11 +337,63 @@ void link(const Img &m, uint64_t s1, uint64_t g, uint64_t e_first, uint64_t &E,
   }
 }
 
-// block-wide reductions over the NT threads (two barriers; scratch: NT / WAVE words)
+// Wave scans and reductions on DPP (row shifts, then row broadcasts): __shfl_xor reductions cost
+// ~5 VALU and a ds_bpermute per step. The compiler leaves update_dpp + op uncombined in the claims
+// kernels (three VALU per step); DRP_DPP_ASM=1 writes one DPP op per step in inline asm. Every use
+// runs with all 64 lanes active (block-level code). s_nop 4 first: the five wait states between an SALU write of EXEC
+// (the end of the branch before) and a DPP op; s_nop 1: the two between a VALU write and a DPP read.
+#define DRP_DPP_STEPS(op)                                                                    \
+  "s_nop 4\n\t" op " %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
+  "s_nop 1\n\t" op " %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
+  "s_nop 1\n\t" op " %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
+  "s_nop 1\n\t" op " %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
+  "s_nop 1\n\t" op " %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"              \
+  "s_nop 1\n\t" op " %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+#ifndef DRP_DPP_ASM
+#define DRP_DPP_ASM 0  // 1: the inline-asm forms (one VALU per step; A/B)
+#endif
+// inclusive prefix sum over the wave
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+#if DRP_DPP_ASM
+  asm volatile(DRP_DPP_STEPS("v_add_u32_dpp") : "+v"(v));
+#else
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+#endif
+  return v;
+}
+// wave-uniform sum / maximum (lane 63 of the inclusive scan)
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(v), 63);
+}
+__device__ __forceinline__ uint32_t wave_max_dpp(uint32_t v) {
+#if DRP_DPP_ASM
+  asm volatile(DRP_DPP_STEPS("v_max_u32_dpp") : "+v"(v));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+#else
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+#endif
+}
+
+// block-wide reductions over the NT threads (two barriers; scratch: NT / WAVE words). The scratch
+// must not be one whose last reads were not followed by a barrier (link()'s fl: the first wave
+// to finish would overwrite it under the other's last read, which then runs another link round
+// against the wrong barrier; the shuffle reductions of earlier rounds only hid this by taking
+// longer than that read).
 __device__ __forceinline__ uint32_t block_max_u32(uint32_t v, uint32_t *xf) {
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (uint32_t k = 1; k < WAVE; k <<= 1) v = max(v, shfl_xor32(v, k));
+  v = wave_max_dpp(v);
+  if constexpr (NT == WAVE) return v;
   if (lane == 0) xf[wid] = v;
   bsync();
   uint32_t r = 0;
@@ -353,11 +405,9 @@ __device__ __forceinline__ uint32_t block_max_u32(uint32_t v, uint32_t *xf) {
 // two maxima with one exchange (scratch: 2 * NT / WAVE words)
 __device__ __forceinline__ void block_max2_u32(uint32_t &a, uint32_t &b, uint32_t *xf) {
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (uint32_t k = 1; k < WAVE; k <<= 1) {
-    a = max(a, shfl_xor32(a, k));
-    b = max(b, shfl_xor32(b, k));
-  }
+  a = wave_max_dpp(a);
+  b = wave_max_dpp(b);
+  if constexpr (NT == WAVE) return;
   if (lane == 0) {
     xf[wid] = a;
     xf[NT / WAVE + wid] = b;
@@ -384,7 +434,8 @@ __device__ __forceinline__ bool any_from(uint64_t m0, uint64_t m1, uint32_t j) {
 
 __device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t *xf) {
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  v = wave_sum32(v);
+  v = wave_sum_dpp(v);
+  if constexpr (NT == WAVE) return v;
   if (lane == 0) xf[wid] = v;
   bsync();
   uint32_t r = 0;
@@ -797,7 +848,7 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
     if (!moved) {
       after = any_from(S0, S1, js);  // survivors at or after the last carrier + 1
     } else {  // candidates changed in HBM: count them again
-      after = block_max_u32(g != NONE && tid + 1 > js ? 1u : 0u, xf) != 0;
+      after = block_max_u32(g != NONE && tid + 1 > js ? 1u : 0u, xf2) != 0;
     }
     if (js && after) {
       const uint64_t Ea = E, Ra = R;
@@ -808,7 +859,8 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
       R = NONE;
       n = 0;
       link<false>(m, s1, mine ? g : NONE, NONE, E, R, n, xr, xf, P.overflow, &rs);
-      const uint32_t nb = block_sum_u32(mine ? (n & 0xFFFFu) : 0u, xf);
+      // (xf2: link's last reads of xf are not behind a barrier)
+      const uint32_t nb = block_sum_u32(mine ? (n & 0xFFFFu) : 0u, xf2);
       if (nb < 2 || !mine) {  // keep the first chain where the dense one does not apply
         E = Ea;
         R = Ra;
@@ -873,16 +925,6 @@ __device__ __forceinline__ uint32_t masks16(const uint4 v) {  // m | s << 16
   return m | (s << 16);
 }
 
-// inclusive prefix sum over the wave (DPP: row shifts, then row broadcasts)
-__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
-  return v;
-}
 
 // A Change frame that leaves the listed positions (long frames: C5's 4 KB values) cannot have its
 // chain followed in the image. It is strong when its payload parses as a Change in the schema's
@@ -1302,7 +1344,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   // the parse's loads of later nodes from being issued together (C2: claims 2.8 -> 5.2 ms). Only
   // a wave whose bytes chain few frames inside the image runs it (C5: two real frames per tile,
   // their chains leave the image; C2: ~47 per wave, predicted without it).
-  if (CF && wave_sum32(chained) < 16u) {
+  if (CF && wave_sum_dpp(chained) < 16u) {
 #pragma unroll
     for (uint32_t j = 0; j < KPT; j++) {
       // (field headers may lie past the image, up to 512 bytes: a halo frame's key runs past it;
@@ -1611,7 +1653,7 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
 __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint64_t xr[NT / WAVE];
-  __shared__ uint32_t xf[NT / WAVE];
+  __shared__ uint32_t xf[NT / WAVE], xs[NT / WAVE];
   __shared__ uint64_t sh_e;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wid = tid >> 6;
@@ -1737,8 +1779,8 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     P.ent[ix] = carrier ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // exact, for kernel 3
     P.ent_n[ix] = carrier ? (uint8_t)(n & 0xFFFFu) : (uint8_t)0;
     P.ent_c[ix] = carrier ? (uint8_t)(n >> 16) : (uint8_t)0;  // (a repair pass may take the fast check)
-    count_t = block_sum_u32(n & 0xFFFFu, xf);
-    nch_t = block_sum_u32(n >> 16, xf);
+    count_t = block_sum_u32(n & 0xFFFFu, xs);  // (xs: link's last reads of xf are not behind a barrier)
+    nch_t = block_sum_u32(n >> 16, xs);
     // the last thread's R is the tile's exact exit; it must be what the claim predicted (an
     // error on the exact chain never is: predictions restart after errors)
     xr[0] = 0;
@@ -2951,6 +2993,8 @@ extern "C" uint32_t drp_spec_retry_mask(void) { return spec::F_MISS | spec::F_WA
 extern "C" uint32_t drp_spec_miss_bit(void) { return spec::F_MISS; }
 
 // Claims and verification only (the host checks the prediction before anything is emitted).
+extern "C" void drp_dbg_mark(const char *name, hipStream_t st);  // (drp_api.hip: DRP_WATCHDOG)
+
 extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                            uint32_t *tile_stream, hipStream_t st) {
   if (nt_max == 0) return hipSuccess;
@@ -2960,6 +3004,7 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
     const uint32_t blk = 256;
     hipLaunchKernelGGL(spec::tile_stream_kernel, dim3((uint32_t)((nt_max + blk - 1) / blk)), dim3(blk), 0, st,
                        P->tile_prefix, nstreams, nt_max, tile_stream);
+    drp_dbg_mark("tile_stream_kernel", st);
     Q.tile_stream = tile_stream;
   }
 #if DRP_CLAIMS_FAST
@@ -2968,19 +3013,25 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
     hipLaunchKernelGGL(spec::claims_fast<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
   else
     hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  drp_dbg_mark("claims_fast", st);
   const uint32_t gw = (uint32_t)(nt_max < 16384 ? nt_max : 16384);
   hipLaunchKernelGGL(spec::spec_claims, dim3(gw), dim3(spec::NT), 0, st, Q);
+  drp_dbg_mark("spec_claims", st);
 #else
   Q.work = nullptr;
   hipLaunchKernelGGL(spec::spec_claims, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  drp_dbg_mark("spec_claims", st);
 #endif
   if (Q.vlist) {  // records-only verification, then verify_counts on the tiles it lists
     const uint64_t nb = (nt_max * spec::VL_G + spec::VL_BLK - 1) / spec::VL_BLK;
     hipLaunchKernelGGL(spec::verify_lite, dim3((uint32_t)nb), dim3(spec::VL_BLK), 0, st, Q);
+    drp_dbg_mark("verify_lite", st);
     hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0, st,
                        Q);
+    drp_dbg_mark("verify_counts", st);
   } else {
     hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+    drp_dbg_mark("verify_counts", st);
   }
   return hipGetLastError();
 }
@@ -2994,10 +3045,13 @@ extern "C" hipError_t drp_launch_spec_verify(const DecodeParams *P, uint64_t nt_
   if (Q.vlist) {  // records-only verification, verify_counts on the tiles it lists (caller zeroes vlist_n)
     const uint64_t nb = (nt_max * spec::VL_G + spec::VL_BLK - 1) / spec::VL_BLK;
     hipLaunchKernelGGL(spec::verify_lite, dim3((uint32_t)nb), dim3(spec::VL_BLK), 0, st, Q);
+    drp_dbg_mark("verify_lite", st);
     hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0, st,
                        Q);
+    drp_dbg_mark("verify_counts", st);
   } else {
     hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+    drp_dbg_mark("verify_counts", st);
   }
   return hipGetLastError();
 }
@@ -3011,6 +3065,7 @@ extern "C" hipError_t drp_launch_spec_verify_list(const DecodeParams *P, uint64_
   Q.tile_stream = nstreams > 1 ? tile_stream : nullptr;
   const uint64_t g = n == ~0ull ? 1024 : (n < 16384 ? n : 16384);
   hipLaunchKernelGGL(spec::verify_counts, dim3((uint32_t)g), dim3(spec::NT), 0, st, Q);
+  drp_dbg_mark("verify_counts", st);
   return hipGetLastError();
 }
 
@@ -3023,12 +3078,14 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
   hipError_t e = drp_launch_tile_scan(Q.tile_count, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_base, Q.cap,
                                       Q.overflow, st);
   if (e != hipSuccess) return e;
+  drp_dbg_mark("tile_scan(count)", st);
   if (DRP_EMIT_SPLIT && Q.vlist) {  // the fast kernel, then the general one on the tiles it lists
     e = hipMemsetAsync(Q.vlist_n, 0, 4, st);
     if (e != hipSuccess) return e;
     if (spec::SP_FRAMES && Q.tile_sparse) {  // sparse tiles first (no staging), then every other tile
       hipLaunchKernelGGL(spec::emit_sparse, dim3((uint32_t)((nt_max + spec::SP_TPB - 1) / spec::SP_TPB)), dim3(256),
                          0, st, Q);
+      drp_dbg_mark("emit_sparse", st);
     } else {
       Q.tile_sparse = nullptr;
     }
@@ -3036,14 +3093,18 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
       hipLaunchKernelGGL(spec::emit_lean, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
     else
       hipLaunchKernelGGL(spec::emit_tiles<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+    drp_dbg_mark("emit_fast", st);
     hipLaunchKernelGGL(spec::emit_tiles<false>, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0,
                        st, Q);
+    drp_dbg_mark("emit_tiles<false>", st);
   } else {
     Q.vlist = nullptr;  // every tile in the general form
     hipLaunchKernelGGL(spec::emit_tiles<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+    drp_dbg_mark("emit_tiles<false>", st);
   }
   e = drp_launch_tile_scan(Q.tile_nch, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_nch_base, ~0ull, Q.overflow, st);
   if (e != hipSuccess) return e;
+  drp_dbg_mark("tile_scan(nch)", st);
   return drp_launch_stream_counts(Q.tile_prefix, nstreams, Q.tile_count, Q.tile_base, Q.tile_nch, Q.tile_nch_base,
                                   Q.scount, st, Q.counter + 3);
 }

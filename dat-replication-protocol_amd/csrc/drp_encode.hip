@@ -699,6 +699,8 @@ using namespace drp;
 // the capacity allows; blocks past the real end exit at once)
 extern "C" uint64_t drp_encode_out_blocks(uint64_t cap) { return (cap + 15) / ENC_BS + 2; }
 
+extern "C" void drp_dbg_mark(const char *name, hipStream_t st);  // (drp_api.hip: DRP_WATCHDOG)
+
 extern "C" hipError_t drp_launch_encode(const EncodeParams *Pp, hipStream_t st) {
   EncodeParams P = *Pp;
   if (P.n == 0) return hipSuccess;
@@ -706,12 +708,15 @@ extern "C" hipError_t drp_launch_encode(const EncodeParams *Pp, hipStream_t st) 
   hipLaunchKernelGGL(enc_size_kernel, dim3((uint32_t)nblk), dim3(SCAN_BLK), 0, st, P);
   hipLaunchKernelGGL(enc_blocksum_kernel, dim3(1), dim3(SCAN_BLK), 0, st, P, nblk);
   hipLaunchKernelGGL(enc_addbase_kernel, dim3((uint32_t)nblk), dim3(SCAN_BLK), 0, st, P);
+  drp_dbg_mark("enc_size+scan", st);
   if (P.out && DRP_ENC_OS && P.nob && P.nob < (1ull << 31)) {
     hipLaunchKernelGGL(enc_oblk_kernel, dim3((uint32_t)((P.n + 255) / 256)), dim3(256), 0, st, P);
     hipError_t e = hipMemsetAsync(P.dense_n, 0, 4, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(enc_write_os, dim3((uint32_t)P.nob), dim3(ENC_OS_T), 0, st, P);
+    drp_dbg_mark("enc_write_os", st);
     hipLaunchKernelGGL(enc_write_dense, dim3(2048), dim3(256), 0, st, P);
+    drp_dbg_mark("enc_write_dense", st);
   } else if (P.out) {
     uint64_t waves = P.n < DRP_ENC_WAVES ? P.n : DRP_ENC_WAVES;  // one frame per wave at a time
     uint32_t grid = (uint32_t)((waves * 64 + 255) / 256);
