@@ -141,6 +141,7 @@ struct drp_ctx {
   // predictions, DRP_DIRTY_CAP caps the repair dirty lists, DRP_STATS / DRP_TRACE_FILE collect
   // kernel counters and per-tile traces into dstats (allocated here when asked for)
   uint32_t kstrong_hbm = 0;
+  uint32_t cascade_min = 4096;  // DRP_CASCADE_MIN (tests: small cascades)
   uint64_t dirty_cap = ~0ull;
   bool stats = false;
   const char *trace_file = nullptr;
@@ -221,6 +222,7 @@ int drp_open(int device, drp_ctx **out) {
     if (v > 0 && v <= 32) c->waves_per_cu = (uint32_t)v;
   }
   if (const char *e = getenv("DRP_KSTRONG_HBM")) c->kstrong_hbm = (uint32_t)atoi(e);
+  if (const char *e = getenv("DRP_CASCADE_MIN")) c->cascade_min = (uint32_t)strtoul(e, nullptr, 10);
   if (const char *e = getenv("DRP_DIRTY_CAP")) c->dirty_cap = strtoull(e, nullptr, 10);
   c->trace_file = getenv("DRP_TRACE_FILE");
   if (getenv("DRP_STATS") && hipMalloc((void **)&c->dstats, 64 * 8) == hipSuccess) c->stats = true;
@@ -610,6 +612,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.pass_id = 1;
   P.change_checks = (uint32_t)c->change_checks;
   P.kstrong_hbm = c->kstrong_hbm;  // (tests: weaker predictions)
+  P.cascade_min = c->cascade_min;
   CHK(hipMemsetAsync(P.dstamp, 0, NT * 4, st));
   P.dlist_cap = std::min<uint64_t>(NT, c->dirty_cap);  // (tests: DRP_DIRTY_CAP)
   CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
@@ -659,7 +662,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     for (; pass < kSpecRepairPasses && (h[1] & miss); pass++) {
       // a dirty list this long after a pass is a cascade already (C5's first list is ~300 tiles)
       const uint64_t seg_early = std::max<uint64_t>(1024, NT / 256);
-      if ((pass >= kSegRepairAfter || h[8 + k] > seg_early) && !seg_done) {
+      if ((pass >= kSegRepairAfter || h[8 + k] > seg_early || (h[1] & drp_spec_cascade_bit())) && !seg_done) {
         // the misses keep coming one tile per pass (wrong predictions that agree with each
         // other): recompute the claims of each stream from its first missed tile by exact
         // chain walks (drp_decode_spec.hip, segmented repair), then verify them

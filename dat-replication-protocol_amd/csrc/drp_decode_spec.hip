@@ -91,6 +91,7 @@ constexpr uint64_t NONE = ~0ull;              // internal: no chain
 
 constexpr uint32_t F_MISS = 1u << 12;         // overflow bit: prediction failed -> exact re-run
 constexpr uint32_t F_WAIT = 1u << 13;
+constexpr uint32_t F_CASCADE = 1u << 14;      // with F_MISS: go straight to the segmented repair
          // overflow bit: bounded wait expired -> exact re-run
 
 // header parse on a 16-byte window (same grammar as parse_hdr_lds)
@@ -383,6 +384,16 @@ __device__ __forceinline__ uint32_t wave_max_dpp(uint32_t v) {
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false));
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 #endif
+}
+
+__device__ __forceinline__ uint32_t wave_min_dpp(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, 0x111, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, 0x112, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, 0x114, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, 0x118, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, 0x142, 0xA, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, 0x143, 0xC, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 // block-wide reductions over the NT threads (two barriers; scratch: NT / WAVE words). The scratch
@@ -1567,6 +1578,9 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
 // that does not pass (a re-walk is needed, a miss, a longer identity run) goes to a list that
 // verify_counts then takes, so results are verify_counts' in every case. Threads before k are
 // left to emit_tiles through tile_k (the records stay as kernel 1 wrote them).
+#ifndef DRP_CASCADE_DIV
+#define DRP_CASCADE_DIV 8  // verify_counts hands the listed tiles to the segmented repair when more
+#endif                     // than 1/8 of the tiles (and P.cascade_min) are listed (0: never)
 constexpr uint32_t VL_BLK = 256, VL_G = NT / 16;  // lanes per tile (16 threads' records each)
 #ifndef DRP_SP_FRAMES
 #define DRP_SP_FRAMES 8  // frames of a sparse tile (0: no sparse emission)
@@ -1666,6 +1680,29 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
       atomicOr(P.dlist_n + 2, 1u);
       atomicOr(P.overflow, F_MISS);
     }
+    return;
+  }
+  // A cascade: verify_lite listed more than 1 / DRP_CASCADE_DIV of the tiles (and at least
+  // P.cascade_min, 4096 unless DRP_CASCADE_MIN says otherwise), i.e. the prediction followed a
+  // second framing through the stream (tests/_streams.shadow_stream). Re-walking every listed tile only to find them missed costs
+  // as much as the segmented repair that follows (1.7 GB dense cascade: 2.4 of 11.7 ms), so the
+  // list goes to that repair directly: each stream's first listed tile in first_miss (every tile
+  // before it passed the records-only proof, so its entry is exact) and F_CASCADE for the host.
+  // Only in the head's pass (pass_id 1).
+  if (DRP_CASCADE_DIV && P.pass_id == 1 && P.vlist && !P.vlist_ovf && nwork >= P.cascade_min &&
+      (uint64_t)nwork * DRP_CASCADE_DIV > ntiles) {
+    // one stream: a wave minimum, one atomic per wave; several: one atomic per listed tile
+    uint32_t tmin = ~0u;
+    for (uint32_t wi = blockIdx.x * NT + tid; wi < nwork; wi += gridDim.x * NT) {
+      const uint32_t t = P.vlist[wi];
+      if (P.nstreams == 1) tmin = min(tmin, t);
+      else atomicMin((unsigned long long *)&P.first_miss[P.tile_stream[t]], (unsigned long long)t);
+    }
+    if (P.nstreams == 1) {
+      tmin = wave_min_dpp(tmin);
+      if (lane == 0 && tmin != ~0u) atomicMin((unsigned long long *)&P.first_miss[0], (unsigned long long)tmin);
+    }
+    if (blockIdx.x == 0 && tid == 0) atomicOr(P.overflow, F_MISS | F_CASCADE);
     return;
   }
   for (uint32_t wi = blockIdx.x; P.vlist ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
@@ -2991,6 +3028,7 @@ extern "C" uint32_t drp_spec_tile_bytes(void) { return spec::TILE; }
 extern "C" uint32_t drp_spec_retry_mask(void) { return spec::F_MISS | spec::F_WAIT; }
 
 extern "C" uint32_t drp_spec_miss_bit(void) { return spec::F_MISS; }
+extern "C" uint32_t drp_spec_cascade_bit(void) { return spec::F_CASCADE; }
 
 // Claims and verification only (the host checks the prediction before anything is emitted).
 extern "C" void drp_dbg_mark(const char *name, hipStream_t st);  // (drp_api.hip: DRP_WATCHDOG)

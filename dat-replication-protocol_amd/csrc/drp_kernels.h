@@ -71,6 +71,7 @@ struct DecodeParams {
   uint32_t pass_id;     // this verify pass (1: the head's; zeroed stamps before it)
   uint32_t change_checks;  // 1: claims_fast checks long frames' Change structure (drp_api.hip picks)
   int kstrong_hbm;      // 0: DRP_KSTRONG_HBM; else frames a deferred candidate must survive (tests)
+  uint32_t cascade_min;  // listed tiles that make the head's verify a cascade (drp_decode_spec.hip)
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
   unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
 };
@@ -103,6 +104,7 @@ uint32_t drp_decode_waves_per_group(void);  // tiles (waves) per workgroup; grid
 uint32_t drp_spec_tile_bytes(void);
 uint32_t drp_spec_retry_mask(void);
 uint32_t drp_spec_miss_bit(void);
+uint32_t drp_spec_cascade_bit(void);
 hipError_t drp_launch_spec_head(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                 uint32_t *tile_stream, hipStream_t st);
 // out[0] = payload bytes of the blob rows among rows [0, n) (out zeroed by the caller)

@@ -1,5 +1,6 @@
 """Probe: decode times of dense two-framing (shadow) streams on the default path, with the
-path taken (repair passes, segmented repairs, exact re-runs). Usage: python scripts/probe_dense.py"""
+path taken (repair passes, segmented repairs, exact re-runs). Usage: python scripts/probe_dense.py [k]
+(k: only the k-th case, e.g. under rocprofv3)"""
 import ctypes as C
 import os
 import sys
@@ -17,8 +18,8 @@ from _gpu import drp_amd  # noqa: E402
 
 dev = torch.device("cuda", 0)
 ctx = drp_amd.Ctx(0)
-for period, at, small, gb in [(200, 20, 4, 0.2), (200, 20, 4, 1.7), (1000, 40, 10, 1.7), (3000, 70, 4, 1.7),
-                              (6000, 200, 40, 0.5)]:
+CASES = [(200, 20, 4, 0.2), (200, 20, 4, 1.7), (1000, 40, 10, 1.7), (3000, 70, 4, 1.7), (6000, 200, 40, 0.5)]
+for period, at, small, gb in ([CASES[int(sys.argv[1])]] if len(sys.argv) > 1 else CASES):
     n = int(gb * 1e9) // period
     w = torch.from_numpy(S.shadow_stream_np(n, period=period, shadow_at=at, small=small)).to(dev)
     so = torch.tensor([0, w.numel()], dtype=torch.int64, device=dev)
