@@ -1114,6 +1114,13 @@ __device__ __forceinline__ void flink(const uint32_t *lnd, uint32_t s1r, uint32_
   }
 }
 
+// measurement builds (DRP_ABLATE_F): every value a later phase would read is kept live through an
+// empty asm, so the build's instruction counts are those of the phases before the stop
+__device__ __forceinline__ void abl_sink1(uint64_t v) { asm volatile("" ::"v"(v)); }
+template <class... T>
+__device__ __forceinline__ void abl_sink(const T &...v) {
+  (abl_sink1((uint64_t)v), ...);
+}
 // measurement builds (DRP_ABLATE_F): valid "no prediction" records that keep x live
 __device__ __forceinline__ void abl_out(const DecodeParams &P, uint64_t t, uint64_t x) {
   const uint64_t ix = t * NT + threadIdx.x;
@@ -1210,7 +1217,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   const uint64_t Xs1 = (X0 >> 1) | (X1 << 63), Xs2 = (X0 >> 2) | (X1 << 62), Ms1 = (M0 >> 1) | (M1 << 63);
   const uint64_t live = X0 | (M0 & (Xs1 | (Ms1 & Xs2)));
 #if DRP_ABLATE_F == 1
-  abl_out(P, t, (uint64_t)(live));
+  abl_sink(live);
+  abl_out(P, t, 0);
   return FC_ABLATE;
 #endif
   // Halo nodes (DRP_HALO_NODES): the halo's live positions join the list as HV more "threads", so
@@ -1376,7 +1384,10 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   }
   bsync();
 #if DRP_ABLATE_F == 2
-  abl_out(P, t, (uint64_t)(ncode[0] + na[1]));
+#pragma unroll
+  for (uint32_t j = 0; j < KPT; j++) abl_sink(ncode[j], na[j], npos[j]);
+  abl_sink(live, off);
+  abl_out(P, t, 0);
   return FC_ABLATE;
 #endif
   lmw[tid] = 0;  // (now the strong masks)
@@ -1419,13 +1430,15 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     far = gc == NX_FAR || gc == NX_NEAR;
   }
 #if DRP_ABLATE_F == 3
-  abl_out(P, t, (uint64_t)(g + defer));
+  abl_sink(g, defer, far, live, off);
+  abl_out(P, t, 0);
   return FC_ABLATE;
 #endif
   uint32_t n = 0, R = RX_NONE;
   if (g != RX_NONE) R = fwalk(lnd, g, s1r, n);
 #if DRP_ABLATE_F == 4
-  abl_out(P, t, (uint64_t)(R + n));
+  abl_sink(g, defer, far, R, n, live, off);
+  abl_out(P, t, 0);
   return FC_ABLATE;
 #endif
   // rule 2: a chain that starts by jumping past the tile only where nothing later can start one
@@ -1458,7 +1471,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   bool rs = false;
   flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow, P.stats);
 #if DRP_ABLATE_F == 5
-  abl_out(P, t, (uint64_t)(R + E));
+  abl_sink(g, defer, R, n, E, rs, S0m, S1m, live, off);
+  abl_out(P, t, 0);
   return FC_ABLATE;
 #endif
   // restarts from deferred candidates, decided in HBM (big frames), as in spec_claims
@@ -1491,7 +1505,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     block_max2_u32(need, js, xf);
   }
 #if DRP_ABLATE_F == 6
-  abl_out(P, t, (uint64_t)(R + E + need));
+  abl_sink(g, R, n, E, rs, js, moved, S0m, S1m, live, off);
+  abl_out(P, t, 0);
   return FC_ABLATE;
 #endif
   // rule 3: the chain's last frame may jump over threads holding strong candidates; keep the

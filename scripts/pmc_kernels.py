@@ -1,6 +1,6 @@
 """Per-kernel PMC summary of scripts/gpu_pmc.sh passes (gpurun_out/pmc/<pass>/): average per dispatch
 and per frame, FETCH_SIZE doubled per the gfx950 note (MI355X_MICROARCH.md: 128-B requests
-tallied at 64 B). Usage: python scripts/pmc_kernels.py [frames] [--dir gpurun_out/pmc] [--workload c2|c4|c5]
+tallied at 64 B). Usage: python scripts/pmc_kernels.py [frames (default: from the passes' bench lines)] [--dir gpurun_out/pmc] [--workload c2|c4|c5]
 [--write profiles/pmc_<workload>.json] (c5: the encode kernels are counted too: its roofline prices the
 round trip)"""
 import collections
@@ -14,7 +14,27 @@ PMC_DIR = sys.argv[sys.argv.index("--dir") + 1] if "--dir" in sys.argv else "gpu
 WORKLOAD = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else "c2"
 opt_vals = {sys.argv[sys.argv.index(o) + 1] for o in ("--dir", "--write", "--workload") if o in sys.argv}
 args = [a for a in sys.argv[1:] if not a.startswith("--") and a not in opt_vals]
-frames = float(args[0]) if args else 20e6
+
+
+def frames_from_logs():
+    """The frames one dispatch of the workload decodes, from the bench JSON line a pass logged
+    (C2: frames_per_gpu; C4: frames_node; C5: the Changes per GPU in its workload string)."""
+    import re
+    for f in sorted(glob.glob(PMC_DIR + "/*.log")):
+        for line in open(f, errors="replace"):
+            if line.startswith('{"metric"'):
+                cfg = json.loads(line).get("config", {})
+                if "frames_per_gpu" in cfg:
+                    return float(cfg["frames_per_gpu"])
+                if "frames_node" in cfg:
+                    return float(cfg["frames_node"])
+                m = re.match(r"C5: (\d+) Changes", cfg.get("workload", ""))
+                if m:
+                    return float(m.group(1))
+    return None
+
+
+frames = float(args[0]) if args else (frames_from_logs() or 20e6)
 tot = collections.defaultdict(float)
 disp = collections.defaultdict(set)
 for f in glob.glob(PMC_DIR + "/*/**/*counter_collection.csv", recursive=True):
