@@ -431,6 +431,31 @@ __device__ __forceinline__ void block_max2_u32(uint32_t &a, uint32_t &b, uint32_
   }
   bsync();
 }
+// need = any thread's pn; js = (the last thread with pj) + 1, or 0: ballots and one exchange
+// (block_max2_u32 over 0/1 and tid + 1 values, without the wave reductions)
+__device__ __forceinline__ void block_any_last(bool pn, bool pj, uint32_t &need, uint32_t &js, uint32_t *xf) {
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  const uint64_t bn = __ballot(pn), bj = __ballot(pj);
+  const uint32_t n_w = bn != 0, j_w = bj ? wid * WAVE + 64u - (uint32_t)__builtin_clzll(bj) : 0u;
+  if constexpr (NT == WAVE) {
+    need = n_w;
+    js = j_w;
+    return;
+  }
+  if (lane == 0) {
+    xf[wid] = n_w;
+    xf[NT / WAVE + wid] = j_w;
+  }
+  bsync();
+  need = 0;
+  js = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < NT / WAVE; w++) {
+    need |= xf[w];
+    js = max(js, xf[NT / WAVE + w]);
+  }
+  bsync();
+}
 // bits strictly above bit j of the 128-bit mask (m0 low, m1 high) exist
 __device__ __forceinline__ bool any_above(uint64_t m0, uint64_t m1, uint32_t j) {
   if (j >= 64) return j < 127 && (m1 >> (j - 63)) != 0;
@@ -1257,6 +1282,11 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     push_work(P, t);
     return FC_DENSE;
   }
+#if DRP_ABLATE_F == 11
+  abl_sink(live, hlive, off, total, ttotal, hpre);
+  abl_out(P, t, 0);
+  return FC_ABLATE;
+#endif
   loff[tid] = (uint16_t)off;
   {
     uint64_t bits = live;
@@ -1276,6 +1306,11 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     }
   }
   bsync();
+#if DRP_ABLATE_F == 12
+  abl_sink(live, off, total, ttotal);
+  abl_out(P, t, 0);
+  return FC_ABLATE;
+#endif
   // ---- parse every node once --------------------------------------------------------------------
   const uint32_t se_rel = (uint32_t)umin64(G.se - G.A, 0x7FFFFFFFull);  // >= IMG
   constexpr uint32_t KPT = FCAP / NT;  // nodes per thread (at most)
@@ -1477,9 +1512,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
 #endif
   // restarts from deferred candidates, decided in HBM (big frames), as in spec_claims
   const Img m{buf, P.bytes, G.A, G.se, !DRP_K1_GIMG};
-  uint32_t need = (E == RX_NONE && defer && !any_above(S0m, S1m, tid)) ? 1u : 0u;
-  uint32_t js = (rx_node(E) && rx_off(E) < s1r) ? tid + 1 : 0u;  // last carrier + 1
-  block_max2_u32(need, js, xf);
+  uint32_t need, js;  // a thread needs a restart; the last carrier + 1
+  block_any_last(E == RX_NONE && defer && !any_above(S0m, S1m, tid), rx_node(E) && rx_off(E) < s1r, need, js, xf);
   bool moved = false;
 #pragma unroll 1
   for (uint32_t it = 0; need && it < 3; it++) {
@@ -1500,9 +1534,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
       }
     }
     flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow);
-    need = (E == RX_NONE && defer && !any_above(S0m, S1m, tid)) ? 1u : 0u;
-    js = (rx_node(E) && rx_off(E) < s1r) ? tid + 1 : 0u;
-    block_max2_u32(need, js, xf);
+    block_any_last(E == RX_NONE && defer && !any_above(S0m, S1m, tid), rx_node(E) && rx_off(E) < s1r, need, js,
+                   xf);
   }
 #if DRP_ABLATE_F == 6
   abl_sink(g, R, n, E, rs, js, moved, S0m, S1m, live, off);
