@@ -1180,6 +1180,8 @@ struct FastLds {
   uint16_t lpos[FCAP];
   uint32_t lnd[FCAP > NT + 1 ? FCAP : NT + 1];  // nodes (first: the next-16-byte masks; last: the emit list)
   uint8_t lal[FCAP];  // 0 dead, 1 strong, 2 undecided (leaves the image)
+  uint32_t lsucc[FCAP];  // successor offset of the nodes whose frame leaves the list (the claim of a
+                         // chain that ends in one: no header re-read from HBM at the tile's end)
   uint32_t xw[8];
   uint32_t xf[2 * NT / WAVE], wl[NT / WAVE], fl[NT / WAVE];
   uint64_t xm[4];  // candidate masks (two waves): [w] strong, [2 + w] strong and far
@@ -1359,9 +1361,11 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
       } else if (succ >= se_rel) {
         c = NX_NEAR;  // ends at the stream end: survived
         a = 1;
+        S.lsucc[i] = succ;
       } else if (succ >= (DRP_HALO_NODES ? IMG - 16 : TILE)) {
         c = NX_FAR;   // past the listed positions: undecided (a restart that needs it checks in HBM),
         a = 2;        // unless it is a Change frame whose fields fill it exactly (below)
+        S.lsucc[i] = succ;
         // (halo nodes: only frames longer than the halo, so C2's short frames there never pay for
         // it; C5's long ones do, so a tile's last real frame is not left undecided by its successor)
         // The first field is checked here from the header's own bytes (no load): subset or key
@@ -1582,8 +1586,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     if (R < RX_DEAD && !rx_node(R)) {
       const uint64_t p = G.A + lpos[R & 0xFFFFu];
       if (R & RX_FAR) {
-        const Hdr h = m.at(p);
-        if (h.kind == H_VALID) cl = h.succ;
+        cl = G.A + S.lsucc[R & 0xFFFFu];  // (the node's header is valid: fwalk gives RX_FAR for NX_FAR / NX_NEAR)
       } else {
         cl = MARK_TERM | p;  // a tail ends the chain
       }
