@@ -638,6 +638,42 @@ __device__ __forceinline__ uint64_t stage_live(const DecodeParams &P, const Tile
   return live;
 }
 
+// stage_live's live mask of this thread's bytes, from an image already staged in LDS
+__device__ __forceinline__ uint64_t live_lds(const TileGeo &G, const uint8_t *buf) {
+  const uint32_t tid = threadIdx.x;
+  const uint64_t lb = G.A + (uint64_t)tid * SEGB;
+  uint32_t m16[5], s16[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) gather16(*reinterpret_cast<const uint4 *>(buf + tid * SEGB + 16 * k), m16[k], s16[k]);
+  const uint64_t M0 = (uint64_t)m16[0] | ((uint64_t)m16[1] << 16) | ((uint64_t)m16[2] << 32) | ((uint64_t)m16[3] << 48);
+  const uint64_t S0 = (uint64_t)s16[0] | ((uint64_t)s16[1] << 16) | ((uint64_t)s16[2] << 32) | ((uint64_t)s16[3] << 48);
+  const uint64_t M1 = m16[4], S1 = s16[4];
+  uint64_t X[2], Mk[2];
+  X[0] = ~M0 & ((S0 >> 1) | (S1 << 63));
+  X[1] = ~M1 & (S1 >> 1);
+  Mk[0] = M0;
+  Mk[1] = M1;
+#pragma unroll
+  for (uint32_t d = 1; d <= 8; d <<= 1) {
+    const uint64_t x0 = (X[0] >> d) | (X[1] << (64 - d)), x1 = X[1] >> d;
+    X[0] |= Mk[0] & x0;
+    X[1] |= Mk[1] & x1;
+    if (d < 8) {
+      const uint64_t m0 = (Mk[0] >> d) | (Mk[1] << (64 - d)), m1 = Mk[1] >> d;
+      Mk[0] &= m0;
+      Mk[1] &= m1;
+    }
+  }
+  uint64_t live = X[0];
+  const uint64_t lo = G.so > lb ? G.so - lb : 0, hi = G.se > lb ? G.se - lb : 0;
+  if (lo >= 64 || hi == 0) live = 0;
+  else {
+    if (lo) live &= ~0ull << lo;
+    if (hi < 64) live &= (1ull << hi) - 1;
+  }
+  return live;
+}
+
 // ==== kernel 1: every tile's claim (entry-independent, no waiting) ===========================
 #ifndef DRP_LLCAP
 #define DRP_LLCAP (8 * DRP_SPEC_NT)  // 1024 live positions per 8 KiB tile (C2 has ~220)
@@ -2722,6 +2758,7 @@ __device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t
 // A verify pass then proves the new claims as usual. Cost: two streaming passes over the range
 // spread over the CUs plus a short serial stitch, however the predictions failed.
 constexpr uint32_t SEG_CAND = 64, SEG_GMAX = 1024;  // candidates per segment, tiles per segment (max)
+static_assert((uint64_t)SEG_GMAX * TILE < (1ull << 32), "seg_walk: 32-bit offsets in a segment");
 constexpr uint64_t SEG_NMAX = 8192;  // segments per repair (max)
 #ifndef DRP_SEG_NTARGET
 #define DRP_SEG_NTARGET 2048
@@ -2780,9 +2817,151 @@ __device__ __forceinline__ uint64_t seg_advance(const Img &m, uint64_t p, uint64
   }
   return p;
 }
+// seg_advance, counting the headers parsed (steps)
+__device__ __forceinline__ uint64_t seg_advance_n(const Img &m, uint64_t p, uint64_t lim, uint32_t &steps) {
+  while (is_pos(p) && p < lim && p < m.se) {
+    const Hdr h = hdr_fast(m, p);
+    steps++;
+    if (h.kind != H_VALID) return term_of(h, p);
+    p = h.succ;
+  }
+  return p;
+}
 
+// One tile of seg_walk's chains by table (the candidates' serial walks cost one header parse per
+// frame, and a lane on a dense shadow chain walks ~80 frames per tile): every live position of the
+// tile is parsed once into a node (its successor node, or its exit: a position at or past lim,
+// or the chain's terminal), then pointer jumping gives every node its exit in log2(chain length)
+// rounds, and each lane of wave 0 looks its chain's exit up. A successor that is not a live
+// position (a header with a varint of more than 3 bytes, or none) continues serially from there,
+// as does a tile with more than SW_CAP live positions. Same exits as seg_advance.
+constexpr uint32_t SW_CAP = 512, SW_KW = SW_CAP / NT;
+constexpr uint32_t SW_TERM = 0xFFFFFFFFu, SW_CONT = 0xFFFFFFFEu;  // (node codes below SW_CONT)
+constexpr uint32_t SW_STEPS = 40;  // headers per tile above which the next tile is walked by table
+struct SegWalkLds {
+  uint64_t lmw[NT];
+  uint64_t val[SW_CAP];
+  uint32_t nx[SW_CAP];
+  uint16_t dist[SW_CAP];  // headers from the node to its value (its chain's steps)
+  uint16_t loff[NT];
+  uint16_t lpos[SW_CAP];
+  uint32_t xw[NT / WAVE], fl[NT / WAVE];
+};
+__device__ __forceinline__ uint64_t seg_tile_walk(const DecodeParams &P, const TileGeo &G, const uint8_t *buf,
+                                                  SegWalkLds &T, uint64_t pos, uint64_t lim, uint32_t &steps) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  const Img mt{buf, P.bytes, G.A, G.se};
+  const uint64_t live = live_lds(G, buf);
+  const uint32_t cnt = (uint32_t)__builtin_popcountll(live);
+  const uint32_t pre = wave_scan_dpp(cnt);
+  if (lane == 63) T.xw[wid] = pre;
+  T.lmw[tid] = live;
+  bsync();
+  const uint32_t off = pre - cnt + (wid ? T.xw[0] : 0u);
+  const uint32_t total = NT == 2 * WAVE ? T.xw[0] + T.xw[1] : T.xw[0];
+  const bool mine = wid == 0 && is_pos(pos) && pos >= G.A && pos < lim;  // (this lane's chain is here)
+  if (total > SW_CAP) {  // dense tile: serial walks
+    if (mine) pos = seg_advance_n(mt, pos, lim, steps);
+    return pos;
+  }
+  T.loff[tid] = (uint16_t)off;
+  {
+    uint64_t bits = live;
+    uint32_t i = off;
+    while (bits) {
+      T.lpos[i++] = (uint16_t)(tid * SEGB + (uint32_t)__builtin_ctzll(bits));
+      bits &= bits - 1;
+    }
+  }
+  bsync();
+#pragma unroll
+  for (uint32_t k = 0; k < SW_KW; k++) {
+    const uint32_t i = tid + k * NT;
+    if (i < total) {
+      const uint64_t p = G.A + T.lpos[i];
+      const Hdr h = hdr_fast(mt, p);
+      uint32_t nx = SW_TERM;
+      uint64_t v = 0;
+      if (h.kind != H_VALID) {
+        v = term_of(h, p);
+      } else if (h.succ >= lim || h.succ >= mt.se) {
+        v = h.succ;
+      } else {
+        const uint32_t rel = (uint32_t)(h.succ - G.A), th = rel / SEGB, b = rel % SEGB;
+        const uint64_t lw = T.lmw[th];
+        if ((lw >> b) & 1ull) {
+          nx = T.loff[th] + (uint32_t)__builtin_popcountll(lw & ((1ull << b) - 1ull));
+        } else {
+          nx = SW_CONT;
+          v = h.succ;
+        }
+      }
+      T.nx[i] = nx;
+      T.val[i] = v;
+      T.dist[i] = 1;
+    }
+  }
+  bsync();
+  // pointer jumping: a node's (next, value) becomes its next node's, until every next is a code
+  for (uint32_t round = 0;; round++) {
+    uint32_t nn[SW_KW], dd[SW_KW];
+    uint64_t vv[SW_KW];
+    uint32_t chm = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SW_KW; k++) {
+      const uint32_t i = tid + k * NT;
+      nn[k] = 0;
+      vv[k] = 0;
+      dd[k] = 0;
+      if (i < total) {
+        const uint32_t j = T.nx[i];
+        if (j < SW_CONT) {
+          nn[k] = T.nx[j];
+          vv[k] = T.val[j];
+          dd[k] = (uint32_t)T.dist[i] + T.dist[j];
+          chm |= 1u << k;
+        }
+      }
+    }
+    const uint64_t b = __ballot(chm != 0);
+    if (lane == 0) T.fl[wid] = b != 0;
+    bsync();  // this round's reads are done; flags visible
+    uint32_t more = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NT / WAVE; w++) more |= T.fl[w];
+#pragma unroll
+    for (uint32_t k = 0; k < SW_KW; k++)
+      if ((chm >> k) & 1u) {
+        T.nx[tid + k * NT] = nn[k];
+        T.val[tid + k * NT] = vv[k];
+        T.dist[tid + k * NT] = (uint16_t)min(dd[k], 0xFFFFu);
+      }
+    bsync();  // writes visible; flag reads done
+    if (!more || round > 16) break;  // (chains in a tile are shorter than 2^16 nodes)
+  }
+  if (mine) {
+    const uint32_t rel = (uint32_t)(pos - G.A), th = rel / SEGB, b = rel % SEGB;
+    const uint64_t lw = T.lmw[th];
+    if ((lw >> b) & 1ull) {
+      const uint32_t i = T.loff[th] + (uint32_t)__builtin_popcountll(lw & ((1ull << b) - 1ull));
+      const uint32_t c = T.nx[i];
+      pos = T.val[i];
+      steps += T.dist[i];
+      if (c == SW_CONT) pos = seg_advance_n(mt, pos, lim, steps);
+    } else {
+      pos = seg_advance_n(mt, pos, lim, steps);
+    }
+  }
+  return pos;
+}
+
+#ifndef DRP_SEG_TABLE
+#define DRP_SEG_TABLE 1  // 0: every candidate chain walked frame by frame (A/B)
+#endif
 __global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+  __shared__ SegWalkLds T;
+  __shared__ uint32_t tmode;
   __shared__ uint64_t cpos[SEG_CAND];
   __shared__ uint32_t xw[NT / WAVE];
   __shared__ uint64_t nxt;
@@ -2833,18 +3012,33 @@ __global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
   // the next tile is fetched into registers while wave 0 walks this one (the chains usually go on
   // there), so its load latency is not on the segment's serial path
   uint4 pv[SEGB / 16], ph;
+  bool table = false;
   for (;;) {
     TileGeo Gn = G;
     Gn.A = G.A + TILE;
     const bool pre = Gn.A < send;
     if (pre) load_image(P, Gn, pv, ph);
+    // (the image of the tile staged last) The walk is by table while the last tile's longest chain
+    // took more than SW_STEPS headers (dense chains), frame by frame otherwise.
+    uint32_t steps = 0;
+    if (DRP_SEG_TABLE && table) pos = seg_tile_walk(P, G, buf, T, pos, umin64(G.A + TILE, send), steps);
     if (wid == 0) {
-      const Img mt{buf, P.bytes, G.A, G.se};  // (the image of the tile staged last)
-      pos = seg_advance(mt, pos, umin64(G.A + TILE, send));
-      const uint64_t mn = lane_min64(is_pos(pos) && pos < send ? pos : NONE);
-      if (lane == 0) nxt = mn;
+      if (!(DRP_SEG_TABLE && table)) {
+        const Img mt{buf, P.bytes, G.A, G.se};
+        pos = seg_advance_n(mt, pos, umin64(G.A + TILE, send), steps);
+      }
+      // (the wave's lowest chain position, as a 32-bit offset from the segment start: a segment
+      // is at most SEG_GMAX tiles)
+      const uint64_t sb = seg_tile_a(G, ta);
+      const uint32_t mr = wave_min_dpp(is_pos(pos) && pos < send ? (uint32_t)(pos - umin64(pos, sb)) : ~0u);
+      const uint32_t smax = wave_max_dpp(steps);
+      if (lane == 0) {
+        nxt = mr == ~0u ? NONE : sb + mr;
+        tmode = smax > SW_STEPS;
+      }
     }
     bsync();
+    table = tmode != 0;
     const uint64_t q = nxt;
     if (q == NONE) break;
     G.A = seg_tile_a(G, ta + (q - seg_tile_a(G, ta)) / TILE);
