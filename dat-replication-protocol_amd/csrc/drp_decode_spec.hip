@@ -945,7 +945,10 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
   // per-thread record for kernel 2: entry offset (| 0x40 when the thread restarts the chain,
   // 0xFF none), frames and change frames delivered from it
   {
-    const bool carrier = is_pos(E) && E < s1;
+    // (a thread at or past its stream's end gets the chain's end passed on as E: no record, so the
+    // records-only check does not read a wrapped entry byte as a restart and relist every stream's
+    // last tile)
+    const bool carrier = is_pos(E) && E >= lb && E < s1 && E < G.se;
     const uint64_t ix = t * NT + tid;
     P.ent[ix] = carrier ? (uint8_t)((E - lb) | (rs ? 0x40u : 0u)) : (uint8_t)0xFF;
     P.ent_n[ix] = carrier ? (uint8_t)(n & 0xFFFFu) : (uint8_t)0;
@@ -1899,7 +1902,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     uint32_t n = 0;
     uint64_t R = walk(m, E, s1, n);
     link<true>(m, s1, NONE, et, E, R, n, xr, xf, P.overflow);
-    const bool carrier = is_pos(E) && E < s1;
+    const bool carrier = is_pos(E) && E >= lb && E < s1 && E < G.se;  // (as spec_claims' records)
     P.ent[ix] = carrier ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // exact, for kernel 3
     P.ent_n[ix] = carrier ? (uint8_t)(n & 0xFFFFu) : (uint8_t)0;
     P.ent_c[ix] = carrier ? (uint8_t)(n >> 16) : (uint8_t)0;  // (a repair pass may take the fast check)
@@ -2327,6 +2330,76 @@ struct GlobalWinReader {
   }
 };
 
+// change_canon for a payload in HBM, in two dependent reads instead of one per field: the key
+// field from a window at the payload start, then change / from / to and the value header from a
+// 32-byte window after the key, parsed in registers. Canonical shape only (key first, varints of
+// <= 7 bytes, the value last); false: decode_change decides (same columns wherever this accepts).
+__device__ __forceinline__ bool change_canon_g(const GlobalWinReader &rd, uint64_t po, uint64_t pl, ChangeCols &c) {
+  c.subset_off = c.subset_len = c.value_off = c.value_len = 0;
+  c.change = c.from = c.to = 0;
+  c.flags = 0;
+  c.err = 0;
+  if (pl < 8 || pl > 0x7FFFFFFFull || !rd.ok(po, pl)) return false;
+  uint64_t w0, w1;
+  rd.win(po, w0, w1);
+  if ((w0 & 0xFFu) != 0x12u) return false;
+  const uint32_t b1 = (uint32_t)(w0 >> 8) & 0xFFu, b2 = (uint32_t)(w0 >> 16) & 0xFFu;
+  uint32_t kl, ko;
+  if (b1 < 0x80u) {
+    kl = b1;
+    ko = 2;
+  } else {
+    if (b2 >= 0x80u) return false;
+    kl = (b1 & 0x7Fu) | (b2 << 7);
+    ko = 3;
+  }
+  const uint64_t q = (uint64_t)ko + kl;
+  if (q >= pl) return false;
+  c.key_off = ko;
+  c.key_len = kl;
+  uint64_t x[4];
+  rd.win(po + q, x[0], x[1]);
+  rd.win(po + q + 16, x[2], x[3]);
+  uint64_t used = 0;
+  uint64_t v[3];
+#pragma unroll
+  for (uint32_t f = 0; f < 3; f++) {
+    if ((x[0] & 0xFFu) != 0x18u + 8u * f) return false;
+    const uint64_t y = x[0] >> 8;  // the varint's bytes (up to 7)
+    const uint64_t tm = ~y & 0x80808080808080ull;
+    if (!tm) return false;
+    const uint32_t k = ((uint32_t)__builtin_ctzll(tm) >> 3) + 1u;
+    v[f] = ((y & 0x7Full) | ((y >> 1) & 0x3F80ull) | ((y >> 2) & 0x1FC000ull) | ((y >> 3) & 0xFE00000ull) |
+            ((y >> 4) & 0x7F0000000ull) | ((y >> 5) & 0x3F800000000ull) | ((y >> 6) & 0x1FC0000000000ull)) &
+           ((1ull << (7u * k)) - 1ull);
+    const uint32_t sb = 8u * (1u + k);  // (2..8 bytes)
+    used += 1u + k;
+    if (q + used > pl) return false;
+    x[0] = sb == 64 ? x[1] : (x[0] >> sb) | (x[1] << (64u - sb));
+    x[1] = sb == 64 ? x[2] : (x[1] >> sb) | (x[2] << (64u - sb));
+    x[2] = sb == 64 ? x[3] : (x[2] >> sb) | (x[3] << (64u - sb));
+    x[3] = sb == 64 ? 0ull : x[3] >> sb;
+  }
+  c.change = v[0];
+  c.from = v[1];
+  c.to = v[2];
+  if (q + used == pl) return true;  // (no value)
+  if ((x[0] & 0xFFu) != 0x32u) return false;
+  const uint64_t y = x[0] >> 8;
+  const uint64_t tm = ~y & 0x80808080ull;  // a value length of <= 4 bytes
+  if (!tm) return false;
+  const uint32_t k = ((uint32_t)__builtin_ctzll(tm) >> 3) + 1u;
+  const uint64_t vl =
+      ((y & 0x7Full) | ((y >> 1) & 0x3F80ull) | ((y >> 2) & 0x1FC000ull) | ((y >> 3) & 0xFE00000ull)) &
+      ((1ull << (7u * k)) - 1ull);
+  const uint64_t vo = q + used + 1u + k;
+  if (vo + vl != pl) return false;
+  c.value_off = (uint32_t)vo;
+  c.value_len = (uint32_t)vl;
+  c.flags = DRP_F_VALUE;
+  return true;
+}
+
 constexpr uint32_t SP_TPB = 64;  // tiles per workgroup
 __global__ __launch_bounds__(256) void emit_sparse(DecodeParams P) {
   __shared__ uint32_t lst[SP_TPB * SP_FRAMES];  // tile (in the workgroup) << 16 | thread << 8 | rank
@@ -2393,7 +2466,8 @@ __global__ __launch_bounds__(256) void emit_sparse(DecodeParams P) {
     P.payload_len[f] = pl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pl;
     P.type[f] = (uint8_t)(h.id | (h.kind == H_TAIL_BLOB ? DRP_FRAME_PARTIAL : 0u));
     if (h.id != 1) continue;
-    const ChangeCols cc = decode_change(rd, po, pl);
+    ChangeCols cc;
+    if (!change_canon_g(rd, po, pl, cc)) cc = decode_change(rd, po, pl);
     P.key_off[f] = cc.key_off;
     P.key_len[f] = cc.key_len;
     P.subset_off[f] = cc.subset_off;
@@ -2658,10 +2732,12 @@ __device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t
   uint32_t *wsum = L.wsum;
   uint32_t &defer = L.defer;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  // emit_sparse wrote it (first: on C5 nearly every tile leaves here, after one load; the mark
+  // array covers the grid, and a stale mark past the tile count only ends a tile that ends anyway)
+  if (P.tile_sparse && P.tile_sparse[t]) return;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   const TileGeo G = tile_geo(P, t);
   if (t >= ntiles) return;  // (whole workgroup)
-  if (P.tile_sparse && P.tile_sparse[t]) return;  // emit_sparse wrote it
   const uint64_t A = G.A;
   const uint32_t se_rel = (uint32_t)umin64(G.se - A, 0x7FFFFFFFull);
   const uint32_t lim = se_rel < IMG ? se_rel : IMG;  // image bytes of the stream
