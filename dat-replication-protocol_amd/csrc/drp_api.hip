@@ -593,11 +593,6 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   uint64_t *sgscan = c->scratch.at<uint64_t>(L.scan_tmp);
   hipStream_t st = c->st;
   CHK(hipEventRecord(c->ev[0], st));
-  CHK(hipMemsetAsync(rec, 0, 2 * NT * 8, st));  // claim, incl_e
-  CHK(hipMemsetAsync(perr, 0xFF, ns * 8, st));
-  CHK(hipMemsetAsync(scount, 0, 2 * ns * 8, st));
-  CHK(hipMemsetAsync(ctrl, 0, 64, st));
-  CHK(drp_launch_tile_prefix(B, stream_off, ns, tile_prefix, st));
   DecodeParams P;
   memset(&P, 0, sizeof(P));
   P.bytes = bytes;
@@ -652,13 +647,24 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.change_checks = (uint32_t)c->change_checks;
   P.kstrong_hbm = c->kstrong_hbm;  // (tests: weaker predictions)
   P.cascade_min = c->cascade_min;
-  CHK(hipMemsetAsync(P.dstamp, 0, NT * 4, st));
   P.dlist_cap = std::min<uint64_t>(NT, c->dirty_cap);  // (tests: DRP_DIRTY_CAP)
-  CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
   unsigned long long *dstats = c->stats ? c->dstats : nullptr;
-  if (dstats) {
-    CHK(hipMemsetAsync(dstats, 0, 64 * 8, st));
-    P.stats = dstats;
+  if (dstats) P.stats = dstats;
+  {  // tile_prefix and every per-decode clear in one launch
+    ClearSet cs = {};
+    auto add = [&](void *p, uint64_t bytes, uint32_t v) {
+      cs.ptr[cs.n] = p;
+      cs.bytes[cs.n] = bytes;
+      cs.value[cs.n++] = v;
+    };
+    add(rec + NT, NT * 8, 0);  // incl_e (every claim is written by the claims kernels)
+    add(perr, ns * 8, 0xFF);
+    add(scount, 2 * ns * 8, 0);
+    add(ctrl, 64, 0);
+    add(P.dstamp, NT * 4, 0);
+    add(P.first_miss, ns * 8, 0xFF);
+    if (dstats) add(dstats, 64 * 8, 0);
+    CHK(drp_launch_prologue(B, stream_off, ns, tile_prefix, &cs, st));
   }
   c->timing.seg_repairs = 0;
   CHK(hipEventRecord(c->ev[1], st));
@@ -669,8 +675,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   // few passes (e.g. a protocol error on the exact chain) does the caller run the exact kernel.
   uint32_t h[16];
   const uint32_t miss = drp_spec_miss_bit();
-  CHK(drp_launch_spec_head(&P, NT, ns, tstream, st));
-  CHK(hipMemcpyAsync(ctrl + 14, ctrl + 5, 4, hipMemcpyDeviceToDevice, st));  // (verify's relisted tiles)
+  CHK(drp_launch_spec_head(&P, NT, ns, tstream, st));  // (verify_counts keeps the relisted count in ctrl[14])
   // Emission, the output bases and the per-stream results go right behind verification, with no
   // host read in between: the emit, finalize and key kernels read the flag word and do nothing
   // after a failed prediction, which is repaired below before they run again. A decode whose

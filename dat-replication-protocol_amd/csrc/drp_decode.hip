@@ -1463,8 +1463,34 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
 
 // tile_prefix[s] = number of tiles of streams < s; tile_prefix[nstreams] = total.
 template <int B>
+__device__ __forceinline__ void tile_prefix_body(const uint64_t *stream_off, uint64_t nstreams,
+                                                 uint64_t *tile_prefix);
+template <int B>
 __global__ __launch_bounds__(1024) void tile_prefix_kernel(const uint64_t *stream_off, uint64_t nstreams,
                                                            uint64_t *tile_prefix) {
+  tile_prefix_body<B>(stream_off, nstreams, tile_prefix);
+}
+// The speculative decode's prologue in one launch: workgroup 0 computes tile_prefix, the others
+// fill the per-decode scratch regions (each a multiple of 4 bytes, 4-byte aligned) with their
+// byte value: six hipMemsetAsync dispatches cost ~9 us apiece on the decode's serial path.
+template <int B>
+__global__ __launch_bounds__(1024) void prologue_kernel(const uint64_t *stream_off, uint64_t nstreams,
+                                                        uint64_t *tile_prefix, ClearSet cs) {
+  if (blockIdx.x == 0) {
+    tile_prefix_body<B>(stream_off, nstreams, tile_prefix);
+    return;
+  }
+  const uint64_t stride = (uint64_t)(gridDim.x - 1) * 1024u;
+  for (uint32_t r = 0; r < cs.n; r++) {
+    uint32_t *p = reinterpret_cast<uint32_t *>(cs.ptr[r]);
+    const uint64_t words = cs.bytes[r] / 4;
+    const uint32_t v = cs.value[r] * 0x01010101u;
+    for (uint64_t i = (uint64_t)(blockIdx.x - 1) * 1024u + threadIdx.x; i < words; i += stride) p[i] = v;
+  }
+}
+template <int B>
+__device__ __forceinline__ void tile_prefix_body(const uint64_t *stream_off, uint64_t nstreams,
+                                                 uint64_t *tile_prefix) {
   constexpr uint64_t TILE = 64ull * B;
   __shared__ uint64_t part[1024];
   __shared__ uint64_t carry;
@@ -1597,6 +1623,20 @@ extern "C" hipError_t drp_launch_tile_prefix(uint32_t B, const uint64_t *stream_
   switch (B) {
     case 64: hipLaunchKernelGGL(tile_prefix_kernel<64>, dim3(1), dim3(1024), 0, st, stream_off, nstreams, tile_prefix); break;
     case 128: hipLaunchKernelGGL(tile_prefix_kernel<128>, dim3(1), dim3(1024), 0, st, stream_off, nstreams, tile_prefix); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t drp_launch_prologue(uint32_t B, const uint64_t *stream_off, uint64_t nstreams,
+                                          uint64_t *tile_prefix, const ClearSet *cs, hipStream_t st) {
+  uint64_t mx = 0;
+  for (uint32_t r = 0; r < cs->n; r++) mx = cs->bytes[r] > mx ? cs->bytes[r] : mx;
+  const uint64_t blocks = (mx / 4 + 4096 - 1) / 4096;  // (4 words per thread and pass at most)
+  const uint32_t grid = 1u + (uint32_t)(blocks < 1024 ? (blocks ? blocks : 1) : 1024);
+  switch (B) {
+    case 64: hipLaunchKernelGGL(prologue_kernel<64>, dim3(grid), dim3(1024), 0, st, stream_off, nstreams, tile_prefix, *cs); break;
+    case 128: hipLaunchKernelGGL(prologue_kernel<128>, dim3(grid), dim3(1024), 0, st, stream_off, nstreams, tile_prefix, *cs); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

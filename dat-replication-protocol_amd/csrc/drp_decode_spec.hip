@@ -1765,6 +1765,8 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   // every tile (one per workgroup), or the tiles verify_lite listed (a few per workgroup)
   const uint32_t nwork = P.vlist ? *P.vlist_n : 0u;
+  if (P.pass_id == 1 && P.vlist && !P.vlist_ovf && blockIdx.x == 0 && tid == 0)
+    P.counter[14] = nwork;  // (the head's relisted tiles, for drp_timing.verify_relisted)
   if (P.vlist_ovf && (*P.vlist_ovf || nwork > P.dlist_cap)) {  // an incomplete dirty list: the host
     if (blockIdx.x == 0 && tid == 0) {                          // runs a full pass next
       atomicOr(P.dlist_n + 2, 1u);

@@ -97,6 +97,15 @@ struct EncodeParams {
 }  // namespace drp
 
 extern "C" {
+// regions a decode's prologue fills (drp_launch_prologue): byte value, 4-byte multiples
+struct ClearSet {
+  void *ptr[8];
+  uint64_t bytes[8];
+  uint32_t value[8];
+  uint32_t n;
+};
+hipError_t drp_launch_prologue(uint32_t B, const uint64_t *stream_off, uint64_t nstreams, uint64_t *tile_prefix,
+                               const ClearSet *cs, hipStream_t st);
 hipError_t drp_launch_tile_prefix(uint32_t B, const uint64_t *stream_off, uint64_t nstreams,
                                   uint64_t *tile_prefix, hipStream_t st);
 hipError_t drp_launch_decode(uint32_t B, const drp::DecodeParams *P, uint32_t grid, hipStream_t st);
