@@ -214,14 +214,19 @@ class Ctx:
         return ext
 
     def order_after_torch(self, t):
-        """libdrp's stream waits for the work queued so far on torch's current stream."""
+        """libdrp's stream waits for the work queued so far on torch's current stream (nothing
+        to do when torch's current stream is libdrp's own, e.g. under torch.cuda.stream(...))."""
         import torch
-        self._ext(t.device).wait_stream(torch.cuda.current_stream(t.device))
+        ext, cur = self._ext(t.device), torch.cuda.current_stream(t.device)
+        if cur.cuda_stream != ext.cuda_stream:
+            ext.wait_stream(cur)
 
     def order_torch_after(self, t):
         """torch's current stream waits for the work queued so far on libdrp's stream."""
         import torch
-        torch.cuda.current_stream(t.device).wait_stream(self._ext(t.device))
+        ext, cur = self._ext(t.device), torch.cuda.current_stream(t.device)
+        if cur.cuda_stream != ext.cuda_stream:
+            cur.wait_stream(ext)
 
     def set_strict(self, on):
         _chk("drp_set_strict", self.L.drp_set_strict(self.h, 1 if on else 0))
