@@ -12,7 +12,7 @@ phase, seen = 0, 0
 acc = collections.defaultdict(list)
 for r in rows:
     k = r["Kernel_Name"].split("(")[0].replace("drp::spec::", "").replace("drp::", "").replace("void ", "")
-    if k.startswith("tile_prefix_kernel"):
+    if k.startswith("tile_prefix_kernel") or k.startswith("prologue_kernel"):
         seen += 1
         phase = (seen - 1) // per
     acc[(phase, k)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)

@@ -6,7 +6,7 @@ import sys
 
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if "drp" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "tile_prefix" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "tile_prefix" in r["Kernel_Name"] or "prologue_kernel" in r["Kernel_Name"]]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else len(starts) - 1
 i0 = starts[k]
 i1 = starts[k + 1] if k + 1 < len(starts) else len(rows)
