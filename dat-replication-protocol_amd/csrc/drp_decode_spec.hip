@@ -2718,9 +2718,23 @@ struct LeanLds {
 };
 __device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t, LeanLds &L);
 
+// Long-frame streams (the context's change_checks form: >= 512 B per frame) leave nearly every
+// tile to emit_sparse, so a workgroup per tile would mostly be dispatched to exit: there each
+// workgroup takes EMIT_LONG_TPW tiles, strided by the grid (drp_launch_spec_tail sizes it).
+constexpr uint32_t EMIT_LONG_TPW = 8;
 __global__ __launch_bounds__(NT, DRP_EMIT_LEAN_WAVES) void emit_lean(DecodeParams P) {
   __shared__ LeanLds L;
   if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
+  if (P.change_checks) {
+    const uint64_t ntiles = P.tile_prefix[P.nstreams];
+    for (uint32_t j = 0; j < EMIT_LONG_TPW; j++) {
+      const uint64_t t = blockIdx.x + (uint64_t)j * gridDim.x;
+      if (t >= ntiles) break;  // (uniform)
+      if (j) bsync();          // (the last tile's LDS reads are done)
+      emit_lean_tile(P, t, L);
+    }
+    return;
+  }
   uint64_t t;
   {  // XCD-contiguous tile order, as the fast emit_tiles
     const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = blockIdx.x % 8u;
@@ -3451,7 +3465,10 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
       Q.tile_sparse = nullptr;
     }
     if (DRP_EMIT_LEAN)
-      hipLaunchKernelGGL(spec::emit_lean, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+      hipLaunchKernelGGL(spec::emit_lean,
+                         dim3((uint32_t)(Q.change_checks ? (nt_max + spec::EMIT_LONG_TPW - 1) / spec::EMIT_LONG_TPW
+                                                         : nt_max)),
+                         dim3(spec::NT), 0, st, Q);
     else
       hipLaunchKernelGGL(spec::emit_tiles<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
     drp_dbg_mark("emit_fast", st);
