@@ -254,6 +254,39 @@ def test_c5_predicted_without_repairs():
     assert t.strict_reruns == 0 and t.spec_repairs == 0, (t.spec_repairs, t.strict_reruns)
 
 
+def test_stream_ends_not_relisted():
+    """The same C2 frames as 1 and as 512 streams cut at frame boundaries: the records-only check
+    relists about as many tiles either way. (Threads past a stream's end used to get the chain's
+    end as a wrapped entry byte that read as a restart, so every stream's last tile went to the
+    full re-walk: C4 relisted 11909 tiles instead of ~4000.) Results stay exact (bench.verify_c4
+    checks the frame table against the generator)."""
+    import ctypes as C
+
+    import torch
+
+    import bench
+    from _gpu import drp_amd
+    dev = torch.device("cuda", 0)
+    n, fb = 2_000_000, 86
+    wire = bench.c2_on_device(n, seed=77, dev=dev)
+    outs = bench.alloc_outputs(n + 64, dev)
+    res = torch.zeros(512 * C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+    relisted = {}
+    with drp_amd.Ctx(0) as ctx:
+        for s in (1, 512):
+            per = n // s
+            cuts = [i * per * fb for i in range(s)] + [wire.numel()]
+            so = torch.tensor(cuts, dtype=torch.int64, device=dev)
+            ctx.decode_device(wire, so, None, outs, n + 64, res)
+            torch.cuda.synchronize()
+            t = ctx.timing()
+            assert t.strict_reruns == 0
+            relisted[s] = t.verify_relisted
+            off = outs["payload_off"][:n].cpu().numpy()
+            np.testing.assert_array_equal(off, np.arange(n, dtype=np.int64) * fb + 2)
+    assert relisted[512] <= relisted[1] + 64, relisted
+
+
 def test_c5_after_c2_on_one_context():
     """native.js pools contexts across streams, so a C5 stream can land on a context whose last
     decode was dense C2, which turned claims_fast's long-frame check off: that decode then relies
