@@ -792,7 +792,9 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
                                "k2_stage", "k2_entry", "k2_link", "k3_stage", "k3_link", "k3_emit"};
     for (int k = 0; k < 14; k++)
       if (ph[k][0]) fprintf(stderr, " %s=%.0f", ph[k], (double)hs[40 + k] / (double)(h[0] ? h[0] : 1));
-    fprintf(stderr, " repairs=%d (avg cycles per tile) link_rounds=%llu\n", pass, hs[56]);
+    fprintf(stderr, " repairs=%d (avg cycles per tile) link_rounds=%llu max=%llu tiles_over8=%llu restart_tiles=%llu"
+            " jump_tiles=%llu seg_claims: walk_cycles=%llu frames=%llu tiles=%llu wg_cycles=%llu\n", pass, hs[56],
+            hs[57], hs[58], hs[59], hs[60], hs[61], hs[62], hs[63], hs[55]);
   }
   if (h[1] & drp_spec_retry_mask()) return DRP_E_RETRY;
   if (h[1]) return DRP_E_CAPACITY;

@@ -684,6 +684,15 @@ constexpr uint16_t NX_NEAR = 0xFFFD, NX_FAR = 0xFFFE, NX_DEAD = 0xFFFF;
 #ifndef DRP_K1G_WAVES
 #define DRP_K1G_WAVES 5  // min waves per SIMD for the general claims kernel (edge and dense tiles)
 #endif
+#ifndef DRP_EDGE_FAST
+#define DRP_EDGE_FAST 1  // 0: stream-edge tiles take the general form (A/B)
+#endif
+// the fast form (below), which spec_claims also runs for the stream-edge tiles on its list
+struct FastLds;
+enum : uint32_t { FC_OK = 0, FC_DENSE = 1, FC_ABLATE = 2 };
+template <bool CF, bool EDGE = false>
+__device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const TileGeo &G, uint64_t t, FastLds &S,
+                                                uint32_t &eb_o, uint32_t &en_o, uint32_t &ecn_o, uint64_t &cl_o);
 __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint64_t xr[NT / WAVE];
@@ -706,6 +715,16 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
   bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
   if (t >= ntiles) continue;  // (whole workgroup)
+#if DRP_EDGE_FAST
+  // a stream-edge tile claims_fast listed: the fast form with the stream's bounds (its LDS in buf;
+  // one with more than FCAP live positions goes on below)
+  if (P.work && (G.A < G.so || G.A + IMG > G.se)) {
+    uint32_t eb, en, ecn;
+    uint64_t cl;
+    if (fast_claims<true, true>(P, G, t, *reinterpret_cast<FastLds *>(buf), eb, en, ecn, cl) != FC_DENSE) continue;
+    bsync();  // (its LDS reads are done before stage_live writes buf)
+  }
+#endif
   const uint64_t live = stage_live(P, G, buf);
   const Img m{buf, P.bytes, G.A, G.se};
   const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
@@ -1123,10 +1142,13 @@ __device__ __forceinline__ uint32_t fwalk(const uint32_t *lnd, uint32_t x, uint3
 }
 
 // Link rounds (spec mode of link()): a thread's entry is the exit of the latest carrier before it;
-// no carrier, or a dead one, restarts the chain at the thread's own strong node g.
-__device__ __forceinline__ void flink(const uint32_t *lnd, uint32_t s1r, uint32_t g, uint32_t &E, uint32_t &R,
+// no carrier, or a dead one, restarts the chain at the thread's own strong node g. A correction
+// travels one carrier per round, so two chains that never merge (a dense second framing) take a
+// round per frame of the tile: with cap, the rounds stop there and flink returns true (E, R, n
+// then unsettled; the caller takes claims_fast's pointer-jumping form instead).
+__device__ __forceinline__ bool flink(const uint32_t *lnd, uint32_t s1r, uint32_t g, uint32_t &E, uint32_t &R,
                                       uint32_t &n, bool &rs, uint32_t *wl, uint32_t *fl, uint32_t *overflow,
-                                      unsigned long long *stats = nullptr) {
+                                      unsigned long long *stats = nullptr, uint32_t cap = ~0u) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll 1
@@ -1154,8 +1176,13 @@ __device__ __forceinline__ void flink(const uint32_t *lnd, uint32_t s1r, uint32_
       more = (fl[0] | fl[1]) != 0;
     }
     rs = r;
+    if (more && round + 1 >= cap) return true;  // (block-uniform: more is)
     if (!more) {
-      if (stats && tid == 0) atomicAdd(&stats[56], (unsigned long long)(round + 1));  // (DRP_STATS)
+      if (stats && tid == 0) {  // (DRP_STATS: rounds, their maximum, tiles over 8)
+        atomicAdd(&stats[56], (unsigned long long)(round + 1));
+        atomicMax(&stats[57], (unsigned long long)(round + 1));
+        if (round + 1 > 8) atomicAdd(&stats[58], 1ull);
+      }
       if (ch) {  // a non-carrier passes the exit on
         E = En;
         R = En;
@@ -1176,6 +1203,7 @@ __device__ __forceinline__ void flink(const uint32_t *lnd, uint32_t s1r, uint32_
       }
     }
   }
+  return false;
 }
 
 // measurement builds (DRP_ABLATE_F): every value a later phase would read is kept live through an
@@ -1228,12 +1256,160 @@ struct FastLds {
   uint8_t pad[DRP_K1_PAD];  // (A/B only: caps the workgroups per CU through LDS)
 #endif
 };
-enum : uint32_t { FC_OK = 0, FC_DENSE = 1, FC_ABLATE = 2 };
+static_assert(sizeof(FastLds) <= IMG + 32, "spec_claims runs the edge form in its image buffer");
+
+__device__ __forceinline__ Hdr hdr_global(const uint8_t *g, uint64_t p, uint64_t se) {  // (as Img::at from HBM)
+  uint64_t w0, w1;
+  const uint64_t a = p & ~15ull;
+  const uint4 u = ld16(g, a, se), v = ld16(g, a + 16, se);
+  const uint64_t q0 = ((uint64_t)u.y << 32) | u.x, q1 = ((uint64_t)u.w << 32) | u.z;
+  const uint64_t q2 = ((uint64_t)v.y << 32) | v.x, q3 = ((uint64_t)v.w << 32) | v.z;
+  const uint32_t o = (uint32_t)(p & 15);
+  if (o < 8) {
+    w0 = funnel(q0, q1, 8 * o);
+    w1 = funnel(q1, q2, 8 * o);
+  } else {
+    w0 = funnel(q1, q2, 8 * (o - 8));
+    w1 = funnel(q2, q3, 8 * (o - 8));
+  }
+  return parse_win(w0, w1, p, se);
+}
+
+// claims_fast when the link rounds do not settle within DRP_FL_CAP rounds (two chains that never
+// merge, e.g. tests/_streams.shadow_stream's second framing: ~42 rounds per tile, 77% of the
+// kernel on that input). The converged link is the chain from the first thread's strong node,
+// node to node by each node's walk through its own thread's bytes (a death restarts at the next
+// thread's strong node; the halo, a frame past the image or a tail ends it). Every node's next
+// node is computed once, and pointer jumping gives every node its chain's end in log2(hops)
+// rounds; the claim is the first strong node's. The deferred restarts and rule 3 are not applied.
+// Records: none (0xFF), so the records-only check relists the tile and verify_counts re-walks it
+// from its exact entry (on the second framing, the cascade shortcut takes the whole list instead).
+#ifndef DRP_FL_CAP
+#define DRP_FL_CAP 8  // link rounds before the pointer-jumping form (~0: never)
+#endif
+constexpr uint32_t JT_C_ID = 2u << 30, JT_TERM = 1u << 30, JT_NONE = 0xFFFFu;
+template <uint32_t NTT>
+__device__ __forceinline__ uint32_t fast_claims_jump(const DecodeParams &P, uint64_t t, uint64_t A, FastLds &S, uint32_t g,
+                                                  uint32_t ttotal, uint32_t total, uint32_t &eb_o, uint32_t &en_o,
+                                                  uint32_t &ecn_o, uint64_t &cl_o) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  constexpr uint32_t KPT = FCAP / NTT;
+  uint16_t *nx = reinterpret_cast<uint16_t *>(S.lmw);  // (the candidate masks are read: free)
+  uint32_t *gl = reinterpret_cast<uint32_t *>(S.dmw);
+  uint32_t *lnd = S.lnd;
+  if (P.stats && tid == 0) atomicAdd(&P.stats[60], 1ull);  // (DRP_STATS: tiles in this form)
+  const uint64_t gm = __ballot(g != RX_NONE);
+  if (lane == 0) S.xm[wid] = gm;
+  gl[tid] = g;
+  bsync();
+  const uint64_t G0 = S.xm[0], G1 = NTT == 2 * WAVE ? S.xm[1] : 0ull;
+  uint32_t yn[KPT], yt[KPT];
+#pragma unroll
+  for (uint32_t j = 0; j < KPT; j++) {
+    const uint32_t i = tid + j * NTT;
+    yn[j] = JT_NONE;
+    yt[j] = JT_C_ID;
+    if (i < ttotal) {  // a tile node: the exit of the walk through its own thread's bytes
+      const uint32_t o = S.lpos[i], th = o / SEGB;
+      uint32_t cnt;
+      const uint32_t x = fwalk(lnd, i, (th + 1u) * SEGB, cnt);
+      if (rx_node(x)) {
+        const uint32_t k = x & 0xFFFFu;
+        if (S.lpos[k] >= TILE) yt[j] = S.lpos[k];  // (a halo node: the chain leaves the tile there)
+        else yn[j] = k;
+      } else if (x == RX_DEAD) {  // the next thread with a strong node restarts the chain
+        const uint64_t a0 = th + 1u < 64u ? G0 & (~0ull << (th + 1u)) : 0ull;
+        const uint64_t a1 = th + 1u < 64u ? G1 : (th + 1u < 128u ? G1 & (~0ull << (th + 1u - 64u)) : 0ull);
+        const uint32_t k = a0 ? (uint32_t)__builtin_ctzll(a0) : (a1 ? 64u + (uint32_t)__builtin_ctzll(a1) : NTT);
+        if (k < NTT) yn[j] = gl[k] & 0xFFFFu;
+      } else if (x & RX_FAR) {
+        yt[j] = S.lsucc[x & 0xFFFFu];
+      } else if (x & RX_TERM) {
+        yt[j] = JT_TERM | S.lpos[x & 0xFFFFu];
+      }
+    } else if (i < total) {
+      yt[j] = S.lpos[i];  // (halo nodes end chains)
+    }
+  }
+  bsync();  // (the walks' reads of lnd are done)
+#pragma unroll
+  for (uint32_t j = 0; j < KPT; j++) {
+    const uint32_t i = tid + j * NTT;
+    if (i < total) {
+      nx[i] = (uint16_t)yn[j];
+      lnd[i] = yt[j];
+    }
+  }
+  bsync();
+#pragma unroll 1
+  for (uint32_t round = 0; round < 10u; round++) {  // (hops < 2^9: each leaves a thread)
+    uint32_t chm = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++) {
+      const uint32_t i = tid + j * NTT;
+      if (i < total && nx[i] != JT_NONE) {
+        const uint32_t a = nx[i], b = nx[a];
+        yn[j] = b;
+        yt[j] = b == JT_NONE ? lnd[a] : 0u;
+        chm |= 1u << j;
+      }
+    }
+    const uint64_t any = __ballot(chm != 0);
+    if (lane == 0) S.fl[wid] = any != 0;
+    bsync();  // (this round's reads are done; flags visible)
+    uint32_t more = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NTT / WAVE; w++) more |= S.fl[w];
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; j++)
+      if ((chm >> j) & 1u) {
+        const uint32_t i = tid + j * NTT;
+        nx[i] = (uint16_t)yn[j];
+        if (yn[j] == JT_NONE) lnd[i] = yt[j];
+      }
+    bsync();  // (writes visible; flag reads done)
+    if (!more) break;
+  }
+  const uint64_t ix = t * NTT + tid;
+  eb_o = 0xFFu;
+  en_o = 0;
+  ecn_o = 0;
+  P.ent[ix] = 0xFF;
+  P.ent_n[ix] = 0;
+  P.ent_c[ix] = 0;
+  cl_o = 0;
+  if (tid == NTT - 1) {
+    uint64_t cl = C_ID;
+    if (G0 | G1) {
+      const uint32_t k = G0 ? (uint32_t)__builtin_ctzll(G0) : 64u + (uint32_t)__builtin_ctzll(G1);
+      const uint32_t s0 = gl[k] & 0xFFFFu;
+      const uint32_t code = nx[s0] == JT_NONE ? lnd[s0] : JT_C_ID;  // (settled: every next is JT_NONE)
+      if (code == JT_C_ID) cl = C_ID;
+      else if (code & JT_TERM) cl = MARK_TERM | (A + (code & ~JT_TERM));
+      else cl = A + code;
+    }
+    P.claim[t] = cl;
+    cl_o = cl;
+  }
+  return FC_OK;
+}
+
+// bits of the 64 positions from base (tile-relative) that lie in [lo, hi)
+__device__ __forceinline__ uint64_t range_bits(uint32_t base, uint32_t lo, uint32_t hi) {
+  const uint32_t a = lo > base ? min(lo - base, 64u) : 0u, z = hi > base ? min(hi - base, 64u) : 0u;
+  const uint64_t za = z >= 64u ? ~0ull : ((1ull << z) - 1ull), aa = a >= 64u ? ~0ull : ((1ull << a) - 1ull);
+  return za & ~aa;
+}
 
 // The fast claims of interior tile t: writes the per-thread records (P.ent*) and P.claim[t], and
 // returns this thread's record (eb, en, ecn) and, in thread NT - 1, the claim. FC_DENSE: more than
 // FCAP live positions (the tile went to the general kernel's work list; nothing written).
-template <bool CF>
+// EDGE: a stream-edge tile (the stream starts after A, or ends before A + IMG), run from
+// spec_claims' list: loads bounds-checked at the batch end, live positions only in [e0, se) (the
+// stream's exact entry on, its end before), the last 3 positions before se always listed and
+// every header whose 16-byte window crosses se parsed by the exact grammar (a header cut by the
+// stream end is a tail, as parse_win has it); FC_DENSE lists nothing (the caller goes on).
+template <bool CF, bool EDGE>
 __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const TileGeo &G, uint64_t t, FastLds &S,
                                                 uint32_t &eb_o, uint32_t &en_o, uint32_t &ecn_o, uint64_t &cl_o) {
 #if DRP_K1_GIMG
@@ -1246,9 +1422,12 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   uint32_t *hmx = S.hmx, *lnd = S.lnd, *xw = S.xw, *xf = S.xf, *wl = S.wl, *fl = S.fl;
   uint8_t *lal = S.lal;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  static_assert(!EDGE || DRP_K1_GIMG, "the edge form has no LDS image");
   // ---- stage, masks, live positions (varints of 1..3 bytes) --------------------------------
   uint4 v[SEGB / 16], hv;
-  {
+  if (EDGE) {
+    load_image(P, G, v, hv);  // (bounds-checked near the batch end)
+  } else {
     const uint4 *q = reinterpret_cast<const uint4 *>(P.bytes + G.A + (uint64_t)tid * SEGB);
 #pragma unroll
     for (int k = 0; k < (int)(SEGB / 16); k++) v[k] = q[k];
@@ -1281,7 +1460,15 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   const uint64_t X0 = ~M0 & ((S0 >> 1) | (S1 << 63));  // varint terminator followed by an id <= 2
   const uint64_t X1 = ~M1 & (S1 >> 1);
   const uint64_t Xs1 = (X0 >> 1) | (X1 << 63), Xs2 = (X0 >> 2) | (X1 << 62), Ms1 = (M0 >> 1) | (M1 << 63);
-  const uint64_t live = X0 | (M0 & (Xs1 | (Ms1 & Xs2)));
+  uint64_t live = X0 | (M0 & (Xs1 | (Ms1 & Xs2)));
+  // (edge tiles) the stream's positions [lo_rel, hi_rel) only; the last 3 before its end always
+  uint32_t lo_rel = 0, hi_rel = IMG, fo_rel = IMG;
+  if (EDGE) {
+    lo_rel = G.e0 > G.A ? (uint32_t)umin64(G.e0 - G.A, IMG) : 0u;
+    hi_rel = (uint32_t)umin64(G.se - G.A, IMG);
+    fo_rel = hi_rel < IMG ? max(lo_rel, hi_rel >= 3u ? hi_rel - 3u : 0u) : IMG;
+    live = (live & range_bits(tid * SEGB, lo_rel, hi_rel)) | range_bits(tid * SEGB, fo_rel, hi_rel);
+  }
 #if DRP_ABLATE_F == 1
   abl_sink(live);
   abl_out(P, t, 0);
@@ -1304,6 +1491,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     const uint64_t hX0 = ~hM0 & ((hS0 >> 1) | (hS1 << 63)), hX1 = ~hM1 & (hS1 >> 1);
     const uint64_t hXs1 = (hX0 >> 1) | (hX1 << 63), hXs2 = (hX0 >> 2) | (hX1 << 62), hMs1 = (hM0 >> 1) | (hM1 << 63);
     hlive = hX0 | (hM0 & (hXs1 | (hMs1 & hXs2)));
+    if (EDGE)
+      hlive = (hlive & range_bits(TILE + tid * SEGB, lo_rel, hi_rel)) | range_bits(TILE + tid * SEGB, fo_rel, hi_rel);
     if (tid == HV - 1) hlive &= (1ull << (SEGB - 16)) - 1ull;  // (the image's last 16 bytes: no lookahead)
   }
   // ---- the tile's (and halo's) live positions as an LDS list -----------------------------------
@@ -1320,7 +1509,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   const uint32_t ttotal = NT == 2 * WAVE ? xw[0] + xw[1] : xw[0];  // the tile's nodes
   const uint32_t total = ttotal + (DRP_HALO_NODES ? xw[2] : 0u);
   if (total > FCAP) {  // very dense tile: the general kernel's per-thread checks
-    push_work(P, t);
+    if (!EDGE) push_work(P, t);
     return FC_DENSE;
   }
 #if DRP_ABLATE_F == 11
@@ -1374,20 +1563,36 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     cfw[j] = 0;
     cff[j] = 0;
     if (i < total) {
-      const uint32_t o = lpos[i], d = o >> 2, sh = (o & 3u) * 8u;
-      const uint32_t a0 = w32[d], a1 = w32[d + 1], a2 = w32[d + 2];
-      const uint32_t w = __builtin_amdgcn_alignbit(a1, a0, sh), wn = __builtin_amdgcn_alignbit(a2, a1, sh);
-      const uint32_t tm = ~w & 0x808080u;  // live => a terminator in bytes 0..2
-      const uint32_t k = ((uint32_t)__builtin_ctz(tm | 0x80000000u) >> 3) + 1u;
-      const uint32_t L3 = (w & 0x7Fu) | ((w >> 1) & 0x3F80u) | ((w >> 2) & 0x1FC000u);
-      const uint32_t L = L3 & ((1u << (7u * k)) - 1u);
-      const uint32_t id = (w >> (8u * k)) & 0xFFu;
-      const uint32_t succ = o + k + (id ? L : 1u);
-      const uint32_t avail = se_rel - o;  // >= IMG - o
-      bool valid = id <= 2u && (id == 0u || L != 0u);
-      const bool tail = valid && id != 0u && L > avail - k;
+      const uint32_t o = lpos[i];
+      uint32_t w, wn, k, L, id, succ;
+      bool valid, tail, exact = false;
+      if (EDGE && o + 16u > se_rel) {  // (edge tiles) the window crosses the stream end: parse_win's grammar
+        const Hdr h = hdr_global(P.bytes, G.A + o, G.se);
+        exact = true;
+        tail = h.kind == H_TAIL_HDR || h.kind == H_TAIL_CHANGE || h.kind == H_TAIL_BLOB;
+        valid = h.kind == H_VALID || tail;
+        id = h.kind == H_TAIL_HDR ? 1u : h.id;  // (a cut header delivers nothing, as a cut change frame)
+        k = h.vlen;
+        L = (uint32_t)umin64(h.L, 0xFFFFFFFFull);
+        succ = h.kind == H_VALID ? (uint32_t)(h.succ - G.A) : o + 1u;
+        w = wn = 0;
+      } else {
+        const uint32_t d = o >> 2, sh = (o & 3u) * 8u;
+        const uint32_t a0 = w32[d], a1 = w32[d + 1], a2 = w32[d + 2];
+        w = __builtin_amdgcn_alignbit(a1, a0, sh);
+        wn = __builtin_amdgcn_alignbit(a2, a1, sh);
+        const uint32_t tm = ~w & 0x808080u;  // live => a terminator in bytes 0..2
+        k = ((uint32_t)__builtin_ctz(tm | 0x80000000u) >> 3) + 1u;
+        const uint32_t L3 = (w & 0x7Fu) | ((w >> 1) & 0x3F80u) | ((w >> 2) & 0x1FC000u);
+        L = L3 & ((1u << (7u * k)) - 1u);
+        id = (w >> (8u * k)) & 0xFFu;
+        succ = o + k + (id ? L : 1u);
+        const uint32_t avail = se_rel - o;  // >= IMG - o (interior); > 0 (edge: o < se)
+        valid = id <= 2u && (id == 0u || L != 0u);
+        tail = valid && id != 0u && L > avail - k;
+      }
       uint32_t c = NX_DEAD, a = 0;
-      if (valid && !tail && id == 1u && k >= 2u && succ <= IMG) {  // Change field tag first
+      if (valid && !tail && !exact && id == 1u && k >= 2u && succ <= IMG) {  // Change field tag first
         const uint32_t pb = k == 3u ? (wn & 0xFFu) : (w >> (8u * (k + 1u))) & 0xFFu;
         constexpr uint64_t TAGS = (1ull << 0x0a) | (1ull << 0x12) | (1ull << 0x18) | (1ull << 0x20) | (1ull << 0x28) |
                                   (1ull << 0x32);
@@ -1547,7 +1752,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   }
   uint32_t E = g;
   bool rs = false;
-  flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow, P.stats);
+  if (flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow, P.stats, DRP_FL_CAP))
+    return fast_claims_jump<NT>(P, t, G.A, S, g, ttotal, total, eb_o, en_o, ecn_o, cl_o);
 #if DRP_ABLATE_F == 5
   abl_sink(g, defer, R, n, E, rs, S0m, S1m, live, off);
   abl_out(P, t, 0);
@@ -1558,6 +1764,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   uint32_t need, js;  // a thread needs a restart; the last carrier + 1
   block_any_last(E == RX_NONE && defer && !any_above(S0m, S1m, tid), rx_node(E) && rx_off(E) < s1r, need, js, xf);
   bool moved = false;
+  if (P.stats && tid == 0 && need) atomicAdd(&P.stats[59], 1ull);  // (DRP_STATS: tiles with restarts)
 #pragma unroll 1
   for (uint32_t it = 0; need && it < 3; it++) {
     moved = true;
@@ -2864,23 +3071,6 @@ struct SegRange {
   uint64_t *seg_entry;          // [nseg + 1] exact entry of each segment (and the final exit)
 };
 
-__device__ __forceinline__ Hdr hdr_global(const uint8_t *g, uint64_t p, uint64_t se) {  // (as Img::at from HBM)
-  uint64_t w0, w1;
-  const uint64_t a = p & ~15ull;
-  const uint4 u = ld16(g, a, se), v = ld16(g, a + 16, se);
-  const uint64_t q0 = ((uint64_t)u.y << 32) | u.x, q1 = ((uint64_t)u.w << 32) | u.z;
-  const uint64_t q2 = ((uint64_t)v.y << 32) | v.x, q3 = ((uint64_t)v.w << 32) | v.z;
-  const uint32_t o = (uint32_t)(p & 15);
-  if (o < 8) {
-    w0 = funnel(q0, q1, 8 * o);
-    w1 = funnel(q1, q2, 8 * o);
-  } else {
-    w0 = funnel(q1, q2, 8 * (o - 8));
-    w1 = funnel(q2, q3, 8 * (o - 8));
-  }
-  return parse_win(w0, w1, p, se);
-}
-
 __device__ __forceinline__ TileGeo seg_geo(const DecodeParams &P, uint64_t s) {
   TileGeo G;
   G.s = s;
@@ -3211,6 +3401,8 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
   TileGeo G = seg_geo(P, R.s);
   const uint64_t ta = R.t0 + seg * R.G, tb = umin64(ta + R.G, R.tl), send = seg_end(G, R, seg);
   for (uint64_t i = tid; i < tb - ta; i += NT) lcl[i] = C_ID;
+  const uint64_t t_wg = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;  // (DRP_STATS)
+  uint64_t c_walk = 0, n_walk = 0, n_tiles = 0;
   uint64_t p = R.seg_entry[seg];
   if (tid == 0) nxt = (is_pos(p) && p < send) ? p : NONE;
   bsync();
@@ -3237,6 +3429,7 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
       const Img m{buf, P.bytes, G.A, G.se};
       const uint64_t lim = umin64(G.A + TILE, send);
       uint32_t ok = 1;
+      const uint64_t t_w = P.stats ? __builtin_amdgcn_s_memtime() : 0;
       p = q;
       // seg_advance, keeping the records of the chain's frames in this tile: positions rise, so
       // the current thread's record is kept in registers and written once when the chain leaves
@@ -3264,6 +3457,11 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
         cn += h.id != 0;
         cc += h.id == 1;
         p = h.succ;
+        if (P.stats) n_walk++;
+      }
+      if (P.stats) {
+        c_walk += __builtin_amdgcn_s_memtime() - t_w;
+        n_tiles++;
       }
       if (cth < NT) {
         re[cth] = (uint8_t)ce;
@@ -3285,6 +3483,12 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
     bsync();  // (the records are read before the next tile resets them)
   }
   for (uint64_t i = tid; i < tb - ta; i += NT) P.claim[ta + i] = lcl[i];
+  if (P.stats && tid == 0) {  // (DRP_STATS: walk cycles, frames walked, tiles, workgroup cycles)
+    atomicAdd(&P.stats[61], (unsigned long long)c_walk);
+    atomicAdd(&P.stats[62], (unsigned long long)n_walk);
+    atomicAdd(&P.stats[63], (unsigned long long)n_tiles);
+    atomicAdd(&P.stats[55], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_wg));
+  }
 }
 
 // payload bytes of the blob rows among rows [0, n) (a host batch's blob share: drp_api.hip

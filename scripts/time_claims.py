@@ -1,5 +1,6 @@
 """Decode C2 frames on the device a few times (for rocprofv3 kernel stats of ablated builds:
-their outputs are invalid by design). Usage: python scripts/time_claims.py [frames | c5]"""
+their outputs are invalid by design). Usage: python scripts/time_claims.py [frames | c5 | dense]
+(dense: 0.4 GB of the two-framing cascade stream, tests/_streams.shadow_stream_np)"""
 import os
 import sys
 
@@ -24,6 +25,11 @@ if arg == "c5":  # the C5 round trip's wire (1M Changes, 4 KB values), encoded o
         ectx.encode_device(cols, heap, n, foff, out, W + 64)
     torch.cuda.synchronize()
     wire = out[:W]
+elif arg == "dense":
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _streams as S  # noqa: E402
+    n = int(0.4e9) // 200
+    wire = torch.from_numpy(S.shadow_stream_np(n, period=200, shadow_at=20, small=4)).to(dev)
 else:
     n = int(arg)
     wire = bench.c2_on_device(n, seed=1234, dev=dev)

@@ -431,3 +431,64 @@ def test_stage_fetch_pieces_and_continuations(ctx):
     for cut in (3, 100, len(f) - 1):  # (1 or 2 bytes: the header itself is incomplete)
         g = ctx.decode_staged(wire + f[:cut])
         assert g["tail"] == 2 and g["frame_bytes"] == len(f) and g["consumed"] == len(wire), cut
+
+
+@pytest.mark.parametrize("shape", ["c2", "c5", "random"])
+def test_cut_streams_edge_tiles(shape):
+    """One wire cut into ~150 streams at arbitrary bytes (no cut on a frame boundary): every stream
+    enters mid-frame (its entry is the first frame start, as the JS carry passes it) and ends in a
+    cut frame, so nearly every first and last tile is a stream-edge tile, which spec_claims runs in
+    the fast claims form (DRP_EDGE_FAST) with the stream's bounds. Rows, counts and tails equal the
+    oracle's decode of each stream's bytes from its entry; no exact re-run."""
+    import ctypes as C
+
+    import sys
+
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from _gpu import drp_amd
+    dev = torch.device("cuda", 0)
+    rng = random.Random(404)
+    wire = {"c2": lambda: S.c2_stream(60_000, seed=6).tobytes(),
+            "c5": lambda: S.c5_stream(rng, 1200),
+            "random": lambda: S.random_stream(rng, 20_000, blob_p=0.02, blob_max=20000)}[shape]()
+    whole = O.decode_batch(wire)
+    assert whole["err_code"] == 0
+    ends = whole["payload_off"].astype(np.int64) + whole["payload_len"].astype(np.int64)
+    starts = np.concatenate([[0], ends[:-1]])  # frame k starts where frame k - 1's payload ends
+    cuts = sorted(rng.sample(range(1, len(wire)), 149))
+    cuts = [0] + [c for c in cuts if int(np.searchsorted(starts, c, "left")) < len(starts) and
+                  starts[np.searchsorted(starts, c, "left")] != c] + [len(wire)]
+    cuts = sorted(set(cuts))
+    entry = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        j = int(np.searchsorted(starts, a, "left"))
+        entry.append(min(int(starts[j]) if j < len(starts) else b, b) - a)
+    ns = len(cuts) - 1
+    cap = len(starts) + 64
+    outs = bench.alloc_outputs(cap, dev)
+    res = torch.zeros(ns * C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+    w = torch.from_numpy(np.frombuffer(wire, np.uint8).copy()).to(dev)
+    so = torch.tensor(cuts, dtype=torch.int64, device=dev)
+    en = torch.tensor(entry, dtype=torch.int64, device=dev)
+    with drp_amd.Ctx(0) as ctx:
+        for _ in range(2):  # (the second decode with the long-frame check chosen from the first)
+            ctx.decode_device(w, so, en, outs, cap, res)
+            torch.cuda.synchronize()
+            t = ctx.timing()
+            print(f"{shape}: {ns} streams, repairs {t.spec_repairs}, relisted {t.verify_relisted}, "
+                  f"seg {t.seg_repairs}, exact {t.strict_reruns}")
+            assert t.strict_reruns == 0
+            rs = (drp_amd.StreamResult * ns).from_buffer_copy(res.cpu().numpy().tobytes())
+            off = outs["payload_off"].cpu().numpy()
+            ln = outs["payload_len"].cpu().numpy()
+            ty = outs["type"].cpu().numpy()
+            for s, (a, b) in enumerate(zip(cuts[:-1], cuts[1:])):
+                e = a + entry[s]
+                r = O.decode_batch(wire[e:b])
+                f0, nf = rs[s].frame_begin, rs[s].frames
+                assert (nf, rs[s].err_code, rs[s].tail_kind) == (r["nframes"], r["err_code"], r["tail"]), (s, a, b)
+                np.testing.assert_array_equal(off[f0:f0 + nf], r["payload_off"].astype(np.int64) + e)
+                np.testing.assert_array_equal(ln[f0:f0 + nf], r["payload_len"])
+                np.testing.assert_array_equal(ty[f0:f0 + nf], r["type"])
