@@ -142,6 +142,7 @@ struct drp_ctx {
   // kernel counters and per-tile traces into dstats (allocated here when asked for)
   uint32_t kstrong_hbm = 0;
   uint32_t cascade_min = 4096;  // DRP_CASCADE_MIN (tests: small cascades)
+  int64_t jump_min = -1;        // DRP_JUMP_MIN (-1: max(64, tiles / 512))
   uint64_t dirty_cap = ~0ull;
   bool stats = false;
   const char *trace_file = nullptr;
@@ -224,6 +225,7 @@ int drp_open(int device, drp_ctx **out) {
   }
   if (const char *e = getenv("DRP_KSTRONG_HBM")) c->kstrong_hbm = (uint32_t)atoi(e);
   if (const char *e = getenv("DRP_CASCADE_MIN")) c->cascade_min = (uint32_t)strtoul(e, nullptr, 10);
+  if (const char *e = getenv("DRP_JUMP_MIN")) c->jump_min = strtoll(e, nullptr, 10);
   if (const char *e = getenv("DRP_DIRTY_CAP")) c->dirty_cap = strtoull(e, nullptr, 10);
   c->trace_file = getenv("DRP_TRACE_FILE");
   if (getenv("DRP_STATS") && hipMalloc((void **)&c->dstats, 64 * 8) == hipSuccess) c->stats = true;
@@ -647,6 +649,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.change_checks = (uint32_t)c->change_checks;
   P.kstrong_hbm = c->kstrong_hbm;  // (tests: weaker predictions)
   P.cascade_min = c->cascade_min;
+  P.jump_min = c->jump_min >= 0 ? (uint32_t)c->jump_min : (uint32_t)std::max<uint64_t>(64, NT / 512);
   P.dlist_cap = std::min<uint64_t>(NT, c->dirty_cap);  // (tests: DRP_DIRTY_CAP)
   unsigned long long *dstats = c->stats ? c->dstats : nullptr;
   if (dstats) P.stats = dstats;

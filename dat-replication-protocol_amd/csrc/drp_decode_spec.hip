@@ -1752,8 +1752,21 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   }
   uint32_t E = g;
   bool rs = false;
-  if (flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow, P.stats, DRP_FL_CAP))
-    return fast_claims_jump<NT>(P, t, G.A, S, g, ttotal, total, eb_o, en_o, ecn_o, cl_o);
+  if (flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow, P.stats, DRP_FL_CAP)) {
+    // the rounds did not settle: past P.jump_min such tiles in this launch (an input with a second
+    // framing throughout: every tile), pointer jumping; before it (clean streams have a few, whose
+    // predictions rely on the restarts and rule 3 below), the rounds go on
+    // (an atomic only below the threshold: one word takes ~88 atomics per us, and on a cascade
+    // every tile gets here)
+    if (tid == 0) {
+      uint32_t c = __hip_atomic_load(&P.counter[12], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (c < P.jump_min) c = atomicAdd(&P.counter[12], 1u);
+      xw[6] = c;
+    }
+    bsync();
+    if (xw[6] >= P.jump_min) return fast_claims_jump<NT>(P, t, G.A, S, g, ttotal, total, eb_o, en_o, ecn_o, cl_o);
+    flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow, P.stats);
+  }
 #if DRP_ABLATE_F == 5
   abl_sink(g, defer, R, n, E, rs, S0m, S1m, live, off);
   abl_out(P, t, 0);
@@ -1946,11 +1959,18 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
     multi |= shfl_xor32(multi, d);
   }
   const bool miss = !inside && !bogus && claim != C_ID && claim != et;
-  if (r != 0) return;
-  if (!found || bad || bogus || miss || (inside && claim == C_ID)) {
-    P.vlist[atomicAdd(P.vlist_n, 1u)] = (uint32_t)t;  // verify_counts decides this tile
-    return;
+  // verify_counts decides the tiles listed here; one atomic per wave (a cascade lists every tile,
+  // and one counter word takes ~88 atomics per us: 207K single appends cost 0.3 ms)
+  const bool lst = r == 0 && (!found || bad || bogus || miss || (inside && claim == C_ID));
+  const uint64_t lm = __ballot(lst);
+  if (lm) {
+    const uint32_t lane = threadIdx.x & 63u, ld = (uint32_t)__builtin_ctzll(lm);
+    uint32_t base = 0;
+    if (lane == ld) base = atomicAdd(P.vlist_n, (uint32_t)__builtin_popcountll(lm));
+    base = (uint32_t)__shfl((int)base, (int)ld, WAVE);
+    if (lst) P.vlist[base + (uint32_t)__builtin_popcountll(lm & ((1ull << lane) - 1ull))] = (uint32_t)t;
   }
+  if (r != 0 || lst) return;
   P.tile_exit[t] = inside ? claim : et;
   P.tile_count[t] = sf;
   P.tile_nch[t] = sc;
@@ -3390,6 +3410,9 @@ __global__ __launch_bounds__(SEG_STB) void seg_stitch(DecodeParams P, SegRange R
 // the verify pass after the repair proves such a tile from its records alone (verify_lite) instead
 // of re-walking it; a tile where the chain ends (an error or a frame cut by the stream end) keeps
 // its records and is re-walked by verify_counts.
+#ifndef DRP_SEGC_LEAN
+#define DRP_SEGC_LEAN 1  // 0: the chain walk by hdr_fast only (A/B)
+#endif
 __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint64_t lcl[SEG_GMAX];
@@ -3435,14 +3458,55 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
       // the current thread's record is kept in registers and written once when the chain leaves
       // its bytes (LDS writes only: no read-modify-write on the walk's serial path)
       uint32_t cth = NT, ce = 0, cn = 0, cc = 0;
-      while (is_pos(p) && p < lim && p < m.se) {
-        const Hdr h = hdr_fast(m, p);
-        if (h.kind != H_VALID) {
-          p = term_of(h, p);
-          ok = 0;
-          break;
+#if DRP_SEGC_LEAN
+      // 32-bit tile-relative steps while the header's 16-byte window lies in the image and the
+      // stream and its varint has 1..3 bytes (hdr_fast's grammar); any other header takes hdr_fast.
+      // The walk is one lane's (the compiler keeps it in scalar registers), so the step is written
+      // without data-dependent branches: the conditions are combined with & and the records are
+      // stored on every frame (the last store of a thread's record is its final value)
+      {
+        const uint32_t lr = (uint32_t)(lim - G.A);  // (q is in [A, lim))
+        const uint32_t wr = (uint32_t)umin64(G.se - G.A, IMG), sr = (uint32_t)umin64(G.se - G.A, 0x7FFFFFFFull);
+        uint32_t o = (uint32_t)(p - G.A);
+        bool term = false, far = false;
+        while (o < lr) {
+          const uint32_t *qw = reinterpret_cast<const uint32_t *>(buf) + (o >> 2);  // (o < TILE: inside buf)
+          const uint32_t w = __builtin_amdgcn_alignbit(qw[1], qw[0], (o & 3u) * 8u);
+          const uint32_t tm = ~w & 0x808080u;
+          const uint32_t k = ((uint32_t)__builtin_ctz(tm | 0x80000000u) >> 3) + 1u;
+          const uint32_t L = ((w & 0x7Fu) | ((w >> 1) & 0x3F80u) | ((w >> 2) & 0x1FC000u)) & ((1u << (7u * k)) - 1u);
+          uint32_t id = (w >> (8u * (k & 3u))) & 0xFFu;
+          const bool fast = (o + 16u <= wr) & (tm != 0u) & (id < 3u) & ((id == 0u) | ((L != 0u) & (L <= sr - o - k)));
+          uint32_t no = o + k + (id ? L : 1u);
+          if (__builtin_expect(!fast, 0)) {
+            const Hdr h = hdr_fast(m, G.A + o);
+            if (h.kind != H_VALID) {
+              p = term_of(h, G.A + o);
+              ok = 0;
+              term = true;
+              break;
+            }
+            id = h.id;
+            far = h.succ >= lim;
+            p = h.succ;
+            no = far ? lr : (uint32_t)(h.succ - G.A);
+          }
+          const uint32_t th = o / SEGB;
+          const bool nw = th != cth;
+          ce = nw ? o % SEGB : ce;
+          cn = (nw ? 0u : cn) + (id != 0u);
+          cc = (nw ? 0u : cc) + (id == 1u);
+          cth = th;
+          re[th] = (uint8_t)ce;
+          rn[th] = (uint8_t)cn;
+          rc[th] = (uint8_t)cc;
+          o = no;
         }
-        const uint32_t o = (uint32_t)(p - G.A), th = o / SEGB;
+        if (!term && !far) p = G.A + o;
+      }
+#else
+      auto note = [&](uint32_t o, uint32_t id) {  // (the frame at tile offset o)
+        const uint32_t th = o / SEGB;
         if (th != cth) {
           if (cth < NT) {
             re[cth] = (uint8_t)ce;
@@ -3454,11 +3518,21 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
           cn = 0;
           cc = 0;
         }
-        cn += h.id != 0;
-        cc += h.id == 1;
-        p = h.succ;
+        cn += id != 0;
+        cc += id == 1;
         if (P.stats) n_walk++;
+      };
+      while (is_pos(p) && p < lim && p < m.se) {
+        const Hdr h = hdr_fast(m, p);
+        if (h.kind != H_VALID) {
+          p = term_of(h, p);
+          ok = 0;
+          break;
+        }
+        note((uint32_t)(p - G.A), h.id);
+        p = h.succ;
       }
+#endif
       if (P.stats) {
         c_walk += __builtin_amdgcn_s_memtime() - t_w;
         n_tiles++;

@@ -72,6 +72,8 @@ struct DecodeParams {
   uint32_t change_checks;  // 1: claims_fast checks long frames' Change structure (drp_api.hip picks)
   int kstrong_hbm;      // 0: DRP_KSTRONG_HBM; else frames a deferred candidate must survive (tests)
   uint32_t cascade_min;  // listed tiles that make the head's verify a cascade (drp_decode_spec.hip)
+  uint32_t jump_min;     // claims tiles whose link rounds hit DRP_FL_CAP before the rest take the
+                         // pointer-jumping form (counted in counter[12]; drp_decode_spec.hip)
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
   unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
 };

@@ -98,9 +98,10 @@ def test_error_early_settles(ctx, at):
     assert t.strict_reruns == 0, "fell back to the exact kernel"
 
 
-def test_cascade_512mb_under_5ms(ctx):
+def test_cascade_512mb_under_2_5ms(ctx):
     """A 512 MiB shadow stream (long random-payload frames: the exact kernel's slow case) decodes
-    on the device path in <= 5 ms (measured 2.0-2.1 ms, round 4), with the frame table checked against the generator."""
+    on the device path in <= 2.5 ms (measured 1.5 ms, end of round 4: ~1.6x), with the frame table checked
+    against the generator."""
     import ctypes as C
 
     import torch
@@ -131,7 +132,7 @@ def test_cascade_512mb_under_5ms(ctx):
     off = outs["payload_off"][:n].cpu().numpy()
     np.testing.assert_array_equal(off, np.arange(n, dtype=np.int64) * period + hdr)
     assert (outs["type"][:n].cpu().numpy() == 2).all()
-    assert best <= 0.005, f"{best * 1e3:.1f} ms"
+    assert best <= 0.0025, f"{best * 1e3:.1f} ms"
 
 
 def test_dense_cascade_1_7gb(ctx):
@@ -172,7 +173,7 @@ def test_dense_cascade_1_7gb(ctx):
     assert bool((outs["payload_len"][:n] == period - hdr).all()) and bool((outs["type"][:n] == 2).all())
     r = drp_amd.StreamResult.from_buffer_copy(res.cpu().numpy().tobytes())
     assert (r.frames, r.blobs, r.err_code, r.tail_kind) == (n, n, 0, 0)
-    assert best <= 0.012, f"{best * 1e3:.1f} ms (measured 7.9-8.1 ms, round 4)"
+    assert best <= 0.0095, f"{best * 1e3:.1f} ms (measured 6.2-6.4 ms, end of round 4: ~1.5x)"
     del w, outs
     torch.cuda.empty_cache()
 
