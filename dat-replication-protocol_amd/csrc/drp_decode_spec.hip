@@ -2152,6 +2152,14 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   }
   PHASE(10);
   if (tid == NT - 1) {
+    // the stream's last tile: no later tile takes its claim as its entry (the next stream starts at
+    // its own e0), so a miss there rewrites its claim in place instead of asking for a pass (a
+    // stream cut mid-frame can end in a chain too short to be strong before its tail: the
+    // prediction leaves that tile unclaimed). A later repair that changes its entry relists it.
+    if (miss && t + 1 == P.tile_prefix[G.s + 1]) {
+      P.claim[t] = inside ? exit_t : C_ID;
+      miss = false;
+    }
     if (miss) {
       atomicOr(P.overflow, F_MISS);
       // repair: the claim becomes the exit of the chain from this pass's entry. The first
