@@ -2950,23 +2950,38 @@ struct LeanLds {
   __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   uint32_t wsum[NT / WAVE];
   uint32_t defer;
+  uint64_t todo;  // (long-frame form) the workgroup's tiles that are not sparse
 };
 __device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t, LeanLds &L);
 
 // Long-frame streams (the context's change_checks form: >= 512 B per frame) leave nearly every
 // tile to emit_sparse, so a workgroup per tile would mostly be dispatched to exit: there each
-// workgroup takes EMIT_LONG_TPW tiles, strided by the grid (drp_launch_spec_tail sizes it).
-constexpr uint32_t EMIT_LONG_TPW = 8;
+// workgroup takes EMIT_LONG_TPW tiles, strided by the grid (drp_launch_spec_tail sizes it), reads
+// their sparse marks in one load (a lane each) and runs only the others (8 tiles with a load each
+// in turn: C5's emit_lean took 0.116 ms of dependent mark loads).
+constexpr uint32_t EMIT_LONG_TPW = 32;
+static_assert(EMIT_LONG_TPW <= WAVE, "one lane per tile's mark");
 __global__ __launch_bounds__(NT, DRP_EMIT_LEAN_WAVES) void emit_lean(DecodeParams P) {
   __shared__ LeanLds L;
   if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
   if (P.change_checks) {
     const uint64_t ntiles = P.tile_prefix[P.nstreams];
-    for (uint32_t j = 0; j < EMIT_LONG_TPW; j++) {
-      const uint64_t t = blockIdx.x + (uint64_t)j * gridDim.x;
-      if (t >= ntiles) break;  // (uniform)
-      if (j) bsync();          // (the last tile's LDS reads are done)
-      emit_lean_tile(P, t, L);
+    const uint32_t tid = threadIdx.x;
+    if (tid < WAVE) {
+      const uint64_t t = blockIdx.x + (uint64_t)tid * gridDim.x;
+      const bool run = tid < EMIT_LONG_TPW && t < ntiles && !(P.tile_sparse && P.tile_sparse[t]);
+      const uint64_t m = __ballot(run);
+      if (tid == 0) L.todo = m;
+    }
+    bsync();
+    uint64_t todo = L.todo;
+    bool first = true;
+    while (todo) {  // (uniform)
+      const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+      todo &= todo - 1;
+      if (!first) bsync();  // (the last tile's LDS reads are done)
+      first = false;
+      emit_lean_tile(P, blockIdx.x + (uint64_t)j * gridDim.x, L);
     }
     return;
   }
