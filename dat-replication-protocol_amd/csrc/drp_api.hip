@@ -320,7 +320,8 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.tk = o; o += al(L.ntiles_max);             // first entry thread per tile (verify_lite)
   L.tsp = o; o += al(L.ntiles_max);            // sparse-tile marks (verify_lite -> emit_sparse)
   L.fmiss = o; o += al(ns * 8);                  // first missed tile per stream (verify)
-  L.segw = o; o += al((2 * 64 * 8192 + 8193) * 8);  // segmented repair: candidates + entries (SEG_NMAX)
+  L.segw = o; o += al((2 * 64 * 8192 + 8194) * 8 + 64 * 8192);  // segmented repair: candidates, entries,
+                                                                // next-candidate tables (SEG_NMAX)
   L.scan_tmp = o; o += al((L.ntiles_max / 4096 + 2) * 8);  // tile scans: block sums
   L.total = o;
   return L;

@@ -3112,6 +3112,7 @@ struct SegRange {
   uint64_t tend;                // the stream's tile end (tl < tend: the range was clamped)
   uint64_t *cand;               // per segment: 64 starts, then 64 exits
   uint64_t *seg_entry;          // [nseg + 1] exact entry of each segment (and the final exit)
+  uint8_t *nidx;                // [nseg][64] seg_link: the next segment's candidate each exit is
 };
 
 __device__ __forceinline__ TileGeo seg_geo(const DecodeParams &P, uint64_t s) {
@@ -3376,14 +3377,106 @@ __global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
   }
 }
 
+// seg_link: for every candidate of segment s, the index of its exit among segment s + 1's candidate
+// starts (0xFF: none, or the chain ends or passes over s + 1), so the stitch can follow the chain by
+// table lookups instead of a ballot per segment. One wave per segment.
+__global__ __launch_bounds__(WAVE) void seg_link(DecodeParams P, SegRange R) {
+  __shared__ uint64_t st[SEG_CAND];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t s = blockIdx.x;
+  uint32_t f = 0xFFu;
+  if (s + 1 < R.nseg) {
+    const TileGeo G = seg_geo(P, R.s);
+    const uint64_t send = seg_end(G, R, s + 1);
+    const uint64_t ex = R.cand[s * 2 * SEG_CAND + SEG_CAND + lane];
+    st[lane] = R.cand[(s + 1) * 2 * SEG_CAND + lane];
+    __syncthreads();
+    if (is_pos(ex) && ex < send)
+      for (uint32_t j = 0; j < SEG_CAND; j++)
+        if (st[j] == ex) {
+          f = j;
+          break;
+        }
+  }
+  R.nidx[s * SEG_CAND + lane] = (uint8_t)f;
+}
+
 // The candidate tables of SEG_SB segments at a time are staged in LDS by the whole workgroup
 // (double-buffered: the next block loads while wave 0 follows the chain through this one), so
 // the serial part is a ballot per segment on LDS data.
+// Up to SEG_FAST segments, the chain is followed through seg_link's tables first, in parallel: the
+// tables (64 B per segment) go to LDS; each (block of 64 segments, entry candidate) pair is followed
+// through its block (all 64 x 32 of them at once), one thread chains the blocks' end maps, each
+// block then follows its now-known entry, and the entries are written in parallel. Any segment
+// whose entry is not one of its candidates (0xFF on the path) sends the whole range to the serial
+// stitch below (1.7 GB dense cascade: 0.47 ms serially, ~0.02 by the tables).
 constexpr uint32_t SEG_SB = 64, SEG_STB = 1024;  // segments per staged block, threads
+constexpr uint32_t SEG_FAST = 2048, SEG_FB = SEG_FAST / SEG_SB;  // (blocks of 64 segments)
+constexpr uint32_t SEG_SMEM_SERIAL = 2 * SEG_SB * 2 * SEG_CAND * 8;  // the serial stitch's tables (128 KB)
+constexpr uint32_t SEG_SMEM_FAST = SEG_FAST * SEG_CAND + SEG_FB * SEG_CAND + SEG_FB + SEG_FAST;
+constexpr uint32_t SEG_SMEM = SEG_SMEM_SERIAL > SEG_SMEM_FAST ? SEG_SMEM_SERIAL : SEG_SMEM_FAST;
+static_assert(SEG_SMEM + 64 <= 160 * 1024, "seg_stitch LDS");
 __global__ __launch_bounds__(SEG_STB) void seg_stitch(DecodeParams P, SegRange R) {
-  __shared__ uint64_t tab[2][SEG_SB][2 * SEG_CAND];  // 2 x 64 KB
+  __shared__ __attribute__((aligned(16))) uint8_t smem[SEG_SMEM];
+  __shared__ uint32_t bad, idx0;
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const TileGeo G = seg_geo(P, R.s);
+  if (R.nidx && R.nseg <= SEG_FAST) {
+    const uint32_t ns = (uint32_t)R.nseg, nb = (ns + SEG_SB - 1) / SEG_SB;
+    uint8_t *nx = smem;                            // [ns][64]
+    uint8_t *bend = smem + SEG_FAST * SEG_CAND;    // [nb][64]: block start candidate -> next block's
+    uint8_t *bst = bend + SEG_FB * SEG_CAND;       // [nb]: the chain's candidate at each block start
+    uint8_t *sidx = bst + SEG_FB;                  // [ns]: the chain's candidate in each segment
+    for (uint32_t i = tid; i < ns * SEG_CAND / 16; i += SEG_STB)
+      reinterpret_cast<uint4 *>(nx)[i] = reinterpret_cast<const uint4 *>(R.nidx)[i];
+    if (tid < WAVE) {  // segment 0's entry among its candidates
+      const uint64_t e0 = R.seg_entry[0];
+      const uint64_t hit = __ballot(R.cand[lane] == e0);
+      if (tid == 0) {
+        bad = !(is_pos(e0) && e0 < seg_end(G, R, 0) && hit);
+        idx0 = hit ? (uint32_t)__builtin_ctzll(hit) : 0xFFu;
+      }
+    }
+    __syncthreads();
+    for (uint32_t p = tid; p < nb * SEG_CAND; p += SEG_STB) {  // each block's end map
+      const uint32_t b = p / SEG_CAND, s1 = min(b * SEG_SB + SEG_SB, ns - 1);
+      uint32_t x = p % SEG_CAND;
+      for (uint32_t s = b * SEG_SB; s < s1 && x != 0xFFu; s++) x = nx[s * SEG_CAND + x];
+      bend[p] = (uint8_t)x;
+    }
+    __syncthreads();
+    if (tid == 0) {  // the blocks' entries, in order
+      uint32_t x = bad ? 0xFFu : idx0;
+      for (uint32_t b = 0; b < nb; b++) {
+        bst[b] = (uint8_t)x;
+        if (x != 0xFFu) x = bend[b * SEG_CAND + x];
+      }
+    }
+    __syncthreads();
+    if (tid < nb) {  // each block from its entry
+      const uint32_t s0 = tid * SEG_SB, s1 = min(s0 + SEG_SB, ns);
+      uint32_t x = bst[tid];
+      for (uint32_t s = s0; s < s1; s++) {
+        sidx[s] = (uint8_t)x;
+        if (x == 0xFFu) {
+          bad = 1;
+          break;
+        }
+        if (s + 1 < ns) x = nx[s * SEG_CAND + x];
+      }
+    }
+    __syncthreads();
+    if (!bad) {
+      for (uint32_t s = tid; s < ns; s += SEG_STB) {
+        const uint32_t x = sidx[s];
+        R.seg_entry[s] = R.cand[(uint64_t)s * 2 * SEG_CAND + x];
+        if (s == ns - 1) R.seg_entry[ns] = R.cand[(uint64_t)s * 2 * SEG_CAND + SEG_CAND + x];
+      }
+      return;
+    }
+    __syncthreads();  // (the serial stitch reuses the LDS)
+  }
+  auto tab = reinterpret_cast<uint64_t (*)[SEG_SB][2 * SEG_CAND]>(smem);  // [2][SEG_SB][128]: 2 x 64 KB
   constexpr uint32_t W = SEG_SB * 2 * SEG_CAND;  // words per block
   // threads [t0, SEG_STB) copy block blk into buffer buf
   auto load = [&](uint64_t blk, uint32_t buf, uint32_t t0) {
@@ -3484,15 +3577,18 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
 #if DRP_SEGC_LEAN
       // 32-bit tile-relative steps while the header's 16-byte window lies in the image and the
       // stream and its varint has 1..3 bytes (hdr_fast's grammar); any other header takes hdr_fast.
-      // The walk is one lane's (the compiler keeps it in scalar registers), so the step is written
-      // without data-dependent branches: the conditions are combined with & and the records are
-      // stored on every frame (the last store of a thread's record is its final value)
+      // The step is written without data-dependent branches: the conditions are combined with &
+      // and the records are stored on every frame (the last store of a thread's record is its
+      // final value)
       {
         const uint32_t lr = (uint32_t)(lim - G.A);  // (q is in [A, lim))
         const uint32_t wr = (uint32_t)umin64(G.se - G.A, IMG), sr = (uint32_t)umin64(G.se - G.A, 0x7FFFFFFFull);
         uint32_t o = (uint32_t)(p - G.A);
         bool term = false, far = false;
         while (o < lr) {
+          // (o in a vector register: otherwise the compiler moves this one-lane walk to the scalar
+          // unit, which the CU's ~8 walking workgroups share: ~800 cycles per frame)
+          asm volatile("" : "+v"(o));
           const uint32_t *qw = reinterpret_cast<const uint32_t *>(buf) + (o >> 2);  // (o < TILE: inside buf)
           const uint32_t w = __builtin_amdgcn_alignbit(qw[1], qw[0], (o & 3u) * 8u);
           const uint32_t tm = ~w & 0x808080u;
@@ -3861,6 +3957,9 @@ extern "C" hipError_t drp_launch_blob_bytes(const uint8_t *type, const uint32_t 
 
 // Segmented repair of stream s from tile t0 (its first missed tile) to its end (the caller then
 // runs a verify pass). scratch: 2 * 64 * SEG_NMAX + SEG_NMAX + 1 words.
+#ifndef DRP_SEG_LINK
+#define DRP_SEG_LINK 1  // 0: the serial stitch only (A/B)
+#endif
 extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, uint64_t t0, uint64_t tl,
                                             uint64_t *scratch, hipStream_t st) {
   if (tl <= t0) return hipSuccess;
@@ -3881,8 +3980,10 @@ extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, u
   R.nseg = (n + R.G - 1) / R.G;
   R.cand = scratch;
   R.seg_entry = scratch + 2 * spec::SEG_CAND * spec::SEG_NMAX;
+  R.nidx = DRP_SEG_LINK ? reinterpret_cast<uint8_t *>(R.seg_entry + spec::SEG_NMAX + 2) : nullptr;  // (SEG_NMAX x 64 B, 16-B aligned)
   DecodeParams Q = *P;
   hipLaunchKernelGGL(spec::seg_walk, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);
+  if (R.nidx) hipLaunchKernelGGL(spec::seg_link, dim3((uint32_t)R.nseg), dim3(WAVE), 0, st, Q, R);
   hipLaunchKernelGGL(spec::seg_stitch, dim3(1), dim3(spec::SEG_STB), 0, st, Q, R);
   hipLaunchKernelGGL(spec::seg_claims, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);
   return hipGetLastError();
