@@ -147,6 +147,8 @@ struct drp_ctx {
   bool stats = false;
   const char *trace_file = nullptr;
   unsigned long long *dstats = nullptr;
+  uint32_t *ctile = nullptr;  // segmented repair: per-tile candidate positions (grown on demand)
+  uint64_t ctile_cap = 0;
   DecodeParams lastP = {};  // the last speculative decode's parameters (measurement hooks)
   uint64_t lastNT = 0;
   uint32_t *lastTS = nullptr;  // its tile -> stream map
@@ -243,6 +245,7 @@ void drp_close(drp_ctx *c) {
   c->aux.release();
   c->dec_cols.release();
   if (c->dstats) (void)hipFree(c->dstats);
+  if (c->ctile) (void)hipFree(c->ctile);
   for (auto &e : c->ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->st);
   delete c;
@@ -320,8 +323,8 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.tk = o; o += al(L.ntiles_max);             // first entry thread per tile (verify_lite)
   L.tsp = o; o += al(L.ntiles_max);            // sparse-tile marks (verify_lite -> emit_sparse)
   L.fmiss = o; o += al(ns * 8);                  // first missed tile per stream (verify)
-  L.segw = o; o += al((2 * 64 * 8192 + 8194) * 8 + 64 * 8192);  // segmented repair: candidates, entries,
-                                                                // next-candidate tables (SEG_NMAX)
+  L.segw = o; o += al((2 * 64 * 8192 + 8194) * 8 + 65 * 8192);  // segmented repair: candidates, entries,
+                                                                // next-candidate tables, lanes (SEG_NMAX)
   L.scan_tmp = o; o += al((L.ntiles_max / 4096 + 2) * 8);  // tile scans: block sums
   L.total = o;
   return L;
@@ -724,7 +727,18 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
           if (fm[s] != ~0ull) {
             TRACE("decode_spec: segmented repair of stream %llu from tile %llu to %llu", (unsigned long long)s,
                   (unsigned long long)fm[s], (unsigned long long)tp[s + 1]);
-            CHK(drp_launch_seg_repair(&P, s, fm[s], tp[s + 1], c->scratch.at<uint64_t>(L.segw), st));
+            // the parallel seg_claims' per-tile candidate positions (256 B per tile of the range),
+            // allocated on the first segmented repair that needs more
+            const uint64_t need = std::min<uint64_t>(tp[s + 1] - fm[s], 8192ull * 1024) * 64;
+            if (need > c->ctile_cap) {
+              if (c->ctile) (void)hipFree(c->ctile);
+              c->ctile = nullptr;
+              c->ctile_cap = 0;
+              if (hipMalloc((void **)&c->ctile, need * 4) == hipSuccess) c->ctile_cap = need;
+              else (void)hipGetLastError();
+            }
+            CHK(drp_launch_seg_repair(&P, s, fm[s], tp[s + 1], c->scratch.at<uint64_t>(L.segw), c->ctile, c->ctile_cap,
+                                      st));
             c->timing.seg_repairs++;
             full = true;  // (claims rewritten over a range)
           }

@@ -3100,6 +3100,7 @@ __device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t
 // A verify pass then proves the new claims as usual. Cost: two streaming passes over the range
 // spread over the CUs plus a short serial stitch, however the predictions failed.
 constexpr uint32_t SEG_CAND = 64, SEG_GMAX = 1024;  // candidates per segment, tiles per segment (max)
+constexpr uint32_t CT_SKIP = 0xFFFFFFFFu, CT_END = 0xFFFFFFFEu, CT_PAST = 0xFFFFFFFDu;  // (ctile markers)
 static_assert((uint64_t)SEG_GMAX * TILE < (1ull << 32), "seg_walk: 32-bit offsets in a segment");
 constexpr uint64_t SEG_NMAX = 8192;  // segments per repair (max)
 #ifndef DRP_SEG_NTARGET
@@ -3113,6 +3114,9 @@ struct SegRange {
   uint64_t *cand;               // per segment: 64 starts, then 64 exits
   uint64_t *seg_entry;          // [nseg + 1] exact entry of each segment (and the final exit)
   uint8_t *nidx;                // [nseg][64] seg_link: the next segment's candidate each exit is
+  uint8_t *seg_lane;            // [nseg] seg_stitch: the candidate that is the exact chain (0xFF: serial)
+  uint32_t *ctile;              // [tiles of the range][64] seg_walk: each candidate's position entering
+                                // each walked tile, from the segment start (CT_* markers), or null
 };
 
 __device__ __forceinline__ TileGeo seg_geo(const DecodeParams &P, uint64_t s) {
@@ -3334,6 +3338,10 @@ __global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
     cpos[idx] = lb + (uint32_t)__builtin_ctzll(bits);
   bsync();
   uint64_t pos = (wid == 0 && lane < nc) ? cpos[lane] : NONE, start = pos;
+  const uint64_t sb0 = seg_tile_a(G, ta);
+  if (R.ctile)  // (tiles no chain is in stay CT_SKIP)
+    for (uint64_t i = tid; i < (umin64(ta + R.G, R.tl) - ta) * SEG_CAND; i += NT)
+      R.ctile[(ta - R.t0) * SEG_CAND + i] = CT_SKIP;
   // walk: the lanes' chains through the segment, tile by tile (a tile only when a chain is in it);
   // the next tile is fetched into registers while wave 0 walks this one (the chains usually go on
   // there), so its load latency is not on the segment's serial path
@@ -3347,6 +3355,9 @@ __global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
     // (the image of the tile staged last) The walk is by table while the last tile's longest chain
     // took more than SW_STEPS headers (dense chains), frame by frame otherwise.
     uint32_t steps = 0;
+    if (R.ctile && wid == 0)  // (each candidate's position entering this tile, for seg_claims_par)
+      R.ctile[((G.A - sb0) / TILE + ta - R.t0) * SEG_CAND + lane] =
+          !is_pos(pos) ? CT_END : (pos >= send ? CT_PAST : (uint32_t)(pos - sb0));
     if (DRP_SEG_TABLE && table) pos = seg_tile_walk(P, G, buf, T, pos, umin64(G.A + TILE, send), steps);
     if (wid == 0) {
       if (!(DRP_SEG_TABLE && table)) {
@@ -3469,6 +3480,7 @@ __global__ __launch_bounds__(SEG_STB) void seg_stitch(DecodeParams P, SegRange R
     if (!bad) {
       for (uint32_t s = tid; s < ns; s += SEG_STB) {
         const uint32_t x = sidx[s];
+        if (R.seg_lane) R.seg_lane[s] = (uint8_t)x;
         R.seg_entry[s] = R.cand[(uint64_t)s * 2 * SEG_CAND + x];
         if (s == ns - 1) R.seg_entry[ns] = R.cand[(uint64_t)s * 2 * SEG_CAND + SEG_CAND + x];
       }
@@ -3476,6 +3488,8 @@ __global__ __launch_bounds__(SEG_STB) void seg_stitch(DecodeParams P, SegRange R
     }
     __syncthreads();  // (the serial stitch reuses the LDS)
   }
+  if (R.seg_lane)  // (the serial stitch: seg_claims walks every segment)
+    for (uint64_t s = tid; s < R.nseg; s += SEG_STB) R.seg_lane[s] = 0xFF;
   auto tab = reinterpret_cast<uint64_t (*)[SEG_SB][2 * SEG_CAND]>(smem);  // [2][SEG_SB][128]: 2 x 64 KB
   constexpr uint32_t W = SEG_SB * 2 * SEG_CAND;  // words per block
   // threads [t0, SEG_STB) copy block blk into buffer buf
@@ -3537,6 +3551,7 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
   __shared__ uint32_t rok;
   const uint32_t tid = threadIdx.x;
   const uint64_t seg = blockIdx.x;
+  if (R.ctile && R.seg_lane[seg] != 0xFF) return;  // (seg_claims_par's)
   TileGeo G = seg_geo(P, R.s);
   const uint64_t ta = R.t0 + seg * R.G, tb = umin64(ta + R.G, R.tl), send = seg_end(G, R, seg);
   for (uint64_t i = tid; i < tb - ta; i += NT) lcl[i] = C_ID;
@@ -3681,6 +3696,72 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
     atomicAdd(&P.stats[62], (unsigned long long)n_walk);
     atomicAdd(&P.stats[63], (unsigned long long)n_tiles);
     atomicAdd(&P.stats[55], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_wg));
+  }
+}
+
+// seg_claims for the segments whose exact chain is one of seg_walk's candidates (seg_lane): every
+// tile of the range at once, one lane per tile, from that candidate's position entering the tile
+// (seg_walk's ctile) through the tile's headers in L2 / HBM, the thread records gathered in LDS
+// per wave and written out coalesced. The serial seg_claims walked each segment's ~100 tiles one
+// after another in ~2300 workgroups (the LDS per staged tile bounds them).
+__global__ __launch_bounds__(WAVE) void seg_claims_par(DecodeParams P, SegRange R) {
+  __shared__ uint32_t rec[3][WAVE][NT / 4];  // entry byte, frames, change frames of each thread (24 KB)
+  const uint32_t lane = threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * WAVE + lane, n = R.tl - R.t0;
+  const uint64_t u = R.t0 + i, seg = i < n ? i / R.G : 0;
+  const uint32_t x = i < n ? R.seg_lane[seg] : 0xFFu;
+  for (uint32_t w = 0; w < NT / 4; w++) {
+    rec[0][lane][w] = 0xFFFFFFFFu;
+    rec[1][lane][w] = 0;
+    rec[2][lane][w] = 0;
+  }
+  bool rok = false;
+  if (x != 0xFFu) {
+    const TileGeo G = seg_geo(P, R.s);
+    const uint64_t A = seg_tile_a(G, u), send = seg_end(G, R, seg), sb = seg_tile_a(G, R.t0 + seg * R.G);
+    const uint32_t c = R.ctile[i * SEG_CAND + x];
+    uint64_t cl = C_ID;
+    if (c < CT_PAST && sb + c < A + TILE) {  // (else no chain position in the tile: identity)
+      const uint64_t lim = umin64(A + TILE, send);
+      uint64_t p = sb + c;
+      uint32_t ok = 1;
+      uint8_t *r0 = reinterpret_cast<uint8_t *>(rec[0][lane]), *r1 = reinterpret_cast<uint8_t *>(rec[1][lane]),
+              *r2 = reinterpret_cast<uint8_t *>(rec[2][lane]);
+      uint32_t cth = NT, ce = 0, cn = 0, cc = 0;
+      while (is_pos(p) && p < lim && p < G.se) {
+        const Hdr h = hdr_global(P.bytes, p, G.se);
+        if (h.kind != H_VALID) {
+          p = term_of(h, p);
+          ok = 0;
+          break;
+        }
+        const uint32_t o = (uint32_t)(p - A), th = o / SEGB;
+        const bool nw = th != cth;
+        ce = nw ? o % SEGB : ce;
+        cn = (nw ? 0u : cn) + (h.id != 0u);
+        cc = (nw ? 0u : cc) + (h.id == 1u);
+        cth = th;
+        r0[th] = (uint8_t)ce;
+        r1[th] = (uint8_t)cn;
+        r2[th] = (uint8_t)cc;
+        p = h.succ;
+      }
+      cl = (p & MARK_TERM) ? (p & ~M_ERR) : p;
+      rok = ok && lim == A + TILE;  // (the stream's last tile keeps its records: verify re-walks it)
+    }
+    P.claim[u] = cl;
+  }
+  // the walked tiles' records, a tile at a time by the whole wave (128 B per array per tile)
+  uint64_t rm = __ballot(rok);
+  while (rm) {
+    const uint32_t j = (uint32_t)__builtin_ctzll(rm);
+    rm &= rm - 1;
+    const uint64_t uj = R.t0 + (uint64_t)blockIdx.x * WAVE + j;
+    if (lane < NT / 4) {
+      reinterpret_cast<uint32_t *>(P.ent + uj * NT)[lane] = rec[0][j][lane];
+      reinterpret_cast<uint32_t *>(P.ent_n + uj * NT)[lane] = rec[1][j][lane];
+      reinterpret_cast<uint32_t *>(P.ent_c + uj * NT)[lane] = rec[2][j][lane];
+    }
   }
 }
 
@@ -3960,8 +4041,11 @@ extern "C" hipError_t drp_launch_blob_bytes(const uint8_t *type, const uint32_t 
 #ifndef DRP_SEG_LINK
 #define DRP_SEG_LINK 1  // 0: the serial stitch only (A/B)
 #endif
+#ifndef DRP_SEGC_PAR
+#define DRP_SEGC_PAR 1  // 0: seg_claims walks every segment serially (A/B)
+#endif
 extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, uint64_t t0, uint64_t tl,
-                                            uint64_t *scratch, hipStream_t st) {
+                                            uint64_t *scratch, uint32_t *ctile, uint64_t ctile_cap, hipStream_t st) {
   if (tl <= t0) return hipSuccess;
   spec::SegRange R;
   R.s = s;
@@ -3981,10 +4065,14 @@ extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, u
   R.cand = scratch;
   R.seg_entry = scratch + 2 * spec::SEG_CAND * spec::SEG_NMAX;
   R.nidx = DRP_SEG_LINK ? reinterpret_cast<uint8_t *>(R.seg_entry + spec::SEG_NMAX + 2) : nullptr;  // (SEG_NMAX x 64 B, 16-B aligned)
+  R.seg_lane = reinterpret_cast<uint8_t *>(R.seg_entry + spec::SEG_NMAX + 2) + spec::SEG_NMAX * spec::SEG_CAND;
+  // (the parallel seg_claims needs the stitch's tables and a position per candidate per tile)
+  R.ctile = DRP_SEGC_PAR && R.nidx && ctile && ctile_cap >= n * spec::SEG_CAND ? ctile : nullptr;
   DecodeParams Q = *P;
   hipLaunchKernelGGL(spec::seg_walk, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);
   if (R.nidx) hipLaunchKernelGGL(spec::seg_link, dim3((uint32_t)R.nseg), dim3(WAVE), 0, st, Q, R);
   hipLaunchKernelGGL(spec::seg_stitch, dim3(1), dim3(spec::SEG_STB), 0, st, Q, R);
+  if (R.ctile) hipLaunchKernelGGL(spec::seg_claims_par, dim3((uint32_t)((n + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, Q, R);
   hipLaunchKernelGGL(spec::seg_claims, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);
   return hipGetLastError();
 }

@@ -120,8 +120,9 @@ hipError_t drp_launch_spec_head(const drp::DecodeParams *P, uint64_t nt_max, uin
                                 uint32_t *tile_stream, hipStream_t st);
 // out[0] = payload bytes of the blob rows among rows [0, n) (out zeroed by the caller)
 hipError_t drp_launch_blob_bytes(const uint8_t *type, const uint32_t *plen, uint64_t n, uint64_t *out, hipStream_t st);
+// ctile: 64 u32 per tile of the range (seg_claims_par; null or too small: the serial seg_claims)
 hipError_t drp_launch_seg_repair(const drp::DecodeParams *P, uint64_t s, uint64_t t0, uint64_t tl, uint64_t *scratch,
-                                 hipStream_t st);
+                                 uint32_t *ctile, uint64_t ctile_cap, hipStream_t st);
 hipError_t drp_launch_spec_verify(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                   uint32_t *tile_stream, hipStream_t st);
 hipError_t drp_launch_spec_verify_list(const drp::DecodeParams *P, uint64_t n, uint64_t nstreams,
