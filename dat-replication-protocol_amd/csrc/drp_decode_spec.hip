@@ -1285,7 +1285,7 @@ __device__ __forceinline__ Hdr hdr_global(const uint8_t *g, uint64_t p, uint64_t
 // Records: none (0xFF), so the records-only check relists the tile and verify_counts re-walks it
 // from its exact entry (on the second framing, the cascade shortcut takes the whole list instead).
 #ifndef DRP_FL_CAP
-#define DRP_FL_CAP 8  // link rounds before the pointer-jumping form (~0: never)
+#define DRP_FL_CAP 6  // link rounds before the pointer-jumping form (~0: never); clean C2 tiles settle in <= 5
 #endif
 constexpr uint32_t JT_C_ID = 2u << 30, JT_TERM = 1u << 30, JT_NONE = 0xFFFFu;
 template <uint32_t NTT>
