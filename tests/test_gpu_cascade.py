@@ -55,6 +55,25 @@ def test_cascade_shortcut_parity(monkeypatch, period, at, small, chg):
     ctx.close()
 
 
+@pytest.mark.parametrize("shape", ["c2", "random", "shadow"])
+def test_pointer_jumping_claims_parity(monkeypatch, shape):
+    """DRP_JUMP_MIN=0: every tile whose link rounds reach DRP_FL_CAP takes the pointer-jumping claims
+    form (fast_claims_jump: claim by pointer jumping, no records, the tile relisted), not only past
+    the per-launch threshold a cascade reaches. Clean C2, random frames and a shadow stream stay
+    bit-exact with the oracle, and never need the exact kernel."""
+    import random
+
+    from _gpu import assert_same, drp_amd
+    monkeypatch.setenv("DRP_JUMP_MIN", "0")  # (read by drp_open)
+    ctx = drp_amd.Ctx(0)
+    wire = {"c2": lambda: S.c2_stream(300_000, seed=13).tobytes(),
+            "random": lambda: S.random_stream(random.Random(31), 20_000, blob_p=0.05, blob_max=20000),
+            "shadow": lambda: S.shadow_stream(int(16 * 2**20 / 3000), period=3000, shadow_at=70, small=4)}[shape]()
+    assert_same(ctx.decode_batch(wire), O.decode_batch(wire, chunk=65536), shape)
+    assert ctx.timing().strict_reruns == 0, "fell back to the exact kernel"
+    ctx.close()
+
+
 @pytest.mark.parametrize("cap", ["1", "0"])
 def test_dirty_list_overflow_full_pass(monkeypatch, cap):
     """Repair passes verify only the tiles a repair changed (dirty lists, drp_api.hip); a list
