@@ -143,6 +143,10 @@ struct drp_ctx {
   uint32_t kstrong_hbm = 0;
   uint32_t cascade_min = 4096;  // DRP_CASCADE_MIN (tests: small cascades)
   int64_t jump_min = -1;        // DRP_JUMP_MIN (-1: max(64, tiles / 512))
+  // claims kernel: the region walkers (drp_walk.hip) for batches of at least walk_min tiles,
+  // claims_fast below; DRP_CLAIMS=walk / fast forces one (A/B, tests)
+  uint64_t walk_min = 32768;
+  int claims_mode = 0;  // 0 auto, 1 walk, 2 fast
   uint64_t dirty_cap = ~0ull;
   bool stats = false;
   const char *trace_file = nullptr;
@@ -228,6 +232,8 @@ int drp_open(int device, drp_ctx **out) {
   if (const char *e = getenv("DRP_KSTRONG_HBM")) c->kstrong_hbm = (uint32_t)atoi(e);
   if (const char *e = getenv("DRP_CASCADE_MIN")) c->cascade_min = (uint32_t)strtoul(e, nullptr, 10);
   if (const char *e = getenv("DRP_JUMP_MIN")) c->jump_min = strtoll(e, nullptr, 10);
+  if (const char *e = getenv("DRP_WALK_MIN")) c->walk_min = strtoull(e, nullptr, 10);
+  if (const char *e = getenv("DRP_CLAIMS")) c->claims_mode = strcmp(e, "walk") == 0 ? 1 : strcmp(e, "fast") == 0 ? 2 : 0;
   if (const char *e = getenv("DRP_DIRTY_CAP")) c->dirty_cap = strtoull(e, nullptr, 10);
   c->trace_file = getenv("DRP_TRACE_FILE");
   if (getenv("DRP_STATS") && hipMalloc((void **)&c->dstats, 64 * 8) == hipSuccess) c->stats = true;
@@ -302,7 +308,7 @@ int drp_set_blob_skip(drp_ctx *c, int mode) {
 // scratch layout for a decode of `nbytes` over `ns` streams
 struct DecLayout {
   uint64_t ntiles_max;
-  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, tstream, ent, tk, tsp, fmiss, segw, scan_tmp, total;
+  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, tstream, ent, tk, tsp, fmiss, segw, scan_tmp, walk, total;
   uint64_t nsg;
 };
 static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
@@ -326,6 +332,7 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.segw = o; o += al((2 * 64 * 8192 + 8194) * 8 + 65 * 8192);  // segmented repair: candidates, entries,
                                                                 // next-candidate tables, lanes (SEG_NMAX)
   L.scan_tmp = o; o += al((L.ntiles_max / 4096 + 2) * 8);  // tile scans: block sums
+  L.walk = o; o += al((ns + 2) * 8);                         // region walkers: per-stream region prefix
   L.total = o;
   return L;
 }
@@ -655,6 +662,10 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.cascade_min = c->cascade_min;
   P.jump_min = c->jump_min >= 0 ? (uint32_t)c->jump_min : (uint32_t)std::max<uint64_t>(64, NT / 512);
   P.dlist_cap = std::min<uint64_t>(NT, c->dirty_cap);  // (tests: DRP_DIRTY_CAP)
+  if (c->claims_mode == 1 || (c->claims_mode == 0 && NT >= c->walk_min)) {
+    P.walk_rp = c->scratch.at<uint64_t>(L.walk);
+    P.walk_tpr = drp_walk_tiles_per_region(NT);
+  }
   unsigned long long *dstats = c->stats ? c->dstats : nullptr;
   if (dstats) P.stats = dstats;
   {  // tile_prefix and every per-decode clear in one launch
@@ -810,6 +821,8 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
                                "k2_stage", "k2_entry", "k2_link", "k3_stage", "k3_link", "k3_emit"};
     for (int k = 0; k < 14; k++)
       if (ph[k][0]) fprintf(stderr, " %s=%.0f", ph[k], (double)hs[40 + k] / (double)(h[0] ? h[0] : 1));
+    fprintf(stderr, " walk: syncs=%llu deaths=%llu first death at %#llx lds=%#llx hbm=%#llx w|lane|o=%#llx", hs[31], hs[32],
+            hs[36], hs[37], hs[38], hs[39]);
     fprintf(stderr, " repairs=%d (avg cycles per tile) link_rounds=%llu max=%llu tiles_over8=%llu restart_tiles=%llu"
             " jump_tiles=%llu seg_claims: walk_cycles=%llu frames=%llu tiles=%llu wg_cycles=%llu\n", pass, hs[56],
             hs[57], hs[58], hs[59], hs[60], hs[61], hs[62], hs[63], hs[55]);

@@ -74,6 +74,9 @@ struct DecodeParams {
   uint32_t cascade_min;  // listed tiles that make the head's verify a cascade (drp_decode_spec.hip)
   uint32_t jump_min;     // claims tiles whose link rounds hit DRP_FL_CAP before the rest take the
                          // pointer-jumping form (counted in counter[12]; drp_decode_spec.hip)
+  // region walkers (drp_walk.hip): per-stream region prefix [nstreams + 1], tiles per region
+  uint64_t *walk_rp;
+  uint32_t walk_tpr;
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
   unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
 };
@@ -116,6 +119,8 @@ uint32_t drp_spec_tile_bytes(void);
 uint32_t drp_spec_retry_mask(void);
 uint32_t drp_spec_miss_bit(void);
 uint32_t drp_spec_cascade_bit(void);
+hipError_t drp_launch_claims_walk(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t st);
+uint32_t drp_walk_tiles_per_region(uint64_t nt_max);
 hipError_t drp_launch_spec_head(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                 uint32_t *tile_stream, hipStream_t st);
 // out[0] = payload bytes of the blob rows among rows [0, n) (out zeroed by the caller)

@@ -12,6 +12,8 @@
 #   pmc:<w>        FETCH_SIZE / WRITE_SIZE / SQ passes of workload w (c2, c4, c5) (scripts/gpu_pmc.sh)
 #   ab:<variant>   quick C2 + C5 lines with exp/<variant>/libdrp.so (scripts/build_variant.sh)
 #   probe:<script> python3 scripts/<script> (a measurement script)
+#   env:K=V        export K=V for the steps that follow (unenv:K unsets it)
+#   c2             the C2 line alone (no sub-lines, no CPU legs)
 set -e
 export TMPDIR=/tmp
 TAG=$1
@@ -66,6 +68,16 @@ for step in "$@"; do
       S=${step#probe:}
       timeout -k 10 400 python3 -u scripts/$S > $OUT/probe_${S%%.*}.log 2>&1
       echo "probe $S done"
+      ;;
+    env:*)
+      export "${step#env:}"
+      ;;
+    unenv:*)
+      unset "${step#unenv:}"
+      ;;
+    c2)
+      timeout -k 10 300 python -u bench.py --no-cpu --no-sub --steps 10 --warmup 2 >> $OUT/c2.log 2>&1
+      echo "c2 (${DRP_CLAIMS:-auto}): $(tail -1 $OUT/c2.log | cut -c1-400)"
       ;;
     *)
       echo "unknown step $step"
