@@ -153,9 +153,6 @@ struct drp_ctx {
   unsigned long long *dstats = nullptr;
   uint32_t *ctile = nullptr;  // segmented repair: per-tile candidate positions (grown on demand)
   uint64_t ctile_cap = 0;
-  DecodeParams lastP = {};  // the last speculative decode's parameters (measurement hooks)
-  uint64_t lastNT = 0;
-  uint32_t *lastTS = nullptr;  // its tile -> stream map
   DevBuf scratch, in_stage, out_stage, aux;
   DevBuf dec_cols;  // device columns of the staged host-batch decode (drp_decode_stage)
   double frames_per_byte = 0;  // density of the last staged batch (sizes the next one's columns)
@@ -335,66 +332,6 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.walk = o; o += al((ns + 2) * 8);                         // region walkers: per-stream region prefix
   L.total = o;
   return L;
-}
-
-// Measurement hook, not part of the product path (scripts/probe_overlap.py): after a
-// single-stream decode on the ctx, times its claims kernel alone, its emit kernel alone, both side
-// by side on two streams, and both roles in one launch with the emit 0 / 64 / 1024 tiles behind
-// the claims on the same XCD: ms[0..5].
-// Measurement hook: the claims + verification head of the last speculative decode run again (same
-// input, which must still be alive), and the tiles its records-only check relisted copied out
-// (up to cap, in list order; *n: how many there were). scripts/probe_relist.py.
-int drp_probe_relist(drp_ctx *c, uint32_t *out, uint32_t cap, uint32_t *n) {
-  if (!c || !c->lastNT || !n) return DRP_E_INVAL;
-  (void)hipSetDevice(c->device);
-  DecodeParams P = c->lastP;
-  const uint64_t NT = c->lastNT;
-  hipStream_t st = c->st;
-  CHK(hipMemsetAsync(P.claim, 0, 2 * NT * 8, st));  // claim, incl_e
-  CHK(hipMemsetAsync(P.counter, 0, 64, st));
-  CHK(hipMemsetAsync(P.first_miss, 0xFF, P.nstreams * 8, st));
-  CHK(hipMemsetAsync(P.dstamp, 0, NT * 4, st));
-  P.pass_id = 1;
-  CHK(drp_launch_spec_head(&P, NT, P.nstreams, c->lastTS, st));
-  uint32_t cnt = 0;
-  CHK(hipMemcpyAsync(&cnt, P.vlist_n, 4, hipMemcpyDeviceToHost, st));
-  CHK(hipStreamSynchronize(st));
-  *n = cnt;
-  if (out && cap) {
-    CHK(hipMemcpy(out, P.vlist, (size_t)std::min(cnt, cap) * 4, hipMemcpyDeviceToHost));
-  }
-  return DRP_OK;
-}
-
-// Measurement hook (after drp_probe_relist): tile t's per-thread records (entry byte, frames,
-// change frames: 3 x 128 bytes) and its claim and the previous tile's.
-int drp_probe_tile(drp_ctx *c, uint64_t t, uint8_t *rec, uint64_t *claims) {
-  if (!c || !c->lastNT || t >= c->lastNT || !rec || !claims) return DRP_E_INVAL;
-  (void)hipSetDevice(c->device);
-  const DecodeParams &P = c->lastP;
-  CHK(hipMemcpy(rec, P.ent + t * 128, 128, hipMemcpyDeviceToHost));
-  CHK(hipMemcpy(rec + 128, P.ent_n + t * 128, 128, hipMemcpyDeviceToHost));
-  CHK(hipMemcpy(rec + 256, P.ent_c + t * 128, 128, hipMemcpyDeviceToHost));
-  CHK(hipMemcpy(claims, P.claim + (t ? t - 1 : 0), 16, hipMemcpyDeviceToHost));
-  return DRP_OK;
-}
-
-int drp_probe_overlap(drp_ctx *c, float *ms) {
-  if (!c || !ms || !c->lastNT) return DRP_E_INVAL;
-  hipStream_t b = nullptr;
-  hipEvent_t ev[10];
-  CHK(hipStreamCreateWithFlags(&b, hipStreamNonBlocking));
-  for (auto &e : ev) CHK(hipEventCreate(&e));
-  CHK(drp_probe_overlap_launch(&c->lastP, c->lastNT, c->st, b, ev));
-  CHK(hipStreamSynchronize(c->st));
-  CHK(hipStreamSynchronize(b));
-  (void)hipEventElapsedTime(&ms[0], ev[0], ev[1]);
-  (void)hipEventElapsedTime(&ms[1], ev[1], ev[2]);
-  (void)hipEventElapsedTime(&ms[2], ev[3], ev[5]);
-  for (int v = 0; v < 3; v++) (void)hipEventElapsedTime(&ms[3 + v], ev[6 + v], ev[7 + v]);
-  for (auto &e : ev) (void)hipEventDestroy(e);
-  (void)hipStreamDestroy(b);
-  return DRP_OK;
 }
 
 int drp_host_alloc(uint64_t bytes, void **out) {
@@ -712,9 +649,6 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     return DRP_OK;
   };
   if (const int rt = launch_tail()) return rt;
-  c->lastP = P;
-  c->lastNT = NT;
-  c->lastTS = tstream;
   const uint32_t relisted = h[14];
   int pass = 0;
   bool seg_done = false;

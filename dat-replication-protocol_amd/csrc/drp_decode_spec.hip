@@ -42,32 +42,14 @@
 namespace drp {
 namespace spec {
 
-#ifndef DRP_VALIDATE_ALL
-#define DRP_VALIDATE_ALL 0  // 1: validate a candidate's own change even behind a 1-byte varint
-#endif
 #ifndef DRP_K1_WAVES
 #define DRP_K1_WAVES 8  // min waves per SIMD for claims_fast (its occupancy without an LDS image, see DRP_K1_GIMG)
-#endif
-#ifndef DRP_LIST_PLAUSIBLE
-#define DRP_LIST_PLAUSIBLE 0  // 1: the list stage also checks Change payloads (the chain walks always do)
 #endif
 #ifndef DRP_EMIT_WAVES
 #define DRP_EMIT_WAVES 5  // min waves per SIMD for the emit kernel (0.88 -> 0.79 ms at 20M frames)
 #endif
 #ifndef DRP_KSTRONG
 #define DRP_KSTRONG 4
-#endif
-#ifndef DRP_HALO_NODES
-#define DRP_HALO_NODES 1  // 0: the fast claims kernel lists the tile's positions only (A/B)
-#endif
-#ifndef DRP_CLAIMS_FAST
-#define DRP_CLAIMS_FAST 1  // 0: the general claims kernel for every tile (A/B)
-#endif
-#ifndef DRP_ABLATE_F
-#define DRP_ABLATE_F 0  // measurement builds only: claims_fast stops after phase N (output invalid)
-#endif
-#ifndef DRP_ABLATE
-#define DRP_ABLATE 0  // measurement builds only: spec_claims stops after phase N (output invalid)
 #endif
 constexpr int KSTRONG = DRP_KSTRONG;                    // frames a candidate chain must survive
 struct Img {
@@ -112,14 +94,7 @@ __device__ __forceinline__ uint64_t term_of(const Hdr &h, uint64_t p) {
 // the LDS image. Shadow headers whose varint swallows a real header's first bytes declare
 // ~10 KB+ "frames" whose payload runs on into the next frames' headers; real long frames
 // (4 KB values) cost one field walk.
-#ifndef DRP_PLAUS_CALL
-#define DRP_PLAUS_CALL 0  // 1: one out-of-line Change check (fewer SGPR spills, but measured 4% slower)
-#endif
-#if DRP_PLAUS_CALL
-__device__ __noinline__
-#else
 __device__ __forceinline__
-#endif
 bool change_ok(const uint8_t *lds, uint64_t A, uint64_t se, uint64_t po, uint64_t pl) {
   const LdsReader rd{lds, A, umin64(A + IMG, se)};
   const ChangeCols cc = decode_change(rd, po, pl);
@@ -174,7 +149,7 @@ __device__ __forceinline__ uint32_t strong(const Img &m, uint64_t c, uint64_t s1
     const Hdr h = m.at(p);
     if (h.kind == H_VALID) {
       if (k == 0) far = h.succ >= m.A + TILE;
-      if (!plausible(m, p, h, DRP_VALIDATE_ALL && k == 0)) return S_DEAD;
+      if (!plausible(m, p, h, 0 && k == 0)) return S_DEAD;
       if (p < s1) n += (h.id != 0) + ((h.id == 1) << 16);
       p = h.succ;
       if (R == NONE && p >= s1) R = p;
@@ -202,15 +177,8 @@ __device__ __forceinline__ uint32_t strong(const Img &m, uint64_t c, uint64_t s1
 // no carrier, or a carrier whose chain died at an error, restarts at the thread's own strong
 // candidate g. Verify mode: a virtual carrier before thread 0 exits at e_first, errors pass on.
 // One block-wide "latest carrier" scan per round; rounds repeat until no entry changes.
-#ifndef DRP_LINK_CALL
-#define DRP_LINK_CALL 0
-#endif
 template <bool VERIFY>
-#if DRP_LINK_CALL
-__device__ __noinline__
-#else
 __device__ __forceinline__
-#endif
 void link(const Img &m, uint64_t s1, uint64_t g, uint64_t e_first, uint64_t &E,
                                      uint64_t &R, uint32_t &n, uint64_t *wl, uint32_t *fl, uint32_t *overflow,
                                      bool *restart = nullptr) {
@@ -276,21 +244,14 @@ void link(const Img &m, uint64_t s1, uint64_t g, uint64_t e_first, uint64_t &E,
   "s_nop 1\n\t" op " %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
   "s_nop 1\n\t" op " %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"              \
   "s_nop 1\n\t" op " %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
-#ifndef DRP_DPP_ASM
-#define DRP_DPP_ASM 0  // 1: the inline-asm forms (one VALU per step; A/B)
-#endif
 // inclusive prefix sum over the wave
 __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
-#if DRP_DPP_ASM
-  asm volatile(DRP_DPP_STEPS("v_add_u32_dpp") : "+v"(v));
-#else
   v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
   v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
   v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
   v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
   v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
   v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
-#endif
   return v;
 }
 // wave-uniform sum / maximum (lane 63 of the inclusive scan)
@@ -298,10 +259,6 @@ __device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_dpp(v), 63);
 }
 __device__ __forceinline__ uint32_t wave_max_dpp(uint32_t v) {
-#if DRP_DPP_ASM
-  asm volatile(DRP_DPP_STEPS("v_max_u32_dpp") : "+v"(v));
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-#else
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false));
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false));
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false));
@@ -309,7 +266,6 @@ __device__ __forceinline__ uint32_t wave_max_dpp(uint32_t v) {
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false));
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false));
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-#endif
 }
 
 __device__ __forceinline__ uint32_t wave_min_dpp(uint32_t v) {
@@ -471,12 +427,9 @@ __device__ __forceinline__ void put_image(uint8_t *buf, const uint4 (&v)[SEGB / 
 // Stage the tile and its halo with LDS-DMA (global_load_lds_dwordx4: no VGPRs hold the image;
 // wave w's k-th load fills LDS bytes [4096 w + 1024 k, +1024) from the same offsets of the tile),
 // except near the end of the batch buffer (guarded register loads there).
-#ifndef DRP_EMIT_GLDS
-#define DRP_EMIT_GLDS 1
-#endif
 __device__ __forceinline__ void stage_glds(const DecodeParams &P, const TileGeo &G, uint8_t *buf) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-  if (!DRP_EMIT_GLDS || G.A + IMG > P.nbytes) {
+  if (G.A + IMG > P.nbytes) {
     stage(P, G, buf);
     return;
   }
@@ -587,12 +540,9 @@ constexpr uint16_t NX_NEAR = 0xFFFD, NX_FAR = 0xFFFE, NX_DEAD = 0xFFFF;
 #ifndef DRP_K1G_WAVES
 #define DRP_K1G_WAVES 5  // min waves per SIMD for the general claims kernel (edge and dense tiles)
 #endif
-#ifndef DRP_EDGE_FAST
-#define DRP_EDGE_FAST 1  // 0: stream-edge tiles take the general form (A/B)
-#endif
 // the fast form (below), which spec_claims also runs for the stream-edge tiles on its list
 struct FastLds;
-enum : uint32_t { FC_OK = 0, FC_DENSE = 1, FC_ABLATE = 2 };
+enum : uint32_t { FC_OK = 0, FC_DENSE = 1 };
 template <bool CF, bool EDGE = false>
 __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const TileGeo &G, uint64_t t, FastLds &S,
                                                 uint32_t &eb_o, uint32_t &en_o, uint32_t &ecn_o, uint64_t &cl_o);
@@ -618,7 +568,6 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
   bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
   if (t >= ntiles) continue;  // (whole workgroup)
-#if DRP_EDGE_FAST
   // a stream-edge tile claims_fast listed: the fast form with the stream's bounds (its LDS in buf;
   // one with more than FCAP live positions goes on below)
   if (P.work && (G.A < G.so || G.A + IMG > G.se)) {
@@ -627,15 +576,10 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
     if (fast_claims<true, true>(P, G, t, *reinterpret_cast<FastLds *>(buf), eb, en, ecn, cl) != FC_DENSE) continue;
     bsync();  // (its LDS reads are done before stage_live writes buf)
   }
-#endif
   const uint64_t live = stage_live(P, G, buf);
   const Img m{buf, P.bytes, G.A, G.se};
   const uint64_t lb = G.A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
   PHASE(0);
-#if DRP_ABLATE == 1
-  if (tid == 0) P.claim[t] = __builtin_popcountll(live);  // (measurement build: stage + live mask only)
-  continue;
-#endif
 
   // ---- strong candidate: the first live position whose chain survives, preferring chains
   // that can be checked inside the LDS image (shadow headers whose varint swallows a real
@@ -694,7 +638,7 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
       uint16_t code = NX_DEAD;
       uint8_t a = 0;
       if (valid && sr >= TILE) lpos[i] |= 0x8000u;  // first frame leaves the tile
-      if (valid && (DRP_LIST_PLAUSIBLE == 0 || plausible(m, G.A + o, m.at(G.A + o), false))) {
+      if (valid) {
         if (near) {
           code = NX_NEAR;  // the stream end: survived
           a = 1;
@@ -734,10 +678,6 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
       }
       if (a == 2) defer |= 1ull << ((lpos[i] & 0x7FFFu) - tid * SEGB);
     }
-#if DRP_ABLATE == 2
-    if (tid == 0) P.claim[t] = g;  // (measurement build: + list survival)
-    continue;
-#endif
     if (g != NONE) R = walk<true>(m, g, s1, n);
   } else {  // very dense tile: per-thread checks
     uint64_t bits = live;
@@ -791,10 +731,6 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
   uint64_t E = g;
   bool rs = false;  // this thread restarts the chain (no chain enters it, or the entering one died)
   PHASE(1);
-#if DRP_ABLATE == 3
-  if (tid == 0) P.claim[t] = R + E;  // (measurement build: + own walk and masks)
-  continue;
-#endif
   // ---- link the threads' chains ------------------------------------------------------------
   link<false>(m, s1, g, NONE, E, R, n, xr, xf, P.overflow, &rs);
   // A thread no chain reaches and without an LDS-decided candidate, with none later in the
@@ -829,10 +765,6 @@ __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P)
     block_max2_u32(need, js, xf2);
   }
   PHASE(2);
-#if DRP_ABLATE == 4
-  if (tid == 0) P.claim[t] = R + E;  // (measurement build: + link and HBM restarts)
-  continue;
-#endif
   // The chain's last frame may jump over threads that hold strong candidates: a shadow that
   // joined the chain can jump far and land on a real frame start past the tile. Build the
   // chain those candidates start as well and keep it when it is the denser one (>= 2
@@ -931,9 +863,6 @@ __device__ __forceinline__ uint32_t masks16(const uint4 v) {  // m | s << 16
 // required fields present, and the last field ending exactly at the payload end (the value's
 // bytes are not read). Random bytes essentially never pass; a real frame in another shape is left
 // undecided as before. Prediction only: verification is exact.
-#ifndef DRP_CHANGE_FILLS
-#define DRP_CHANGE_FILLS 1  // 1: the tile's nodes and the halo's long frames; 2: every node; 0: none (A/B)
-#endif
 __device__ __forceinline__ bool change_fills(const uint32_t *w32, uint32_t po, uint32_t pl, uint32_t lim,
                                              uint32_t off = 0, uint32_t found = 0) {
 #pragma unroll 1
@@ -1109,37 +1038,16 @@ __device__ __forceinline__ bool flink(const uint32_t *lnd, uint32_t s1r, uint32_
   return false;
 }
 
-// measurement builds (DRP_ABLATE_F): every value a later phase would read is kept live through an
-// empty asm, so the build's instruction counts are those of the phases before the stop
-__device__ __forceinline__ void abl_sink1(uint64_t v) { asm volatile("" ::"v"(v)); }
-template <class... T>
-__device__ __forceinline__ void abl_sink(const T &...v) {
-  (abl_sink1((uint64_t)v), ...);
-}
-// measurement builds (DRP_ABLATE_F): valid "no prediction" records that keep x live
-__device__ __forceinline__ void abl_out(const DecodeParams &P, uint64_t t, uint64_t x) {
-  const uint64_t ix = t * NT + threadIdx.x;
-  P.ent[ix] = x == 0x123456789ull ? 0 : 0xFF;
-  P.ent_n[ix] = 0;
-  P.ent_c[ix] = 0;
-  if (threadIdx.x == 0) P.claim[t] = C_ID;
-}
 
 
-constexpr uint32_t HV = DRP_HALO_NODES ? HALO / SEGB : 0;  // halo "threads" with nodes
+constexpr uint32_t HV = HALO / SEGB;  // halo "threads" with nodes
 // LDS of the fast claims form
 // claims_fast keeps no LDS image of the tile: every live position's header is parsed from the
 // L2 lines the tile load just brought in (the byte masks come from the loaded registers), so a
 // tile takes 6.2 KB of LDS instead of 15 and the kernel runs at 8 waves/SIMD (52 VGPRs) instead
 // of 5: the HBM stream of some workgroups overlaps the instruction-bound work of others
 // (C2 100M: 3.37 -> ~2.8 ms; C5: 3.77 -> ~2.4 ms).
-#ifndef DRP_K1_GIMG
-#define DRP_K1_GIMG 1  // 0: the LDS image (15 KB per tile, 5 waves/SIMD)
-#endif
 struct FastLds {
-#if !DRP_K1_GIMG
-  __attribute__((aligned(16))) uint8_t buf[IMG + 32];
-#endif
   uint64_t lmw[NT + HV];   // live masks; then strong masks
   uint64_t dmw[NT];        // undecided masks
   uint16_t loff[NT + HV];  // first list index of each thread
@@ -1296,17 +1204,13 @@ __device__ __forceinline__ uint64_t range_bits(uint32_t base, uint32_t lo, uint3
 template <bool CF, bool EDGE>
 __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const TileGeo &G, uint64_t t, FastLds &S,
                                                 uint32_t &eb_o, uint32_t &en_o, uint32_t &ecn_o, uint64_t &cl_o) {
-#if DRP_K1_GIMG
   uint8_t *buf = nullptr;
-#else
-  uint8_t *buf = S.buf;
-#endif
   uint64_t *lmw = S.lmw, *dmw = S.dmw, *xm = S.xm;
   uint16_t *loff = S.loff, *lpos = S.lpos;
   uint32_t *hmx = S.hmx, *lnd = S.lnd, *xw = S.xw, *xf = S.xf, *wl = S.wl, *fl = S.fl;
   uint8_t *lal = S.lal;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-  static_assert(!EDGE || DRP_K1_GIMG, "the edge form has no LDS image");
+  static_assert(!EDGE || 1, "the edge form has no LDS image");
   // ---- stage, masks, live positions (varints of 1..3 bytes) --------------------------------
   uint4 v[SEGB / 16], hv;
   if (EDGE) {
@@ -1317,12 +1221,6 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     for (int k = 0; k < (int)(SEGB / 16); k++) v[k] = q[k];
     hv = tid < HALO / 16 ? *reinterpret_cast<const uint4 *>(P.bytes + G.A + TILE + tid * 16) : make_uint4(0, 0, 0, 0);
   }
-#if !DRP_K1_GIMG
-#pragma unroll
-  for (int k = 0; k < (int)(SEGB / 16); k++) *reinterpret_cast<uint4 *>(buf + tid * SEGB + 16 * k) = v[k];
-  if (tid < HALO / 16) *reinterpret_cast<uint4 *>(buf + TILE + tid * 16) = hv;
-  if (tid < 2) *reinterpret_cast<uint4 *>(buf + IMG + tid * 16) = make_uint4(0, 0, 0, 0);
-#endif
   uint32_t mk[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) mk[k] = masks16(v[k]);
@@ -1330,10 +1228,10 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   mx[tid] = mk[0];
   if (tid < HALO / 16) {
     const uint32_t hmk = masks16(hv);
-    if (DRP_HALO_NODES) hmx[tid] = hmk;
+    hmx[tid] = hmk;
     if (tid == 0) mx[NT] = hmk;
   }
-  if (DRP_HALO_NODES && tid == HALO / 16) hmx[HALO / 16] = 0xFFFFu;  // (past the image: no terminators)
+  if (tid == HALO / 16) hmx[HALO / 16] = 0xFFFFu;  // (past the image: no terminators)
   bsync();
   const uint32_t nx = mx[tid + 1];
   const uint64_t M0 = (uint64_t)(mk[0] & 0xFFFFu) | ((uint64_t)(mk[1] & 0xFFFFu) << 16) |
@@ -1353,17 +1251,12 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     fo_rel = hi_rel < IMG ? max(lo_rel, hi_rel >= 3u ? hi_rel - 3u : 0u) : IMG;
     live = (live & range_bits(tid * SEGB, lo_rel, hi_rel)) | range_bits(tid * SEGB, fo_rel, hi_rel);
   }
-#if DRP_ABLATE_F == 1
-  abl_sink(live);
-  abl_out(P, t, 0);
-  return FC_ABLATE;
-#endif
   // Halo nodes (DRP_HALO_NODES): the halo's live positions join the list as HV more "threads", so
   // the survival check of the tile's last frames does not stop at the tile end (their chains
   // would otherwise leave the list within KSTRONG frames and stay undecided, and the link would
   // reach their threads one round at a time). Lanes 0..HV-1 of wave 0 build their masks.
   uint64_t hlive = 0;
-  if (DRP_HALO_NODES && tid < HV) {
+  if (tid < HV) {
     uint32_t hk[5];
 #pragma unroll
     for (int k = 0; k < 5; k++) hk[k] = hmx[tid * 4 + k];
@@ -1383,24 +1276,19 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   const uint32_t cnt = (uint32_t)__builtin_popcountll(live);
   const uint32_t cpre = wave_scan_dpp(cnt);
   const uint32_t hcnt = (uint32_t)__builtin_popcountll(hlive);
-  const uint32_t hpre = DRP_HALO_NODES ? wave_scan_dpp(hcnt) : 0u;
+  const uint32_t hpre = wave_scan_dpp(hcnt);
   if (lane == 63) xw[wid] = cpre;
-  if (DRP_HALO_NODES && tid == 63) xw[2] = hpre;
+  if (tid == 63) xw[2] = hpre;
   lmw[tid] = live;
-  if (DRP_HALO_NODES && tid < HV) lmw[NT + tid] = hlive;
+  if (tid < HV) lmw[NT + tid] = hlive;
   bsync();  // (also: mx reads done)
   const uint32_t off = cpre - cnt + (wid ? xw[0] : 0u);
   const uint32_t ttotal = NT == 2 * WAVE ? xw[0] + xw[1] : xw[0];  // the tile's nodes
-  const uint32_t total = ttotal + (DRP_HALO_NODES ? xw[2] : 0u);
+  const uint32_t total = ttotal + xw[2];
   if (total > FCAP) {  // very dense tile: the general kernel's per-thread checks
     if (!EDGE) push_work(P, t);
     return FC_DENSE;
   }
-#if DRP_ABLATE_F == 11
-  abl_sink(live, hlive, off, total, ttotal, hpre);
-  abl_out(P, t, 0);
-  return FC_ABLATE;
-#endif
   loff[tid] = (uint16_t)off;
   {
     uint64_t bits = live;
@@ -1410,7 +1298,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
       bits &= bits - 1;
     }
   }
-  if (DRP_HALO_NODES && tid < HV) {
+  if (tid < HV) {
     uint64_t bits = hlive;
     uint32_t i = ttotal + hpre - hcnt;
     loff[NT + tid] = (uint16_t)i;
@@ -1420,11 +1308,6 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     }
   }
   bsync();
-#if DRP_ABLATE_F == 12
-  abl_sink(live, off, total, ttotal);
-  abl_out(P, t, 0);
-  return FC_ABLATE;
-#endif
   // ---- parse every node once --------------------------------------------------------------------
   const uint32_t se_rel = (uint32_t)umin64(G.se - G.A, 0x7FFFFFFFull);  // >= IMG
   constexpr uint32_t KPT = FCAP / NT;  // nodes per thread (at most)
@@ -1433,11 +1316,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   uint32_t chained = 0;  // this thread's nodes whose successor is a node (in the image)
   uint32_t cfw[KPT];  // a Change frame leaving the image: payload offset | length << 14
   uint32_t cff[KPT];  // its first field's bytes | key seen << 20
-#if DRP_K1_GIMG
   const uint32_t *w32 = reinterpret_cast<const uint32_t *>(P.bytes + G.A);  // (L2: the tile was just read)
-#else
-  const uint32_t *w32 = reinterpret_cast<const uint32_t *>(buf);
-#endif
 #pragma unroll
   for (uint32_t j = 0; j < KPT; j++) {
     const uint32_t i = tid + j * NT;
@@ -1490,7 +1369,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
         c = NX_NEAR;  // ends at the stream end: survived
         a = 1;
         S.lsucc[i] = succ;
-      } else if (succ >= (DRP_HALO_NODES ? IMG - 16 : TILE)) {
+      } else if (succ >= IMG - 16) {
         c = NX_FAR;   // past the listed positions: undecided (a restart that needs it checks in HBM),
         a = 2;        // unless it is a Change frame whose fields fill it exactly (below)
         S.lsucc[i] = succ;
@@ -1499,7 +1378,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
         // The first field is checked here from the header's own bytes (no load): subset or key
         // (protocol-buffers writes fields in schema order), a length of <= 3 bytes, inside the
         // payload. ~99% of shadow headers stop here, so change_fills' loads are rare on C2.
-        if (CF && id == 1u && (DRP_CHANGE_FILLS == 2 || o < TILE || L > HALO) && L - 1u < (1u << 18)) {
+        if (CF && id == 1u && (o < TILE || L > HALO) && L - 1u < (1u << 18)) {
           const uint32_t x = k + 1u < 4u ? __builtin_amdgcn_alignbit(wn, w, 8u * (k + 1u)) : wn;  // bytes k+1..k+4
           const uint32_t tg = x & 0xFFu, lt = ~(x >> 8) & 0x808080u;
           if ((tg == 0x0Au || tg == 0x12u) && lt) {
@@ -1538,7 +1417,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
       uint32_t cr = 0;
       if (cfw[j]) {
         // (the LDS-image build reads its IMG + 32 bytes only; the default reads the batch)
-        const uint32_t lim = min(se_rel, DRP_K1_GIMG ? IMG + 512u : IMG + 32u - 36u), po = cfw[j] & 0x3FFFu,
+        const uint32_t lim = min(se_rel, IMG + 512u), po = cfw[j] & 0x3FFFu,
                        pl = cfw[j] >> 14;
         cr = change_fills_win(w32, po, pl, lim, cff[j] & 0xFFFFFu, cff[j] >> 20);
         if (cr == 2u) cr = change_fills(w32, po, pl, lim, cff[j] & 0xFFFFFu, cff[j] >> 20) ? 1u : 0u;
@@ -1550,13 +1429,6 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     }
   }
   bsync();
-#if DRP_ABLATE_F == 2
-#pragma unroll
-  for (uint32_t j = 0; j < KPT; j++) abl_sink(ncode[j], na[j], npos[j]);
-  abl_sink(live, off);
-  abl_out(P, t, 0);
-  return FC_ABLATE;
-#endif
   lmw[tid] = 0;  // (now the strong masks)
   dmw[tid] = 0;
   // ---- survival: KSTRONG - 1 rounds propagate death / undecided back along the chains ------------
@@ -1596,18 +1468,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     const uint32_t gc = lnd[gi] & 0xFFFFu;
     far = gc == NX_FAR || gc == NX_NEAR;
   }
-#if DRP_ABLATE_F == 3
-  abl_sink(g, defer, far, live, off);
-  abl_out(P, t, 0);
-  return FC_ABLATE;
-#endif
   uint32_t n = 0, R = RX_NONE;
   if (g != RX_NONE) R = fwalk(lnd, g, s1r, n);
-#if DRP_ABLATE_F == 4
-  abl_sink(g, defer, far, R, n, live, off);
-  abl_out(P, t, 0);
-  return FC_ABLATE;
-#endif
   // rule 2: a chain that starts by jumping past the tile only where nothing later can start one
   uint64_t S0m, S1m;
   {
@@ -1651,13 +1513,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     if (xw[6] >= P.jump_min) return fast_claims_jump<NT>(P, t, G.A, S, g, ttotal, total, eb_o, en_o, ecn_o, cl_o);
     flink(lnd, s1r, g, E, R, n, rs, wl, fl, P.overflow, P.stats);
   }
-#if DRP_ABLATE_F == 5
-  abl_sink(g, defer, R, n, E, rs, S0m, S1m, live, off);
-  abl_out(P, t, 0);
-  return FC_ABLATE;
-#endif
   // restarts from deferred candidates, decided in HBM (big frames), as in spec_claims
-  const Img m{buf, P.bytes, G.A, G.se, !DRP_K1_GIMG};
+  const Img m{buf, P.bytes, G.A, G.se, false};
   uint32_t need, js;  // a thread needs a restart; the last carrier + 1
   block_any_last(E == RX_NONE && defer && !any_above(S0m, S1m, tid), rx_node(E) && rx_off(E) < s1r, need, js, xf);
   bool moved = false;
@@ -1684,11 +1541,6 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     block_any_last(E == RX_NONE && defer && !any_above(S0m, S1m, tid), rx_node(E) && rx_off(E) < s1r, need, js,
                    xf);
   }
-#if DRP_ABLATE_F == 6
-  abl_sink(g, R, n, E, rs, js, moved, S0m, S1m, live, off);
-  abl_out(P, t, 0);
-  return FC_ABLATE;
-#endif
   // rule 3: the chain's last frame may jump over threads holding strong candidates; keep the
   // chain they start when it is the denser one (>= 2 frames)
   {
@@ -1862,9 +1714,6 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
   if (P.tile_sparse) P.tile_sparse[t] = (!multi && sf <= SP_FRAMES) ? 1 : 0;
 }
 
-#ifndef DRP_DIRTY_DEDUPE
-#define DRP_DIRTY_DEDUPE 1  // 0: no per-pass stamps (A/B of the duplicate-entry race the tests pin)
-#endif
 __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint64_t xr[NT / WAVE];
@@ -2061,7 +1910,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
         for (; j < tend && r < 64u; j++, r++) {
           // once per tile per list: two workgroups verifying one tile in the same pass would race
           // on its records (the slow path rewrites them while the other reads them)
-          if (!DRP_DIRTY_DEDUPE || atomicMax(&P.dstamp[j], P.pass_id) < P.pass_id) {
+          if (atomicMax(&P.dstamp[j], P.pass_id) < P.pass_id) {
             const uint32_t q = atomicAdd(P.dlist_n, 1u);
             if (q < P.dlist_cap) P.dlist[q] = (uint32_t)j;
           }
@@ -2235,41 +2084,8 @@ __device__ __forceinline__ void emit_frame(const DecodeParams &P, const Img &m, 
   if (c.err) badf = f < badf ? f : badf;
 }
 
-// A frame in the fast kernel: the frame table, and the Change columns when decode_change_fast
-// takes the payload (false: the tile goes to the general kernel).
-__device__ __forceinline__ bool emit_frame_fast(const DecodeParams &P, const Img &m, uint64_t p, uint64_t f,
-                                                uint64_t &badf) {
-  const Hdr h = hdr_fast(m, p);
-  if (f >= P.cap) return true;
-  const uint64_t po = p + h.vlen + 1, pl = h.L - 1;
-  P.payload_off[f] = po;
-  P.payload_len[f] = pl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)pl;
-  P.type[f] = (uint8_t)(h.id | (h.kind == H_TAIL_BLOB ? DRP_FRAME_PARTIAL : 0u));
-  if (h.id != 1) return true;
-  const LdsReader rd{m.lds, m.A, umin64(m.A + IMG, m.se)};
-  ChangeCols c;
-  if (!decode_change_fast(rd, po, pl, c)) return false;
-  P.key_off[f] = c.key_off;
-  P.key_len[f] = c.key_len;
-  P.subset_off[f] = c.subset_off;
-  P.subset_len[f] = c.subset_len;
-  P.value_off[f] = c.value_off;
-  P.value_len[f] = c.value_len;
-  P.change[f] = c.change;
-  P.from[f] = c.from;
-  P.to[f] = c.to;
-  uint32_t fl = c.flags;
-  if (c.err == DRP_ERR_REQUIRED) fl |= DRP_F_MISSING;
-  P.flags[f] = (uint8_t)fl;
-  if (c.err) badf = f < badf ? f : badf;
-  return true;
-}
-
-// ---- the fast emit in 32-bit tile-relative form ----------------------------------------------
-// Every position is an offset into the tile's LDS image (< IMG), every output store is a uniform
-// column pointer at the tile's first row plus a 32-bit row index (SGPR base + VGPR offset
-// addressing), and varints of up to 4 bytes are assembled in 32 bits: the same columns as
-// emit_frame_fast, with far fewer vector instructions per frame.
+// Output columns at a tile's first row: emit_lean stores at a uniform column pointer plus a 32-bit
+// byte offset (SGPR base + VGPR offset addressing).
 struct RowCols {
   uint64_t *poff;
   uint32_t *plen;
@@ -2296,123 +2112,6 @@ __device__ __forceinline__ RowCols row_cols(const DecodeParams &P, uint64_t base
   r.fl = P.flags + base;
   r.lim = base >= P.cap ? 0u : (uint32_t)umin64(P.cap - base, 0xFFFFFFFFull);
   return r;
-}
-
-// bytes o..o+3 and o+4..o+7 of the LDS image
-__device__ __forceinline__ void lds8(const uint8_t *lds, uint32_t o, uint32_t &w, uint32_t &wn) {
-  const uint32_t *q = reinterpret_cast<const uint32_t *>(lds) + (o >> 2);
-  const uint32_t sh = (o & 3u) * 8u, a0 = q[0], a1 = q[1], a2 = q[2];
-  w = __builtin_amdgcn_alignbit(a1, a0, sh);
-  wn = __builtin_amdgcn_alignbit(a2, a1, sh);
-}
-
-// decode_change_fast over the LDS image: payload at image offset po, pl bytes, bytes [0, lim) of
-// the image valid. true with decode_change's columns; false for any other shape (or a field that
-// leaves the image): the tile then goes to the general kernel, as with decode_change_fast.
-__device__ __forceinline__ bool change_fast32(const uint8_t *lds, uint32_t po, uint32_t pl, uint32_t lim,
-                                              ChangeCols &c) {
-  c.key_off = c.key_len = c.subset_off = c.subset_len = c.value_off = c.value_len = 0;
-  c.change = c.from = c.to = 0;
-  c.flags = 0;
-  c.err = 0;
-  uint32_t found = 0, off = 0;
-  while (off < pl) {
-    const uint32_t q = po + off;
-    if (pl - off < 2u || q + 2u > lim) return false;
-    uint32_t w, wn;
-    lds8(lds, q, w, wn);
-    const uint32_t b0 = w & 0xFFu, tag = b0 >> 3;
-    if (b0 >= 0x80u || tag - 1u > 5u) return false;
-    const uint32_t x = __builtin_amdgcn_alignbit(wn, w, 8);  // bytes 1..4
-    const uint32_t tm = ~x & 0x80808080u;
-    uint32_t k2;
-    uint64_t v;
-    const uint32_t v28 = (x & 0x7Fu) | ((x >> 1) & 0x3F80u) | ((x >> 2) & 0x1FC000u) | ((x >> 3) & 0xFE00000u);
-    if (tm) {
-      k2 = ((uint32_t)__builtin_ctz(tm) >> 3) + 1u;
-      v = v28 & ((1u << (7u * k2)) - 1u);  // (k2 = 4: 2^28 - 1, no overflow)
-    } else {  // a 5-byte varint: byte 5 must end it
-      const uint32_t b5 = (wn >> 8) & 0xFFu;
-      if (b5 & 0x80u) return false;
-      k2 = 5u;
-      v = (uint64_t)v28 | ((uint64_t)b5 << 28);
-    }
-    if (k2 > pl - off - 1u || q + 1u + k2 > lim) return false;
-    if (tag - 3u <= 2u) {
-      if (tag == 3u) {
-        c.change = v;
-        found |= 2;
-      } else if (tag == 4u) {
-        c.from = v;
-        found |= 4;
-      } else {
-        c.to = v;
-        found |= 8;
-      }
-      off += 1u + k2;
-    } else {
-      const uint32_t o2 = off + 1u + k2;
-      if (v > (uint64_t)(pl - o2)) return false;
-      const uint32_t v32 = (uint32_t)v;
-      if (tag == 1u) {
-        c.subset_off = o2;
-        c.subset_len = v32;
-        c.flags |= DRP_F_SUBSET;
-      } else if (tag == 2u) {
-        c.key_off = o2;
-        c.key_len = v32;
-        found |= 1;
-      } else {
-        c.value_off = o2;
-        c.value_len = v32;
-        c.flags |= DRP_F_VALUE;
-      }
-      off = o2 + v32;
-    }
-  }
-  if (found != 15) {
-    c.err = DRP_ERR_REQUIRED;
-    c.flags |= DRP_F_BAD;
-  }
-  return true;
-}
-
-// The delivered frame at image offset o, row i of the tile: false when its header or payload is
-// not in the fast shapes (the tile goes to the general kernel). Headers of 1..3-byte varints
-// whose 16 bytes lie inside the image and the stream (se_rel) are parsed here; others take the
-// 64-bit path (emit_frame_fast).
-__device__ __forceinline__ bool emit_frame32(const DecodeParams &P, const Img &m, const RowCols &C, uint32_t o,
-                                             uint32_t i, uint32_t se_rel, uint64_t base, uint64_t &badf) {
-  const uint32_t *q = reinterpret_cast<const uint32_t *>(m.lds) + (o >> 2);
-  const uint32_t w = __builtin_amdgcn_alignbit(q[1], q[0], (o & 3u) * 8u);
-  const uint32_t tm = ~w & 0x808080u;
-  if (!tm || o + 16u > IMG || o + 16u > se_rel) return emit_frame_fast(P, m, m.A + o, base + i, badf);
-  if (i >= C.lim) return true;
-  const uint32_t k = ((uint32_t)__builtin_ctz(tm) >> 3) + 1u;
-  const uint32_t L = ((w & 0x7Fu) | ((w >> 1) & 0x3F80u) | ((w >> 2) & 0x1FC000u)) & ((1u << (7u * k)) - 1u);
-  const uint32_t id = (w >> (8u * k)) & 0xFFu;
-  const uint32_t po = o + k + 1u, pl = L - 1u;
-  const bool partial = id == 2u && L > se_rel - o - k;  // a blob cut by the stream end (H_TAIL_BLOB)
-  C.poff[i] = m.A + po;
-  C.plen[i] = pl;
-  C.type[i] = (uint8_t)(id | (partial ? DRP_FRAME_PARTIAL : 0u));
-  if (id != 1u) return true;
-  ChangeCols c;
-  if (!change_fast32(m.lds, po, pl, se_rel < IMG ? se_rel : IMG, c)) return false;
-  C.ko[i] = c.key_off;
-  C.kl[i] = c.key_len;
-  C.so[i] = c.subset_off;
-  C.sl[i] = c.subset_len;
-  C.vo[i] = c.value_off;
-  C.vl[i] = c.value_len;
-  C.ch[i] = c.change;
-  C.fr[i] = c.from;
-  C.to[i] = c.to;
-  uint32_t fl = c.flags;
-  if (c.err == DRP_ERR_REQUIRED) fl |= DRP_F_MISSING;
-  C.fl[i] = (uint8_t)fl;
-  if (c.err) badf = base + i < badf ? base + i : badf;
-  return true;
 }
 
 // ---- sparse tiles: frames decoded from HBM, no staging ---------------------------------------
@@ -2607,51 +2306,31 @@ __global__ __launch_bounds__(256) void emit_sparse(DecodeParams P) {
   if (tid < SP_TPB && fail[tid]) P.tile_sparse[t0 + tid] = 0;  // ((t0 + tid < ntiles: fail is only set for tiles)
 }
 
-#ifndef DRP_EMIT32
-#define DRP_EMIT32 0  // 1: frames in 32-bit tile-relative form (A/B: 8.59 vs 8.50 ms C2, 2.56 vs 2.51 ms C5 decode)
-#endif
 
-#ifndef DRP_EMIT_FAST_WAVES
-#define DRP_EMIT_FAST_WAVES 6  // the fast emit kernel holds no general Change decoder: 6 waves/SIMD, no spills
-#endif
-#ifndef DRP_EMIT_XCD
-#define DRP_EMIT_XCD 1  // fast emit: XCD-contiguous tile order
-#endif
-#ifndef DRP_EMIT_SPLIT
-#define DRP_EMIT_SPLIT 1  // 0: one emit kernel with the general decoder inline (5 waves/SIMD)
-#endif
-// FAST (every tile): Change payloads in decode_change_fast's shapes are decoded here; a tile with
-// any other frame (or too many frames to list) is appended to P.vlist and re-emitted whole by the
-// general instance (!FAST, over that list), which rewrites the same values for the rest.
-template <bool FAST>
-__global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) void emit_tiles(DecodeParams P) {
+// The general emit: the tiles emit_lean / emit_sparse list (P.vlist; null: every tile), each
+// re-emitted whole from its verified entries with the general Change decoder (decode_change: any
+// field order, repeated or unknown fields, errors).
+__global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint16_t lst[LCAP];
   __shared__ uint32_t wsum[NT / WAVE];
-  __shared__ uint32_t defer;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wid = tid >> 6;
   uint64_t tl_ = P.stats && tid == 0 ? __builtin_amdgcn_s_memtime() : 0;
   if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
-  const uint32_t nwork = (!FAST && P.vlist) ? *P.vlist_n : 0u;
-  for (uint32_t wi = blockIdx.x; (!FAST && P.vlist) ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
-  uint64_t t = (!FAST && P.vlist) ? P.vlist[wi] : wi;
-  if (FAST && DRP_EMIT_XCD) {  // workgroups go to the 8 XCDs round-robin: give each XCD one
-    const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = wi % 8u;  // contiguous eighth, so
-    t = (uint64_t)x * q + min(x, r) + wi / 8u;  // neighbouring tiles share an L2 (column lines)
-  }
-  if (!FAST) bsync();  // the previous tile's LDS reads are done
+  const uint32_t nwork = P.vlist ? *P.vlist_n : 0u;
+  for (uint32_t wi = blockIdx.x; P.vlist ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
+  const uint64_t t = P.vlist ? P.vlist[wi] : wi;
+  bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
   if (t >= ntiles) continue;  // (whole workgroup)
-  if (FAST && P.tile_sparse && P.tile_sparse[t]) continue;  // emit_sparse wrote it
   const uint64_t se = G.se, A = G.A;
   // the records load with the tile bytes, not after them
   const uint64_t base = ldc(P.tile_base + t);
   const uint32_t k0 = P.tile_k ? P.tile_k[t] : 0u;  // threads before e_t's (verify_lite)
   const uint8_t eb = tid < k0 ? (uint8_t)0xFF : P.ent[t * NT + tid];  // exact entry of this thread's bytes
   const uint8_t en = P.ent_n[t * NT + tid];   // exact frames from it (kernel 2)
-  if (FAST && tid == 0) defer = 0;
   stage_glds(P, G, buf);
   const Img m{buf, P.bytes, A, se};
   const uint64_t lb = A + (uint64_t)tid * SEGB, s1 = lb + SEGB;
@@ -2671,10 +2350,6 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
   uint32_t nch = 0, nbl = 0;
   uint64_t badf = ~0ull;
   const bool listed = count_t <= LCAP;
-  if (FAST && !listed) {  // very dense tile: the general kernel emits it per thread
-    if (tid == 0) P.vlist[atomicAdd(P.vlist_n, 1u)] = (uint32_t)t;
-    continue;
-  }
   // this thread's frames, in order: list them (or, for very dense tiles, emit them here)
   if (n) {
     uint32_t i = woff + ni - n;
@@ -2684,7 +2359,7 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
       if (h.kind != H_VALID && h.kind != H_TAIL_BLOB) break;
       if (h.id != 0) {
         if (listed) lst[i] = (uint16_t)(p - A);
-        else if constexpr (!FAST) emit_frame(P, m, p, base + i, nch, nbl, badf);
+        else emit_frame(P, m, p, base + i, nch, nbl, badf);
         i++;
       }
       if (h.kind != H_VALID) break;
@@ -2693,24 +2368,7 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
   }
   if (listed) {
     bsync();
-    if constexpr (FAST) {
-      bool ok = true;
-      if (DRP_EMIT32) {
-        const RowCols C = row_cols(P, base);
-        const uint32_t se_rel = (uint32_t)umin64(se - A, 0x7FFFFFFFull);
-        for (uint32_t i = tid; i < count_t; i += NT) ok &= emit_frame32(P, m, C, lst[i], i, se_rel, base, badf);
-      } else {
-        for (uint32_t i = tid; i < count_t; i += NT) ok &= emit_frame_fast(P, m, A + lst[i], base + i, badf);
-      }
-      if (!ok) defer = 1;
-      bsync();
-      if (defer) {  // the general kernel re-emits the whole tile (its payload errors too)
-        if (tid == 0) P.vlist[atomicAdd(P.vlist_n, 1u)] = (uint32_t)t;
-        continue;
-      }
-    } else {
-      for (uint32_t i = tid; i < count_t; i += NT) emit_frame(P, m, A + lst[i], base + i, nch, nbl, badf);
-    }
+    for (uint32_t i = tid; i < count_t; i += NT) emit_frame(P, m, A + lst[i], base + i, nch, nbl, badf);
   }
   PHASE(13);
   (void)nch;
@@ -2729,10 +2387,7 @@ __global__ __launch_bounds__(NT, FAST ? DRP_EMIT_FAST_WAVES : DRP_EMIT_WAVES) vo
 // 32-bit image offsets, and column stores at the tile's row base plus a 32-bit byte offset. Any
 // other shape (field order, repeated or unknown fields, varints of more than 5 bytes, headers
 // near the image end, length varints of more than 3 bytes) sends the whole tile to the general
-// kernel (emit_tiles<false> over P.vlist), which writes the same columns for the rest.
-#ifndef DRP_EMIT_LEAN
-#define DRP_EMIT_LEAN 1  // 0: emit_tiles<true> as the fast emit (A/B)
-#endif
+// kernel (emit_tiles over P.vlist), which writes the same columns for the rest.
 #ifndef DRP_EMIT_LEAN_WAVES
 #define DRP_EMIT_LEAN_WAVES 6
 #endif
@@ -3169,9 +2824,6 @@ __device__ __forceinline__ uint64_t seg_tile_walk(const DecodeParams &P, const T
   return pos;
 }
 
-#ifndef DRP_SEG_TABLE
-#define DRP_SEG_TABLE 1  // 0: every candidate chain walked frame by frame (A/B)
-#endif
 __global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ SegWalkLds T;
@@ -3242,9 +2894,9 @@ __global__ __launch_bounds__(NT) void seg_walk(DecodeParams P, SegRange R) {
     if (R.ctile && wid == 0)  // (each candidate's position entering this tile, for seg_claims_par)
       R.ctile[((G.A - sb0) / TILE + ta - R.t0) * SEG_CAND + lane] =
           !is_pos(pos) ? CT_END : (pos >= send ? CT_PAST : (uint32_t)(pos - sb0));
-    if (DRP_SEG_TABLE && table) pos = seg_tile_walk(P, G, buf, T, pos, umin64(G.A + TILE, send), steps);
+    if (table) pos = seg_tile_walk(P, G, buf, T, pos, umin64(G.A + TILE, send), steps);
     if (wid == 0) {
-      if (!(DRP_SEG_TABLE && table)) {
+      if (!(1 && table)) {
         const Img mt{buf, P.bytes, G.A, G.se};
         pos = seg_advance_n(mt, pos, umin64(G.A + TILE, send), steps);
       }
@@ -3424,9 +3076,6 @@ __global__ __launch_bounds__(SEG_STB) void seg_stitch(DecodeParams P, SegRange R
 // the verify pass after the repair proves such a tile from its records alone (verify_lite) instead
 // of re-walking it; a tile where the chain ends (an error or a frame cut by the stream end) keeps
 // its records and is re-walked by verify_counts.
-#ifndef DRP_SEGC_LEAN
-#define DRP_SEGC_LEAN 1  // 0: the chain walk by hdr_fast only (A/B)
-#endif
 __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   __shared__ uint64_t lcl[SEG_GMAX];
@@ -3473,7 +3122,6 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
       // the current thread's record is kept in registers and written once when the chain leaves
       // its bytes (LDS writes only: no read-modify-write on the walk's serial path)
       uint32_t cth = NT, ce = 0, cn = 0, cc = 0;
-#if DRP_SEGC_LEAN
       // 32-bit tile-relative steps while the header's 16-byte window lies in the image and the
       // stream and its varint has 1..3 bytes (hdr_fast's grammar); any other header takes hdr_fast.
       // The step is written without data-dependent branches: the conditions are combined with &
@@ -3522,35 +3170,6 @@ __global__ __launch_bounds__(NT) void seg_claims(DecodeParams P, SegRange R) {
         }
         if (!term && !far) p = G.A + o;
       }
-#else
-      auto note = [&](uint32_t o, uint32_t id) {  // (the frame at tile offset o)
-        const uint32_t th = o / SEGB;
-        if (th != cth) {
-          if (cth < NT) {
-            re[cth] = (uint8_t)ce;
-            rn[cth] = (uint8_t)cn;
-            rc[cth] = (uint8_t)cc;
-          }
-          cth = th;
-          ce = o % SEGB;
-          cn = 0;
-          cc = 0;
-        }
-        cn += id != 0;
-        cc += id == 1;
-        if (P.stats) n_walk++;
-      };
-      while (is_pos(p) && p < lim && p < m.se) {
-        const Hdr h = hdr_fast(m, p);
-        if (h.kind != H_VALID) {
-          p = term_of(h, p);
-          ok = 0;
-          break;
-        }
-        note((uint32_t)(p - G.A), h.id);
-        p = h.succ;
-      }
-#endif
       if (P.stats) {
         c_walk += __builtin_amdgcn_s_memtime() - t_w;
         n_tiles++;
@@ -3744,14 +3363,13 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
     drp_dbg_mark("tile_stream_kernel", st);
     Q.tile_stream = tile_stream;
   }
-#if DRP_CLAIMS_FAST
   // interior tiles in the fast form (or by the region walkers); the edge and dense tiles they list
   // in the general one
   if (Q.walk_rp) {
     const hipError_t e = drp_launch_claims_walk(&Q, nt_max, st);
     if (e != hipSuccess) return e;
     drp_dbg_mark("claims_walk", st);
-  } else if (DRP_CHANGE_FILLS && Q.change_checks)
+  } else if (Q.change_checks)
     hipLaunchKernelGGL(spec::claims_fast<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
   else
     hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
@@ -3776,11 +3394,6 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
       fclose(f);
     }
   }
-#else
-  Q.work = nullptr;
-  hipLaunchKernelGGL(spec::spec_claims, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
-  drp_dbg_mark("spec_claims", st);
-#endif
   if (Q.vlist) {  // records-only verification, then verify_counts on the tiles it lists
     const uint64_t nb = (nt_max * spec::VL_G + spec::VL_BLK - 1) / spec::VL_BLK;
     hipLaunchKernelGGL(spec::verify_lite, dim3((uint32_t)nb), dim3(spec::VL_BLK), 0, st, Q);
@@ -3838,7 +3451,7 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
                                       Q.overflow, st);
   if (e != hipSuccess) return e;
   drp_dbg_mark("tile_scan(count)", st);
-  if (DRP_EMIT_SPLIT && Q.vlist) {  // the fast kernel, then the general one on the tiles it lists
+  if (Q.vlist) {  // the fast kernel, then the general one on the tiles it lists
     e = hipMemsetAsync(Q.vlist_n, 0, 4, st);
     if (e != hipSuccess) return e;
     if (spec::SP_FRAMES && Q.tile_sparse) {  // sparse tiles first (no staging), then every other tile
@@ -3848,89 +3461,24 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
     } else {
       Q.tile_sparse = nullptr;
     }
-    if (DRP_EMIT_LEAN)
-      hipLaunchKernelGGL(spec::emit_lean,
-                         dim3((uint32_t)(Q.change_checks ? (nt_max + spec::EMIT_LONG_TPW - 1) / spec::EMIT_LONG_TPW
-                                                         : nt_max)),
-                         dim3(spec::NT), 0, st, Q);
-    else
-      hipLaunchKernelGGL(spec::emit_tiles<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+    hipLaunchKernelGGL(spec::emit_lean,
+                       dim3((uint32_t)(Q.change_checks ? (nt_max + spec::EMIT_LONG_TPW - 1) / spec::EMIT_LONG_TPW
+                                                       : nt_max)),
+                       dim3(spec::NT), 0, st, Q);
     drp_dbg_mark("emit_fast", st);
-    hipLaunchKernelGGL(spec::emit_tiles<false>, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0,
+    hipLaunchKernelGGL(spec::emit_tiles, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0,
                        st, Q);
-    drp_dbg_mark("emit_tiles<false>", st);
+    drp_dbg_mark("emit_tiles", st);
   } else {
     Q.vlist = nullptr;  // every tile in the general form
-    hipLaunchKernelGGL(spec::emit_tiles<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
-    drp_dbg_mark("emit_tiles<false>", st);
+    hipLaunchKernelGGL(spec::emit_tiles, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+    drp_dbg_mark("emit_tiles", st);
   }
   e = drp_launch_tile_scan(Q.tile_nch, Q.tile_prefix, nstreams, nt_max, scan_tmp, Q.tile_nch_base, ~0ull, Q.overflow, st);
   if (e != hipSuccess) return e;
   drp_dbg_mark("tile_scan(nch)", st);
   return drp_launch_stream_counts(Q.tile_prefix, nstreams, Q.tile_count, Q.tile_base, Q.tile_nch, Q.tile_nch_base,
                                   Q.scount, st, Q.counter + 3);
-}
-
-// Measurement only (drp_probe_overlap): one launch in which workgroup 16 k + r (r < 8) runs the
-// claims of tile 8 k + r and workgroup 16 k + 8 + r the lean emit of tile 8 (k - lag / 8) + r: on the
-// round-robin XCD placement both of a tile's workgroups share one XCD, the emit `lag` tiles behind
-// the claims, so the emit may read the tile from that XCD's L2 / the Infinity Cache. This is the
-// schedule a single-pass decode would have (timing only: the records and bases are the previous
-// decode's, rewritten with the same values).
-namespace drp {
-namespace spec {
-union DualLds {
-  FastLds c;
-  LeanLds e;
-};
-__global__ __launch_bounds__(NT, DRP_K1_WAVES) void probe_dual(DecodeParams P, uint64_t nt, uint32_t lag) {
-  __shared__ DualLds U;
-  const uint64_t b = blockIdx.x, k = b >> 4, r = b & 15u;
-  if (r < 8) {
-    const uint64_t t = 8 * k + r;
-    if (t >= nt) return;
-    const TileGeo G = tile_geo(P, t);
-    if (G.A < G.so || G.A + IMG > G.se) return;
-    uint32_t eb, en, ecn;
-    uint64_t cl;
-    (void)fast_claims<false>(P, G, t, U.c, eb, en, ecn, cl);
-  } else {
-    const int64_t t = (int64_t)(8 * k + (r - 8)) - (int64_t)lag;
-    if (t < 0) return;
-    emit_lean_tile(P, (uint64_t)t, U.e);
-  }
-}
-}  // namespace spec
-}  // namespace drp
-
-// Measurement hook (scripts/probe_overlap.py): the C2 claims kernel and the lean emit over every
-// tile of the last decode's parameters, alone and side by side on two streams (the claims kernel
-// rewrites the same records the emit reads, with the same values), each timed with events.
-extern "C" hipError_t drp_probe_overlap_launch(const DecodeParams *P, uint64_t nt_max, hipStream_t a, hipStream_t b,
-                                               hipEvent_t *ev) {
-  DecodeParams Q = *P;
-  Q.tile_stream = nullptr;
-  (void)hipEventRecord(ev[0], a);
-  hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, a, Q);
-  (void)hipEventRecord(ev[1], a);
-  hipLaunchKernelGGL(spec::emit_lean, dim3((uint32_t)nt_max), dim3(spec::NT), 0, a, Q);
-  (void)hipEventRecord(ev[2], a);
-  (void)hipStreamWaitEvent(b, ev[2], 0);
-  (void)hipEventRecord(ev[3], a);
-  hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, a, Q);
-  hipLaunchKernelGGL(spec::emit_lean, dim3((uint32_t)nt_max), dim3(spec::NT), 0, b, Q);
-  (void)hipEventRecord(ev[4], b);
-  (void)hipStreamWaitEvent(a, ev[4], 0);
-  (void)hipEventRecord(ev[5], a);
-  // one launch, both roles, emit lagging by `lag` tiles: the tail past nt covers the last tiles' emit
-  for (int v = 0; v < 3; v++) {
-    const uint32_t lag = v == 0 ? 0u : v == 1 ? 64u : 1024u;
-    const uint64_t groups = (nt_max + lag + 7) / 8;
-    (void)hipEventRecord(ev[6 + v], a);
-    hipLaunchKernelGGL(spec::probe_dual, dim3((uint32_t)(groups * 16)), dim3(spec::NT), 0, a, Q, nt_max, lag);
-  }
-  (void)hipEventRecord(ev[9], a);
-  return hipGetLastError();
 }
 
 extern "C" hipError_t drp_launch_blob_bytes(const uint8_t *type, const uint32_t *plen, uint64_t n, uint64_t *out,
@@ -3944,12 +3492,6 @@ extern "C" hipError_t drp_launch_blob_bytes(const uint8_t *type, const uint32_t 
 
 // Segmented repair of stream s from tile t0 (its first missed tile) to its end (the caller then
 // runs a verify pass). scratch: 2 * 64 * SEG_NMAX + SEG_NMAX + 1 words.
-#ifndef DRP_SEG_LINK
-#define DRP_SEG_LINK 1  // 0: the serial stitch only (A/B)
-#endif
-#ifndef DRP_SEGC_PAR
-#define DRP_SEGC_PAR 1  // 0: seg_claims walks every segment serially (A/B)
-#endif
 extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, uint64_t t0, uint64_t tl,
                                             uint64_t *scratch, uint32_t *ctile, uint64_t ctile_cap, hipStream_t st) {
   if (tl <= t0) return hipSuccess;
@@ -3970,10 +3512,10 @@ extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, u
   R.nseg = (n + R.G - 1) / R.G;
   R.cand = scratch;
   R.seg_entry = scratch + 2 * spec::SEG_CAND * spec::SEG_NMAX;
-  R.nidx = DRP_SEG_LINK ? reinterpret_cast<uint8_t *>(R.seg_entry + spec::SEG_NMAX + 2) : nullptr;  // (SEG_NMAX x 64 B, 16-B aligned)
+  R.nidx = 1 ? reinterpret_cast<uint8_t *>(R.seg_entry + spec::SEG_NMAX + 2) : nullptr;  // (SEG_NMAX x 64 B, 16-B aligned)
   R.seg_lane = reinterpret_cast<uint8_t *>(R.seg_entry + spec::SEG_NMAX + 2) + spec::SEG_NMAX * spec::SEG_CAND;
   // (the parallel seg_claims needs the stitch's tables and a position per candidate per tile)
-  R.ctile = DRP_SEGC_PAR && R.nidx && ctile && ctile_cap >= n * spec::SEG_CAND ? ctile : nullptr;
+  R.ctile = 1 && R.nidx && ctile && ctile_cap >= n * spec::SEG_CAND ? ctile : nullptr;
   DecodeParams Q = *P;
   hipLaunchKernelGGL(spec::seg_walk, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);
   if (R.nidx) hipLaunchKernelGGL(spec::seg_link, dim3((uint32_t)R.nseg), dim3(WAVE), 0, st, Q, R);

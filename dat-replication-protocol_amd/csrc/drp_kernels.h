@@ -150,8 +150,6 @@ hipError_t drp_launch_finalize(const uint8_t *bytes, const uint64_t *stream_off,
                                uint32_t abort_mask, hipStream_t st);
 hipError_t drp_launch_encode(const drp::EncodeParams *P, hipStream_t st);
 uint64_t drp_encode_out_blocks(uint64_t cap);
-hipError_t drp_probe_overlap_launch(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t a, hipStream_t b,
-                                    hipEvent_t *ev);
 // key hash + key flags for every change frame written (no-op when co->key_hash is NULL)
 hipError_t drp_launch_key_post(const uint8_t *bytes, const uint64_t *tile_prefix, uint64_t nstreams,
                                const uint64_t *tile_base, const uint64_t *tile_count, uint64_t cap,

@@ -34,6 +34,8 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* libdrp is built with -fvisibility=hidden: the declarations below are its only exports. */
+#pragma GCC visibility push(default)
 
 #define DRP_ABI_VERSION 4
 
@@ -304,6 +306,7 @@ int drp_index_allgather_multi(drp_ctx **ctxs, drp_comm **comms, int ngpu, const 
 int drp_index_allgather_host(drp_ctx **ctxs, drp_comm **comms, int ngpu, const drp_stream_stats *const *local,
                              uint64_t per_gpu, drp_stream_stats *global, uint64_t *base);
 
+#pragma GCC visibility pop
 #ifdef __cplusplus
 }
 #endif
