@@ -89,7 +89,11 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
     size_t want = n + n / 4 + 4096;
-    if (hipMalloc(&p, want) != hipSuccess) return false;
+    if (hipMalloc(&p, want) != hipSuccess) {
+      p = nullptr;
+      (void)hipGetLastError();  // (the failure is reported by the caller, not by a later launch)
+      return false;
+    }
     cap = want;
     return true;
   }
@@ -102,6 +106,39 @@ struct DevBuf {
   T *at(size_t off) const {
     return reinterpret_cast<T *>(static_cast<char *>(p) + off);
   }
+};
+
+// Page-locked host memory that only grows (the gather buffer of chunked host batches).
+struct PinBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t n) {
+    if (n <= cap) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n + n / 4 + 4096;
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+      p = nullptr;
+      (void)hipGetLastError();
+      return false;
+    }
+    cap = want;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// A host batch: one buffer, or the caller's chunks laid end to end (drp_decode_stage_v).
+struct HostSrc {
+  const uint8_t *flat = nullptr;
+  const drp_chunk *ch = nullptr;
+  std::vector<uint64_t> start;  // chunk k's first batch offset (chunks only)
+  uint64_t n = 0;
 };
 
 bool is_device_ptr(const void *p) {
@@ -146,7 +183,9 @@ struct drp_ctx {
   // claims kernel: the region walkers (drp_walk.hip) for batches of at least walk_min tiles,
   // claims_fast below; DRP_CLAIMS=walk / fast forces one (A/B, tests)
   uint64_t walk_min = 32768;
-  int claims_mode = 0;  // 0 auto, 1 walk, 2 fast
+  int claims_mode = 0;  // 0 auto, 1 walk (ring), 2 fast, 3 hop
+  int walk_rec = 1;     // the walkers' per-frame records and the record emission (DRP_WALK_REC)
+  DevBuf recbuf;
   uint64_t dirty_cap = ~0ull;
   bool stats = false;
   const char *trace_file = nullptr;
@@ -154,6 +193,7 @@ struct drp_ctx {
   uint32_t *ctile = nullptr;  // segmented repair: per-tile candidate positions (grown on demand)
   uint64_t ctile_cap = 0;
   DevBuf scratch, in_stage, out_stage, aux;
+  PinBuf gather;  // chunked host batches: the staged ranges, gathered (drp_decode_stage_v)
   DevBuf dec_cols;  // device columns of the staged host-batch decode (drp_decode_stage)
   double frames_per_byte = 0;  // density of the last staged batch (sizes the next one's columns)
   int blob_skip = DRP_BLOB_SKIP_AUTO;
@@ -230,7 +270,8 @@ int drp_open(int device, drp_ctx **out) {
   if (const char *e = getenv("DRP_CASCADE_MIN")) c->cascade_min = (uint32_t)strtoul(e, nullptr, 10);
   if (const char *e = getenv("DRP_JUMP_MIN")) c->jump_min = strtoll(e, nullptr, 10);
   if (const char *e = getenv("DRP_WALK_MIN")) c->walk_min = strtoull(e, nullptr, 10);
-  if (const char *e = getenv("DRP_CLAIMS")) c->claims_mode = strcmp(e, "walk") == 0 ? 1 : strcmp(e, "fast") == 0 ? 2 : 0;
+  if (const char *e = getenv("DRP_WALK_REC")) c->walk_rec = atoi(e);
+  if (const char *e = getenv("DRP_CLAIMS")) c->claims_mode = strcmp(e, "walk") == 0 ? 1 : strcmp(e, "fast") == 0 ? 2 : strcmp(e, "hop") == 0 ? 3 : 0;
   if (const char *e = getenv("DRP_DIRTY_CAP")) c->dirty_cap = strtoull(e, nullptr, 10);
   c->trace_file = getenv("DRP_TRACE_FILE");
   if (getenv("DRP_STATS") && hipMalloc((void **)&c->dstats, 64 * 8) == hipSuccess) c->stats = true;
@@ -244,9 +285,11 @@ void drp_close(drp_ctx *c) {
   (void)hipStreamSynchronize(c->st);
   c->scratch.release();
   c->in_stage.release();
+  c->gather.release();
   c->out_stage.release();
   c->aux.release();
   c->dec_cols.release();
+  c->recbuf.release();
   if (c->dstats) (void)hipFree(c->dstats);
   if (c->ctile) (void)hipFree(c->ctile);
   for (auto &e : c->ev) (void)hipEventDestroy(e);
@@ -305,7 +348,7 @@ int drp_set_blob_skip(drp_ctx *c, int mode) {
 // scratch layout for a decode of `nbytes` over `ns` streams
 struct DecLayout {
   uint64_t ntiles_max;
-  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, tstream, ent, tk, tsp, fmiss, segw, scan_tmp, walk, total;
+  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, tstream, ent, tk, tsp, fmiss, segw, scan_tmp, walk, went, trec, trok, total;
   uint64_t nsg;
 };
 static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
@@ -330,6 +373,9 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
                                                                 // next-candidate tables, lanes (SEG_NMAX)
   L.scan_tmp = o; o += al((L.ntiles_max / 4096 + 2) * 8);  // tile scans: block sums
   L.walk = o; o += al((ns + 2) * 8);                         // region walkers: per-stream region prefix
+  L.went = o; o += al((L.ntiles_max + ns + 2) * 8);          // region walkers: entries
+  L.trec = o; o += al(L.ntiles_max * 4);                     // first record per tile (region walkers)
+  L.trok = o; o += al(L.ntiles_max);                         // record emission marks (verify_lite)
   L.total = o;
   return L;
 }
@@ -599,9 +645,20 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.cascade_min = c->cascade_min;
   P.jump_min = c->jump_min >= 0 ? (uint32_t)c->jump_min : (uint32_t)std::max<uint64_t>(64, NT / 512);
   P.dlist_cap = std::min<uint64_t>(NT, c->dirty_cap);  // (tests: DRP_DIRTY_CAP)
-  if (c->claims_mode == 1 || (c->claims_mode == 0 && NT >= c->walk_min)) {
+  if (c->claims_mode == 1 || c->claims_mode == 3 || (c->claims_mode == 0 && NT >= c->walk_min)) {
     P.walk_rp = c->scratch.at<uint64_t>(L.walk);
-    P.walk_tpr = drp_walk_tiles_per_region(NT);
+    P.walk_entry = c->scratch.at<uint64_t>(L.went);
+    P.walk_hop = c->claims_mode == 3 ? 1u : 0u;
+    P.walk_tpr = drp_walk_tiles_per_region(NT, (int)P.walk_hop);
+    // per-frame records: the record emission instead of reading the wire again (DRP_WALK_REC=0:
+    // off; a record buffer that cannot be had: off)
+    const uint64_t rcap = drp_walk_rec_cap(P.walk_tpr), nreg = NT / P.walk_tpr + ns + 1;
+    if (c->walk_rec && !P.walk_hop && c->recbuf.ensure(nreg * rcap * 32)) {
+      P.rec = c->recbuf.at<uint32_t>(0);
+      P.rec_cap = rcap;
+      P.tile_rec = c->scratch.at<uint32_t>(L.trec);
+      P.tile_recok = c->scratch.at<uint8_t>(L.trok);
+    }
   }
   unsigned long long *dstats = c->stats ? c->dstats : nullptr;
   if (dstats) P.stats = dstats;
@@ -618,6 +675,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     add(ctrl, 64, 0);
     add(P.dstamp, NT * 4, 0);
     add(P.first_miss, ns * 8, 0xFF);
+    if (P.tile_rec) add(P.tile_rec, NT * 4, 0xFF);
     if (dstats) add(dstats, 64 * 8, 0);
     CHK(drp_launch_prologue(B, stream_off, ns, tile_prefix, &cs, st));
   }
@@ -751,11 +809,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     for (unsigned k = 0; k < 5 && k < hs[0]; k++)
       fprintf(stderr, " | t=%llu e=%#llx claim=%#llx exit=%#llx", hs[1 + 6 * k], hs[2 + 6 * k], hs[3 + 6 * k],
               hs[4 + 6 * k]);
-    static const char *ph[] = {"k1_stage", "k1_cand", "k1_link", "k1_dense", "", "", "", "",
-                               "k2_stage", "k2_entry", "k2_link", "k3_stage", "k3_link", "k3_emit"};
-    for (int k = 0; k < 14; k++)
-      if (ph[k][0]) fprintf(stderr, " %s=%.0f", ph[k], (double)hs[40 + k] / (double)(h[0] ? h[0] : 1));
-    fprintf(stderr, " walk: syncs=%llu deaths=%llu first death at %#llx lds=%#llx hbm=%#llx w|lane|o=%#llx", hs[31], hs[32],
+    fprintf(stderr, " walk: synced regions=%llu deaths=%llu first death at %#llx lds=%#llx hbm=%#llx w|lane|o=%#llx", hs[31], hs[32],
             hs[36], hs[37], hs[38], hs[39]);
     fprintf(stderr, " repairs=%d (avg cycles per tile) link_rounds=%llu max=%llu tiles_over8=%llu restart_tiles=%llu"
             " jump_tiles=%llu seg_claims: walk_cycles=%llu frames=%llu tiles=%llu wg_cycles=%llu\n", pass, hs[56],
@@ -950,6 +1004,30 @@ static uint64_t stage_cap(const drp_ctx *c, uint64_t m) {
   return (uint64_t)((double)m * dens) + 1024;
 }
 
+// Batch bytes [a, a + len) into device memory at dst (asynchronously on st). A chunked batch's
+// range is gathered into the ctx's page-locked buffer first (*copied counts those host bytes),
+// so the copy into HBM runs by DMA and only the staged ranges are ever copied on the host.
+static int h2d_range(drp_ctx *c, const HostSrc &H, uint64_t a, uint64_t len, void *dst, hipStream_t st,
+                     uint64_t *copied) {
+  if (!len) return DRP_OK;
+  if (H.flat) {
+    CHK(hipMemcpyAsync(dst, H.flat + a, len, hipMemcpyDefault, st));
+    return DRP_OK;
+  }
+  if (!c->gather.ensure(len)) return DRP_E_NOMEM;
+  CHK(hipStreamSynchronize(st));  // (the buffer's previous range has left)
+  uint8_t *g = static_cast<uint8_t *>(c->gather.p);
+  uint64_t k = (uint64_t)(std::upper_bound(H.start.begin(), H.start.end(), a) - H.start.begin()) - 1;
+  for (uint64_t at = a, end = a + len; at < end; k++) {
+    const uint64_t s0 = H.start[k], take = std::min(end, s0 + H.ch[k].n) - at;
+    memcpy(g + (at - a), H.ch[k].bytes + (at - s0), take);
+    at += take;
+  }
+  *copied += len;
+  CHK(hipMemcpyAsync(dst, g, len, hipMemcpyHostToDevice, st));
+  return DRP_OK;
+}
+
 // Pass-through of in-batch blob payloads (drp_set_blob_skip): bytes [pos, n) of a host batch are
 // staged and decoded piece by piece. A piece ends kPieceMargin past where the next blob header
 // is expected (the distance from a piece's start to its blob header, learned); when the
@@ -958,7 +1036,7 @@ static uint64_t stage_cap(const drp_ctx *c, uint64_t m) {
 // resumed at that frame. The rows of all pieces are consecutive, as a whole-batch decode
 // writes them (a blob the batch holds whole loses the PARTIAL mark its piece gave it).
 // DRP_E_RETRY: the capacity guess was short; the caller stages the batch whole.
-static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t pos, drp_carry *carry,
+static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *carry,
                         uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail) {
   hipStream_t st = c->st;
   auto &S = c->staged;
@@ -967,6 +1045,8 @@ static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t p
   uint64_t *soff = c->aux.at<uint64_t>(0);
   uint64_t *ent = c->aux.at<uint64_t>(16);
   drp_stream_result *dres = c->aux.at<drp_stream_result>(stage_meta);
+  const uint64_t n = H.n;
+  uint64_t copied = 0;
   const uint64_t cap = stage_cap(c, n - pos);
   if (!c->dec_cols.ensure(carve_bytes(cap))) return DRP_E_NOMEM;
   carve(c->dec_cols, cap, S.fr, S.co);
@@ -984,7 +1064,7 @@ static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t p
     const uint64_t pe = std::min(n, pos + want), ps = pos & ~15ull, mp = pe - ps;
     if (!c->in_stage.ensure(mp + 64)) return DRP_E_NOMEM;
     const double t0 = now_ms();
-    CHK(hipMemcpyAsync(c->in_stage.p, bytes + ps, mp, hipMemcpyDefault, st));
+    if (const int rc = h2d_range(c, H, ps, mp, c->in_stage.p, st, &copied)) return rc;
     uint64_t hv[3] = {0, mp, pos - ps};
     CHK(hipMemcpyAsync(soff, hv, 16, hipMemcpyHostToDevice, st));
     CHK(hipMemcpyAsync(ent, hv + 2, 8, hipMemcpyHostToDevice, st));
@@ -1075,6 +1155,7 @@ static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t p
   c->timing.h2d_ms = h2d_ms;
   c->timing.h2d_bytes = staged;
   c->timing.h2d_skipped = skipped;
+  c->timing.host_copied = copied;
   c->blob_heavy = skipped * 4 >= n;  // (AUTO: keep skipping while it pays)
   c->frames_per_byte = (double)rows / (double)(n - S.pieces[0].second);
   S.rows = S.nf0 + rows;
@@ -1085,9 +1166,11 @@ static int stage_pieces(drp_ctx *c, const uint8_t *bytes, uint64_t n, uint64_t p
 // Decode a host batch (bytes [a, n), a = the 16-byte-aligned start of the bytes after a leading
 // blob continuation) into the ctx's device columns. The frame capacity starts at a guess and is
 // grown to the exact count when the first launch overflows it (the count is exact either way).
-static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *carry, uint64_t *n_frames,
+static int stage_decode(drp_ctx *c, const HostSrc &H, drp_carry *carry, uint64_t *n_frames,
                         uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail) {
   hipStream_t st = c->st;
+  const uint64_t n = H.n;
+  const uint8_t *bytes = H.flat;
   auto &S = c->staged;
   S.rows = S.nf0 = 0;
   S.pieces.clear();
@@ -1097,6 +1180,7 @@ static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry 
   carry->frame_bytes = 0;
   c->timing.h2d_bytes = 0;
   c->timing.h2d_skipped = 0;
+  c->timing.host_copied = 0;
   const uint64_t brem = carry->blob_remaining;
   // A blob continuation (decode.js _id == 2 with _missing > 0 across _write calls) is row 0.
   if (brem) {
@@ -1113,14 +1197,14 @@ static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry 
       return DRP_OK;
     }
   }
-  const bool host_in = !is_device_ptr(bytes) || ((uintptr_t)bytes & 15);
+  const bool host_in = !bytes || !is_device_ptr(bytes) || ((uintptr_t)bytes & 15);
   if (host_in && n - brem >= kPiecesMin &&
       (c->blob_skip == DRP_BLOB_SKIP_ALWAYS ||
        (c->blob_skip == DRP_BLOB_SKIP_AUTO && (c->blob_heavy || c->frames_per_byte == 0)))) {
     // (AUTO: a ctx's first batch probes in pieces too; pieces grow geometrically while no blob
     // is met, so a batch without blobs costs a few more launches once)
     const drp_carry in = *carry;
-    const int rc = stage_pieces(c, bytes, n, brem, carry, n_frames, err_frame, err_code, err_detail);
+    const int rc = stage_pieces(c, H, brem, carry, n_frames, err_frame, err_code, err_detail);
     if (rc != DRP_E_RETRY) return rc;
     *carry = in;  // (capacity: staged whole below)
     *err_frame = ~0ull;
@@ -1130,13 +1214,14 @@ static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry 
   }
   // the continuation's payload bytes are pass-through: only [a, n) goes to the device
   const uint64_t a = brem & ~15ull, m = n - a;
-  const uint8_t *dbytes = bytes + a;
+  const uint8_t *dbytes = bytes ? bytes + a : nullptr;
   float h2d_ms = 0;
+  uint64_t copied = 0;
   if (host_in) {
     if (!c->in_stage.ensure(m + 64)) return DRP_E_NOMEM;
     const double t0 = now_ms();
     if (m) {
-      CHK(hipMemcpyAsync(c->in_stage.p, bytes + a, m, hipMemcpyDefault, st));
+      if (const int rc = h2d_range(c, H, a, m, c->in_stage.p, st, &copied)) return rc;
       CHK(hipStreamSynchronize(st));
     }
     h2d_ms = (float)(now_ms() - t0);
@@ -1190,6 +1275,7 @@ static int stage_decode(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry 
   }
   c->timing.h2d_ms = h2d_ms;
   c->timing.h2d_bytes = host_in ? m : 0;
+  c->timing.host_copied = copied;
   c->frames_per_byte = m ? (double)r.frames / (double)m : 0.0;
   const uint64_t bad = (r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0;
   S.pieces.emplace_back(0, a);
@@ -1263,7 +1349,33 @@ int drp_decode_stage(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *ca
                      uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail) {
   if (!c || !carry || !n_frames || !err_frame || !err_code || !err_detail || (!bytes && n)) return DRP_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
-  return stage_decode(c, bytes, n, carry, n_frames, err_frame, err_code, err_detail);
+  HostSrc H;
+  H.flat = bytes;
+  H.n = n;
+  return stage_decode(c, H, carry, n_frames, err_frame, err_code, err_detail);
+}
+
+int drp_decode_stage_v(drp_ctx *c, const drp_chunk *chunks, uint64_t nchunks, drp_carry *carry, uint64_t *n_frames,
+                       uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail) {
+  if (!c || !carry || !n_frames || !err_frame || !err_code || !err_detail || (!chunks && nchunks)) return DRP_E_INVAL;
+  HostSrc H;
+  H.ch = chunks;
+  H.start.resize(nchunks);
+  for (uint64_t k = 0; k < nchunks; k++) {
+    if (!chunks[k].bytes && chunks[k].n) return DRP_E_INVAL;
+    H.start[k] = H.n;
+    H.n += chunks[k].n;
+  }
+  if (nchunks == 1) {  // (one chunk: the flat form)
+    H.flat = chunks[0].bytes;
+    H.ch = nullptr;
+  }
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  if (!H.n) {
+    HostSrc E;
+    return stage_decode(c, E, carry, n_frames, err_frame, err_code, err_detail);
+  }
+  return stage_decode(c, H, carry, n_frames, err_frame, err_code, err_detail);
 }
 
 int drp_decode_fetch(drp_ctx *c, const drp_frames *frames, const drp_changes *cols, uint64_t first, uint64_t rows) {
@@ -1284,7 +1396,10 @@ int drp_decode_batch(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *ca
   const int key_post = c->key_post;
   if (cols->key_hash) c->key_post = DRP_KEY_POST_HASH;  // key hashes when the caller asks for them
   else if (key_post == DRP_KEY_POST_HASH) c->key_post = DRP_KEY_POST_OFF;
-  int rc = stage_decode(c, bytes, n, carry, n_frames, err_frame, err_code, err_detail);
+  HostSrc H;
+  H.flat = bytes;
+  H.n = n;
+  int rc = stage_decode(c, H, carry, n_frames, err_frame, err_code, err_detail);
   c->key_post = key_post;
   if (rc != DRP_OK) return rc;
   const uint64_t rows = c->staged.rows;

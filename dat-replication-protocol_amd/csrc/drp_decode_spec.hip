@@ -1669,13 +1669,14 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
   const uint32_t k = inside ? (uint32_t)((et - G.A) / SEGB) : NT;
   const uint32_t kr = k / 16u, ki = k % 16u;
   const uint32_t ew[4] = {e4.x, e4.y, e4.z, e4.w}, nw[4] = {n4.x, n4.y, n4.z, n4.w}, cw[4] = {c4.x, c4.y, c4.z, c4.w};
-  uint32_t bad = 0, sf = 0, sc = 0, rsm = 0, multi = 0;
+  uint32_t bad = 0, sf = 0, sc = 0, rsm = 0, multi = 0, sb = 0;
   const uint32_t s = r > kr ? 0u : (r == kr ? ki : 16u);  // this lane's threads from k on
 #pragma unroll
   for (uint32_t d = 0; d < 4; d++) {
     const uint32_t m = bytes_from(s, d);
     sf = __builtin_amdgcn_udot4(nw[d] & m, 0x01010101u, sf, false);
     sc = __builtin_amdgcn_udot4(cw[d] & m, 0x01010101u, sc, false);
+    sb = __builtin_amdgcn_udot4(nw[d] & ~m, 0x01010101u, sb, false);  // (frames before e_t's thread)
     rsm |= restart_bytes(ew[d]) << (4u * d);
     multi |= nw[d] & m & 0xFEFEFEFEu;  // a thread from k on with more than one frame
   }
@@ -1691,6 +1692,7 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
   for (uint32_t d = 1; d < VL_G; d <<= 1) {
     sf += shfl_xor32(sf, d);
     sc += shfl_xor32(sc, d);
+    sb += shfl_xor32(sb, d);
     bad |= shfl_xor32(bad, d);
     multi |= shfl_xor32(multi, d);
   }
@@ -1707,11 +1709,15 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
     if (lst) P.vlist[base + (uint32_t)__builtin_popcountll(lm & ((1ull << lane) - 1ull))] = (uint32_t)t;
   }
   if (r != 0 || lst) return;
+  // the record emission takes the tile when the claims kernel recorded every frame of it and its
+  // first record is the frame at e_t (no recorded frame in the threads before e_t's)
+  const bool recok = P.tile_recok && inside && sb == 0 && P.tile_rec[t] != REC_NONE;
+  if (P.tile_recok) P.tile_recok[t] = recok ? 1 : 0;
   P.tile_exit[t] = inside ? claim : et;
   P.tile_count[t] = sf;
   P.tile_nch[t] = sc;
   P.tile_k[t] = (uint8_t)k;
-  if (P.tile_sparse) P.tile_sparse[t] = (!multi && sf <= SP_FRAMES) ? 1 : 0;
+  if (P.tile_sparse) P.tile_sparse[t] = (!multi && sf <= SP_FRAMES && !recok) ? 1 : 0;
 }
 
 __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
@@ -1864,6 +1870,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     uint32_t n = 0;
     uint64_t R = walk(m, E, s1, n);
     link<true>(m, s1, NONE, et, E, R, n, xr, xf, P.overflow);
+    if (P.tile_rec && tid == 0) P.tile_rec[t] = REC_NONE;  // (the records below are not the claims kernel's)
     const bool carrier = is_pos(E) && E >= lb && E < s1 && E < G.se;  // (as spec_claims' records)
     P.ent[ix] = carrier ? (uint8_t)(E - lb) : (uint8_t)0xFF;  // exact, for kernel 3
     P.ent_n[ix] = carrier ? (uint8_t)(n & 0xFFFFu) : (uint8_t)0;
@@ -1932,6 +1939,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     P.tile_count[t] = count_t;
     P.tile_nch[t] = nch_t;
     if (P.tile_k) P.tile_k[t] = 0;  // (this kernel rewrote the records of the threads before e_t)
+    if (P.tile_recok) P.tile_recok[t] = 0;  // (the wire-reading emission takes it)
     if (P.tile_sparse) P.tile_sparse[t] = 0;  // (its records may be the slow path's: emit_tiles takes it)
   }
   }
@@ -2538,8 +2546,10 @@ __device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t
   uint32_t &defer = L.defer;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
   // emit_sparse wrote it (first: on C5 nearly every tile leaves here, after one load; the mark
-  // array covers the grid, and a stale mark past the tile count only ends a tile that ends anyway)
+  // array covers the grid, and a stale mark past the tile count only ends a tile that ends anyway),
+  // or the record emission writes it
   if (P.tile_sparse && P.tile_sparse[t]) return;
+  if (P.tile_recok && t < P.tile_prefix[P.nstreams] && P.tile_recok[t]) return;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   const TileGeo G = tile_geo(P, t);
   if (t >= ntiles) return;  // (whole workgroup)
@@ -3465,6 +3475,8 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
                        dim3((uint32_t)(Q.change_checks ? (nt_max + spec::EMIT_LONG_TPW - 1) / spec::EMIT_LONG_TPW
                                                        : nt_max)),
                        dim3(spec::NT), 0, st, Q);
+    e = drp_launch_emit_rec(&Q, nt_max, st);  // (the tiles with records; emit_lean skipped them)
+    if (e != hipSuccess) return e;
     drp_dbg_mark("emit_fast", st);
     hipLaunchKernelGGL(spec::emit_tiles, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0,
                        st, Q);
@@ -3517,6 +3529,10 @@ extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, u
   // (the parallel seg_claims needs the stitch's tables and a position per candidate per tile)
   R.ctile = 1 && R.nidx && ctile && ctile_cap >= n * spec::SEG_CAND ? ctile : nullptr;
   DecodeParams Q = *P;
+  if (Q.tile_rec) {  // (the repair rewrites these tiles' records: the region walkers' no longer apply)
+    const hipError_t e = hipMemsetAsync(Q.tile_rec + t0, 0xFF, (tl - t0) * 4, st);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(spec::seg_walk, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);
   if (R.nidx) hipLaunchKernelGGL(spec::seg_link, dim3((uint32_t)R.nseg), dim3(WAVE), 0, st, Q, R);
   hipLaunchKernelGGL(spec::seg_stitch, dim3(1), dim3(spec::SEG_STB), 0, st, Q, R);

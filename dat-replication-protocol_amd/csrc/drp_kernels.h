@@ -76,7 +76,16 @@ struct DecodeParams {
                          // pointer-jumping form (counted in counter[12]; drp_decode_spec.hip)
   // region walkers (drp_walk.hip): per-stream region prefix [nstreams + 1], tiles per region
   uint64_t *walk_rp;
+  uint64_t *walk_entry;  // region walkers: each region's entry (walk_sync)
+  uint32_t walk_hop;      // 1: the hop walkers (claims_hop), 0: the ring walkers (claims_walk)
   uint32_t walk_tpr;
+  // per-frame records (null: none): rec_cap 32-byte slots per region; per tile its first record
+  // (REC_NONE: none, the tile takes the wire-reading emission) and whether verification lets the
+  // record emission take it
+  uint32_t *rec;
+  uint64_t rec_cap;
+  uint32_t *tile_rec;
+  uint8_t *tile_recok;
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
   unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
 };
@@ -120,7 +129,9 @@ uint32_t drp_spec_retry_mask(void);
 uint32_t drp_spec_miss_bit(void);
 uint32_t drp_spec_cascade_bit(void);
 hipError_t drp_launch_claims_walk(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t st);
-uint32_t drp_walk_tiles_per_region(uint64_t nt_max);
+uint32_t drp_walk_tiles_per_region(uint64_t nt_max, int hop);
+hipError_t drp_launch_emit_rec(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t st);
+uint64_t drp_walk_rec_cap(uint32_t tpr);
 hipError_t drp_launch_spec_head(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                 uint32_t *tile_stream, hipStream_t st);
 // out[0] = payload bytes of the blob rows among rows [0, n) (out zeroed by the caller)

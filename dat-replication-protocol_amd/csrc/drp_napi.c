@@ -99,6 +99,141 @@ static napi_value js_open(napi_env env, napi_callback_info info) {
   return ext;
 }
 
+/* ---- per-environment state ------------------------------------------------------------
+ * Each Node environment (the main thread and every worker_thread) has its own pool of pinned
+ * column blocks and its own communicator cache (napi_set_instance_data): nothing mutable is
+ * shared between environments, so a worker's teardown cannot free what another thread uses. The
+ * state lives until the environment is torn down AND every column block it handed out has been
+ * released (an ArrayBuffer's finalizer may run after the environment's own), counted in `refs`. */
+#define COL_KEEP 4 /* idle column blocks kept for reuse; the rest go back to the driver */
+
+typedef struct {
+  pthread_mutex_t mu; /* (decode workers take blocks off the JS thread) */
+  int refs;           /* 1 for the live environment + one per block handed out */
+  int closing;        /* the environment is gone: released blocks are freed, not kept */
+  struct colblock *idle[COL_KEEP];
+  int nidle;
+  int comm_ng;
+  int comm_dev[64];
+  drp_comm *comm[64];
+} env_state;
+
+static void env_unref(env_state *st) {
+  pthread_mutex_lock(&st->mu);
+  const int last = --st->refs == 0;
+  pthread_mutex_unlock(&st->mu);
+  if (last) {
+    pthread_mutex_destroy(&st->mu);
+    free(st);
+  }
+}
+
+static env_state *env_get(napi_env env) {
+  void *p = NULL;
+  if (napi_get_instance_data(env, &p) != napi_ok) return NULL;
+  return (env_state *)p;
+}
+
+/* ---- pinned column blocks ----------------------------------------------------------------
+ * The decoded columns of a batch are copied from HBM into one page-locked block (drp_host_alloc:
+ * DMA at the PCIe rate, not the runtime's pageable bounce buffer) and handed to JS as external
+ * ArrayBuffers over it. The block goes back to its environment's pool when the last of those
+ * ArrayBuffers is collected; a batch takes the smallest idle block that fits, else a new one
+ * (sized to a power of two). */
+typedef struct colblock {
+  env_state *st;
+  void *p;
+  size_t cap;
+  int refs; /* ArrayBuffers over it still alive */
+} colblock;
+
+static colblock *col_get(env_state *st, size_t need) {
+  colblock *b = NULL;
+  pthread_mutex_lock(&st->mu);
+  int best = -1;
+  for (int i = 0; i < st->nidle; i++)
+    if (st->idle[i]->cap >= need && (best < 0 || st->idle[i]->cap < st->idle[best]->cap)) best = i;
+  if (best >= 0) {
+    b = st->idle[best];
+    st->idle[best] = st->idle[--st->nidle];
+  }
+  st->refs++; /* (the block is out) */
+  pthread_mutex_unlock(&st->mu);
+  if (!b) {
+    size_t cap = (size_t)1 << 20;
+    while (cap < need) cap <<= 1;
+    void *p = NULL;
+    b = (colblock *)calloc(1, sizeof *b);
+    if (!b || drp_host_alloc(cap, &p) != DRP_OK) {
+      free(b);
+      env_unref(st);
+      return NULL;
+    }
+    b->st = st;
+    b->p = p;
+    b->cap = cap;
+  }
+  b->refs = 0;
+  return b;
+}
+
+static void col_put(colblock *b) {
+  env_state *st = b->st;
+  pthread_mutex_lock(&st->mu);
+  colblock *drop = b;
+  if (!st->closing) {
+    if (st->nidle < COL_KEEP) {
+      st->idle[st->nidle++] = b;
+      drop = NULL;
+    } else { /* (keep the larger blocks) */
+      int small = 0;
+      for (int i = 1; i < st->nidle; i++)
+        if (st->idle[i]->cap < st->idle[small]->cap) small = i;
+      if (st->idle[small]->cap < b->cap) {
+        drop = st->idle[small];
+        st->idle[small] = b;
+      }
+    }
+  }
+  pthread_mutex_unlock(&st->mu);
+  if (drop) {
+    drp_host_free(drop->p);
+    free(drop);
+  }
+  env_unref(st);
+}
+
+/* finalizer of a column ArrayBuffer (JS thread) */
+static void col_finalize(napi_env env, void *data, void *hint) {
+  (void)data;
+  colblock *b = (colblock *)hint;
+  if (--b->refs > 0) return;
+  int64_t adj;
+  if (!b->st->closing) napi_adjust_external_memory(env, -(int64_t)b->cap, &adj);
+  col_put(b);
+}
+
+static void comm_cache_clear(env_state *st) {
+  for (int g = 0; g < st->comm_ng; g++) drp_comm_destroy(st->comm[g]);
+  st->comm_ng = 0;
+}
+
+static void env_finalize(napi_env env, void *data, void *hint) {
+  (void)env;
+  (void)hint;
+  env_state *st = (env_state *)data;
+  comm_cache_clear(st);
+  pthread_mutex_lock(&st->mu);
+  st->closing = 1;
+  while (st->nidle) {
+    colblock *b = st->idle[--st->nidle];
+    drp_host_free(b->p);
+    free(b);
+  }
+  pthread_mutex_unlock(&st->mu);
+  env_unref(st);
+}
+
 /* ---- decode ---------------------------------------------------------------------------- */
 
 enum { C_OFF, C_LEN, C_TYPE, C_KO, C_KL, C_SO, C_SL, C_VO, C_VL, C_CH, C_FR, C_TO, C_FL, NCOL };
@@ -114,26 +249,40 @@ typedef struct {
   napi_async_work work;
   napi_ref buf_ref, cb_ref;
   ctx_box *box;
-  const uint8_t *bytes;
-  size_t n;
+  env_state *st;
+  drp_chunk *chunks; /* the batch: the written chunks end to end (one: the buffer itself) */
+  uint64_t nchunks;
+  drp_chunk one;
   int rc;
   uint64_t nf, ef, rows;
   uint32_t ec, ed;
   drp_carry carry;
+  colblock *blk;  /* the pinned block the columns live in (NULL: malloc'd columns) */
   void *col[NCOL];
   int key_post;   /* also the key hash column (drp_set_key_post; the key flags are always on) */
   void *khash;
   double t_h2d, t_gpu, t_d2h, t_convert; /* ms: batch to HBM, decode kernels, columns back, u64 -> Number */
-  double h2d_bytes, h2d_skipped;         /* bytes staged into HBM / blob payload bytes left in host memory */
+  double h2d_bytes, h2d_skipped, host_copied; /* bytes staged into HBM / blob payload bytes left in host
+                                                 memory / bytes gathered from the chunks on the host */
 } dec_job;
 
 static void free_cols(dec_job *j) {
-  for (int i = 0; i < NCOL; i++) {
-    free(j->col[i]);
-    j->col[i] = NULL;
+  if (j->blk) {
+    colblock *b = j->blk;
+    j->blk = NULL;
+    if (b->refs == 0) col_put(b); /* (never handed to JS) */
+  } else {
+    for (int i = 0; i < NCOL; i++) free(j->col[i]);
+    free(j->khash);
   }
-  free(j->khash);
+  for (int i = 0; i < NCOL; i++) j->col[i] = NULL;
   j->khash = NULL;
+}
+
+static void free_job(dec_job *j) {
+  free_cols(j);
+  if (j->chunks != &j->one) free(j->chunks);
+  free(j);
 }
 
 /* the GPU part: decode, size the host columns from the frame count, fetch (worker thread) */
@@ -143,20 +292,39 @@ static double now_ms(void) {
   return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
 }
 
+static size_t al64(size_t x) { return (x + 63) & ~(size_t)63; }
+
+/* host columns for j->rows rows: one pinned block (the fetch then runs by DMA), else malloc */
+static int alloc_cols(dec_job *j) {
+  size_t need = 0;
+  for (int i = 0; i < NCOL; i++) need += al64(j->rows * COL_W[i] + 8);
+  if (j->key_post) need += al64(j->rows * 8 + 8);
+  j->blk = j->st ? col_get(j->st, need) : NULL;
+  if (j->blk) {
+    char *p = (char *)j->blk->p;
+    for (int i = 0; i < NCOL; i++) {
+      j->col[i] = p;
+      p += al64(j->rows * COL_W[i] + 8);
+    }
+    if (j->key_post) j->khash = p;
+    return DRP_OK;
+  }
+  for (int i = 0; i < NCOL; i++)
+    if (!(j->col[i] = malloc(j->rows * COL_W[i] + 8))) return DRP_E_NOMEM;
+  if (j->key_post && !(j->khash = malloc(j->rows * 8 + 8))) return DRP_E_NOMEM;
+  return DRP_OK;
+}
+
 static void dec_run(dec_job *j) {
   pthread_mutex_lock(&j->box->mu);
   /* the key flags always (the JS layer cuts ASCII keys from one latin1 string of the batch),
      the key hash column when asked */
   drp_set_key_post(j->box->c, j->key_post ? DRP_KEY_POST_HASH : DRP_KEY_POST_FLAGS);
-  j->rc = drp_decode_stage(j->box->c, j->bytes, j->n, &j->carry, &j->nf, &j->ef, &j->ec, &j->ed);
+  j->rc = drp_decode_stage_v(j->box->c, j->chunks, j->nchunks, &j->carry, &j->nf, &j->ef, &j->ec, &j->ed);
   if (j->rc == DRP_OK) {
     /* rows to expose: delivered frames plus a malformed Change (its flags say why) */
     j->rows = j->nf + ((j->ec == DRP_ERR_CHANGE || j->ec == DRP_ERR_REQUIRED) ? 1 : 0);
-    for (int i = 0; i < NCOL; i++) {
-      j->col[i] = malloc(j->rows * COL_W[i] + 8);
-      if (!j->col[i]) j->rc = DRP_E_NOMEM;
-    }
-    if (j->key_post && !(j->khash = malloc(j->rows * 8 + 8))) j->rc = DRP_E_NOMEM;
+    j->rc = alloc_cols(j);
     if (j->rc == DRP_OK) {
       drp_frames fr = {j->col[C_OFF], j->col[C_LEN], j->col[C_TYPE]};
       drp_changes co = {j->col[C_KO], j->col[C_KL], j->col[C_SO], j->col[C_SL], j->col[C_VO],
@@ -169,6 +337,7 @@ static void dec_run(dec_job *j) {
     j->t_h2d = tm.h2d_ms;
     j->h2d_bytes = (double)tm.h2d_bytes;
     j->h2d_skipped = (double)tm.h2d_skipped;
+    j->host_copied = (double)tm.host_copied;
     j->t_gpu = tm.total_ms;
     j->t_d2h = tm.d2h_ms;
   }
@@ -200,6 +369,20 @@ static void set_num(napi_env env, napi_value obj, const char *k, double v) {
   napi_set_named_property(env, obj, k, x);
 }
 
+/* one column as an external ArrayBuffer + typed array (JS thread): over the pinned block (its
+   last collected ArrayBuffer returns the block to the pool) or a malloc'd array */
+static int col_array(napi_env env, dec_job *j, void **slot, size_t bytes, napi_typedarray_type ty, napi_value *out) {
+  napi_value ab;
+  if (j->blk) {
+    if (napi_create_external_arraybuffer(env, *slot, bytes, col_finalize, j->blk, &ab) != napi_ok) return 0;
+    j->blk->refs++;
+  } else {
+    if (napi_create_external_arraybuffer(env, *slot, bytes, free_finalizer, NULL, &ab) != napi_ok) return 0;
+    *slot = NULL; /* owned by the ArrayBuffer now */
+  }
+  return napi_create_typedarray(env, ty, j->rows, ab, 0, out) == napi_ok;
+}
+
 /* build the JS result object; the columns move into external ArrayBuffers (JS thread) */
 static napi_value dec_result(napi_env env, dec_job *j) {
   napi_value res;
@@ -219,29 +402,40 @@ static napi_value dec_result(napi_env env, dec_job *j) {
     set_num(env, t, "h2d", j->t_h2d);
     set_num(env, t, "h2dBytes", j->h2d_bytes);
     set_num(env, t, "h2dSkipped", j->h2d_skipped);
+    set_num(env, t, "hostCopied", j->host_copied);
     set_num(env, t, "gpu", j->t_gpu);
     set_num(env, t, "d2h", j->t_d2h);
     set_num(env, t, "convert", j->t_convert);
+    set_num(env, t, "pinnedColumns", j->blk ? 1 : 0);
     napi_set_named_property(env, res, "t", t);
   }
-  for (int i = 0; i < NCOL; i++) {
-    napi_value ab, ta;
-    if (napi_create_external_arraybuffer(env, j->col[i], j->rows * COL_W[i] + 8, free_finalizer, NULL, &ab) !=
-        napi_ok)
-      return NULL;
-    j->col[i] = NULL; /* owned by the ArrayBuffer now */
-    if (napi_create_typedarray(env, COL_T[i], j->rows, ab, 0, &ta) != napi_ok) return NULL;
-    napi_set_named_property(env, res, COL_NAME[i], ta);
+  if (j->blk) {
+    int64_t adj;
+    napi_adjust_external_memory(env, (int64_t)j->blk->cap, &adj); /* (so V8 collects spent batches early) */
+    j->blk->refs++; /* (held while the arrays are made: a failure part way leaves it to free_cols) */
   }
-  if (j->khash) {
-    napi_value ab, ta;
-    if (napi_create_external_arraybuffer(env, j->khash, j->rows * 8 + 8, free_finalizer, NULL, &ab) != napi_ok)
-      return NULL;
+  int ok = 1;
+  for (int i = 0; i < NCOL && ok; i++) {
+    napi_value ta;
+    ok = col_array(env, j, &j->col[i], j->rows * COL_W[i] + 8, COL_T[i], &ta);
+    if (ok) napi_set_named_property(env, res, COL_NAME[i], ta);
+  }
+  if (ok && j->khash) {
+    napi_value ta;
+    ok = col_array(env, j, &j->khash, j->rows * 8 + 8, napi_biguint64_array, &ta);
+    if (ok) napi_set_named_property(env, res, "keyHash", ta);
+  }
+  if (j->blk) {
+    colblock *b = j->blk;
+    j->blk = NULL; /* (the arrays own it now) */
+    for (int i = 0; i < NCOL; i++) j->col[i] = NULL;
     j->khash = NULL;
-    if (napi_create_typedarray(env, napi_biguint64_array, j->rows, ab, 0, &ta) != napi_ok) return NULL;
-    napi_set_named_property(env, res, "keyHash", ta);
+    if (--b->refs == 0) { /* (no array was made) */
+      b->refs = 1;
+      col_finalize(env, NULL, b);
+    }
   }
-  return res;
+  return ok ? res : NULL;
 }
 
 static void dec_execute(napi_env env, void *data) {
@@ -265,33 +459,60 @@ static void dec_complete(napi_env env, napi_status status, void *data) {
       argv[1] = undef;
     }
   }
-  free_cols(j);
   napi_delete_reference(env, j->buf_ref);
   napi_delete_reference(env, j->cb_ref);
   napi_delete_async_work(env, j->work);
-  free(j);
+  free_job(j);
   napi_call_function(env, undef, cb, 2, argv, NULL);
+}
+
+/* the batch argument: a Buffer, or an Array of Buffers (the written chunks, end to end) */
+static int batch_chunks(napi_env env, napi_value v, dec_job *j) {
+  bool arr = false;
+  if (napi_is_array(env, v, &arr) != napi_ok) return 0;
+  if (!arr) {
+    void *bytes = NULL;
+    size_t n = 0;
+    if (napi_get_buffer_info(env, v, &bytes, &n) != napi_ok) return 0;
+    j->one.bytes = (const uint8_t *)bytes;
+    j->one.n = n;
+    j->chunks = &j->one;
+    j->nchunks = 1;
+    return 1;
+  }
+  uint32_t len = 0;
+  if (napi_get_array_length(env, v, &len) != napi_ok) return 0;
+  j->chunks = (drp_chunk *)calloc(len ? len : 1, sizeof(drp_chunk));
+  if (!j->chunks) return 0;
+  j->nchunks = len;
+  for (uint32_t k = 0; k < len; k++) {
+    napi_value e;
+    void *bytes = NULL;
+    size_t n = 0;
+    if (napi_get_element(env, v, k, &e) != napi_ok || napi_get_buffer_info(env, e, &bytes, &n) != napi_ok) return 0;
+    j->chunks[k].bytes = (const uint8_t *)bytes;
+    j->chunks[k].n = n;
+  }
+  return 1;
 }
 
 static dec_job *dec_args(napi_env env, napi_callback_info info, size_t want, napi_value *argv) {
   size_t argc = want + 1; /* + optional keyPost */
   if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok || argc < want) {
-    napi_throw_type_error(env, NULL, want == 4 ? "decode(ctx, buffer, blobRemaining, cb)"
-                                               : "decodeSync(ctx, buffer, blobRemaining)");
+    napi_throw_type_error(env, NULL, want == 4 ? "decode(ctx, buffer | buffers, blobRemaining, cb)"
+                                               : "decodeSync(ctx, buffer | buffers, blobRemaining)");
     return NULL;
   }
   dec_job *j = (dec_job *)calloc(1, sizeof *j);
   if (!j) return NULL;
   double brem = 0;
-  void *bytes = NULL;
-  if (napi_get_value_external(env, argv[0], (void **)&j->box) != napi_ok ||
-      napi_get_buffer_info(env, argv[1], &bytes, &j->n) != napi_ok ||
+  if (napi_get_value_external(env, argv[0], (void **)&j->box) != napi_ok || !batch_chunks(env, argv[1], j) ||
       napi_get_value_double(env, argv[2], &brem) != napi_ok) {
-    free(j);
+    free_job(j);
     napi_throw_type_error(env, NULL, "decode: bad arguments");
     return NULL;
   }
-  j->bytes = (const uint8_t *)bytes;
+  j->st = env_get(env);
   j->carry.blob_remaining = (uint64_t)brem;
   if (argc > want) {
     bool kp = false;
@@ -322,8 +543,7 @@ static napi_value js_decode_sync(napi_env env, napi_callback_info info) {
   napi_value res = NULL;
   if (j->rc != DRP_OK) throw_rc(env, "decode", j->rc);
   else if (!(res = dec_result(env, j))) napi_throw_error(env, NULL, "drp addon: result allocation failed");
-  free_cols(j);
-  free(j);
+  free_job(j);
   return res;
 }
 
@@ -448,58 +668,6 @@ static napi_value js_encode(napi_env env, napi_callback_info info) {
   return NULL;
 }
 
-/* ---- pinned staging blocks ---------------------------------------------------------------
- * pinnedBuffer(bytes) -> a Buffer over page-locked host memory (drp_host_alloc), or null. The
- * decoder coalesces small writes into it, so the batch is copied into HBM by DMA instead of
- * through the runtime's pageable bounce buffer. Blocks are PIN_BLOCK bytes and recycled: a
- * block returns to the free list when its Buffer and every slice of it (the change values handed
- * to callbacks) have been collected, so no live slice ever sees a later batch's bytes. At most
- * PIN_MAX blocks exist; past that (or for a larger batch) the caller copies into ordinary memory. */
-#define PIN_BLOCK ((size_t)16 << 20 | (size_t)1 << 16)
-#define PIN_MAX 24
-static void *pin_free[PIN_MAX];
-static int pin_nfree, pin_total;
-
-static void pin_release(napi_env env, void *data, void *hint) {
-  (void)hint;
-  int64_t adj;
-  if (pin_nfree < PIN_MAX) pin_free[pin_nfree++] = data;
-  else drp_host_free(data);
-  napi_adjust_external_memory(env, -(int64_t)PIN_BLOCK, &adj);
-}
-
-static void pin_cleanup(void *arg) {
-  (void)arg;
-  while (pin_nfree) drp_host_free(pin_free[--pin_nfree]);
-}
-
-static napi_value js_pinned_buffer(napi_env env, napi_callback_info info) {
-  size_t argc = 1;
-  napi_value argv[1], out;
-  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  double want = 0;
-  if (argc < 1 || napi_get_value_double(env, argv[0], &want) != napi_ok || !(want > 0) || want > (double)PIN_BLOCK) {
-    NAPI_CALL(env, napi_get_null(env, &out));
-    return out;
-  }
-  void *p = NULL;
-  if (pin_nfree) {
-    p = pin_free[--pin_nfree];
-  } else if (pin_total < PIN_MAX && drp_host_alloc(PIN_BLOCK, &p) == DRP_OK) {
-    pin_total++;
-  } else {
-    NAPI_CALL(env, napi_get_null(env, &out));
-    return out;
-  }
-  int64_t adj;
-  napi_adjust_external_memory(env, (int64_t)PIN_BLOCK, &adj); /* (so V8 collects spent batches early) */
-  if (napi_create_external_buffer(env, (size_t)want, p, pin_release, NULL, &out) != napi_ok) {
-    pin_free[pin_nfree++] = p;
-    NAPI_CALL(env, napi_get_null(env, &out));
-  }
-  return out;
-}
-
 /* ---- devices and the multi-GPU global index ---------------------------------------------- */
 
 static napi_value js_device_count(napi_env env, napi_callback_info info) {
@@ -519,30 +687,18 @@ static napi_value js_device_count(napi_env env, napi_callback_info info) {
  * call (its stream is the one the collective and the scan run on, and its calls are serialised:
  * native.js hands the same contexts to decoders and encoders). The communicators depend only on
  * the device list, so they are created once per device list (drp_comm_init_all) and reused. */
-static struct {
-  int ng;
-  int dev[64];
-  drp_comm *comm[64];
-} comm_cache;
-
-static void comm_cache_clear(void *arg) {
-  (void)arg;
-  for (int g = 0; g < comm_cache.ng; g++) drp_comm_destroy(comm_cache.comm[g]);
-  comm_cache.ng = 0;
-}
-
 /* the cached communicators of this device list, created on first use (or on a new list) */
-static int comms_for(drp_ctx **ctxs, int ng, drp_comm **out) {
-  int same = comm_cache.ng == ng;
-  for (int g = 0; g < ng && same; g++) same = comm_cache.dev[g] == drp_device(ctxs[g]);
+static int comms_for(env_state *st, drp_ctx **ctxs, int ng, drp_comm **out) {
+  int same = st->comm_ng == ng;
+  for (int g = 0; g < ng && same; g++) same = st->comm_dev[g] == drp_device(ctxs[g]);
   if (!same) {
-    comm_cache_clear(NULL);
-    int rc = drp_comm_init_all(ctxs, ng, comm_cache.comm);
+    comm_cache_clear(st);
+    int rc = drp_comm_init_all(ctxs, ng, st->comm);
     if (rc != DRP_OK) return rc;
-    comm_cache.ng = ng;
-    for (int g = 0; g < ng; g++) comm_cache.dev[g] = drp_device(ctxs[g]);
+    st->comm_ng = ng;
+    for (int g = 0; g < ng; g++) st->comm_dev[g] = drp_device(ctxs[g]);
   }
-  for (int g = 0; g < ng; g++) out[g] = comm_cache.comm[g];
+  for (int g = 0; g < ng; g++) out[g] = st->comm[g];
   return DRP_OK;
 }
 
@@ -610,10 +766,11 @@ static napi_value js_index_allgather(napi_env env, napi_callback_info info) {
       for (uint32_t k = 0; k < locked && !dup; k++) dup = boxes[k] == boxes[locked];
       if (!dup) pthread_mutex_lock(&boxes[locked]->mu);
     }
-    rc = comms_for(ctxs, (int)ng, comms);
+    env_state *st = env_get(env);
+    rc = st ? comms_for(st, ctxs, (int)ng, comms) : DRP_E_INVAL;
     if (rc == DRP_OK)
       rc = drp_index_allgather_host(ctxs, comms, (int)ng, (const drp_stream_stats *const *)local, per, global, base);
-    if (rc != DRP_OK) comm_cache_clear(NULL); /* (a failed collective leaves nothing cached) */
+    if (rc != DRP_OK && st) comm_cache_clear(st); /* (a failed collective leaves nothing cached) */
   }
   for (uint32_t g = locked; g-- > 0;) {
     int dup = 0;
@@ -658,11 +815,20 @@ static napi_value init(napi_env env, napi_value exports) {
       {"encode", NULL, js_encode, NULL, NULL, NULL, napi_enumerable, NULL},
       {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_enumerable, NULL},
       {"indexAllgather", NULL, js_index_allgather, NULL, NULL, NULL, napi_enumerable, NULL},
-      {"pinnedBuffer", NULL, js_pinned_buffer, NULL, NULL, NULL, napi_enumerable, NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
-  napi_add_env_cleanup_hook(env, comm_cache_clear, NULL);
-  napi_add_env_cleanup_hook(env, pin_cleanup, NULL);
+  env_state *st = (env_state *)calloc(1, sizeof *st);
+  if (!st) {
+    napi_throw_error(env, NULL, "drp addon: out of memory");
+    return NULL;
+  }
+  pthread_mutex_init(&st->mu, NULL);
+  st->refs = 1;
+  if (napi_set_instance_data(env, st, env_finalize, NULL) != napi_ok) {
+    env_unref(st);
+    napi_throw_error(env, NULL, "drp addon: napi_set_instance_data failed");
+    return NULL;
+  }
   napi_value v;
   napi_create_int32(env, drp_abi_version(), &v);
   napi_set_named_property(env, exports, "abiVersion", v);

@@ -28,6 +28,7 @@ constexpr uint64_t RDY = 1ull << 63;          // published word: value | RDY
 constexpr uint64_t C_ID = 1ull << 62;         // claim: identity (no chain survives the tile)
 constexpr uint64_t M_ERR = 1ull << 60;        // with MARK_TERM: the chain ended at an error header
 constexpr uint64_t NONE = ~0ull;              // internal: no chain
+constexpr uint32_t REC_NONE = 0xFFFFFFFFu;    // tile_rec: the tile has no records (drp_walk.hip)
 
 constexpr uint32_t F_MISS = 1u << 12;         // overflow bit: prediction failed -> exact re-run
 constexpr uint32_t F_WAIT = 1u << 13;

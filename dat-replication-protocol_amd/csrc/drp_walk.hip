@@ -29,18 +29,38 @@
 namespace drp {
 namespace spec {
 
-constexpr uint32_t WK_WB = 128;                  // window bytes per region and step
-constexpr uint32_t WK_WPT = TILE / WK_WB;        // windows per tile (64)
-constexpr uint32_t WK_SLOTS = 4;                 // LDS ring slots
-constexpr uint32_t WK_AHEAD = 3;                 // windows staged ahead of the one walked
+#ifndef DRP_WK_WB
+#define DRP_WK_WB 128
+#endif
+constexpr uint32_t WK_WB = DRP_WK_WB;            // window bytes per region and step
+constexpr uint32_t WK_WPT = TILE / WK_WB;        // windows per tile
+constexpr uint32_t WK_GW = 512 / WK_WB;          // windows per group of 8 segment records
+constexpr uint32_t WK_LPR = WK_WB / 16;          // lanes of one DMA instruction per region
+constexpr uint32_t SY_WB = 128;                  // the syncs' scan window
+constexpr uint32_t SY_NEAR = 256;                // a "near" sync chain's longest frame
+constexpr uint64_t SY_TAIL = 16384;              // a sync chain's tail counts this close to the stream end
+#ifndef DRP_WK_SLOTS
+#define DRP_WK_SLOTS 4
+#define DRP_WK_AHEAD 3
+#endif
+#ifndef DRP_WK_REGIONS
+#define DRP_WK_REGIONS 65536
+#endif
+constexpr uint32_t WK_SLOTS = DRP_WK_SLOTS;      // LDS ring slots
+constexpr uint32_t WK_AHEAD = DRP_WK_AHEAD;      // windows staged ahead of the one walked
+static_assert(WK_AHEAD == 2 || WK_AHEAD == 3, "the wait accounting below covers these");
 constexpr uint32_t WK_SLOT = WAVE * WK_WB;       // bytes per slot (8 KiB)
 constexpr uint32_t WK_NDMA = WK_SLOT / (WAVE * 16);  // DMA instructions per step (8)
 constexpr uint32_t WK_K = 8;                     // frames a sync chain must survive (no Change shape)
-constexpr uint32_t WK_REGIONS = 65536;           // regions aimed at (one per resident lane)
-static_assert(WK_WPT % 4 == 0, "records are flushed every 4 windows (8 segments)");
+constexpr uint32_t WK_REGIONS = DRP_WK_REGIONS;  // regions aimed at (one per resident lane)
+#ifndef DRP_HOP_REGIONS
+#define DRP_HOP_REGIONS 262144
+#endif
+constexpr uint32_t HOP_REGIONS = DRP_HOP_REGIONS;  // hop walkers: regions aimed at
+static_assert(WK_WB == 64 || WK_WB == 128, "windows of one or two segments");
 static_assert(WK_SLOTS >= WK_AHEAD + 1, "the ring holds the walked window, the next and the in-flight ones");
 
-enum : uint32_t { WM_SYNC = 0, WM_WALK = 1, WM_DONE = 2 };
+enum : uint32_t { WM_WALK = 1, WM_DONE = 2 };
 
 // Interior tiles of stream s: i in [i_lo, i_lo + n) of its tiles (A_i = base + i * TILE).
 struct Interior {
@@ -127,7 +147,7 @@ struct WalkLds {
 // dword of this lane's bytes at window-relative offset o (4-aligned, o < 2 * WK_WB: the window
 // walked and the next one), from the ring
 __device__ __forceinline__ uint32_t wk_rd(const WalkLds &S, uint32_t w, uint32_t o) {
-  const uint32_t slot = (w + (o >> 7)) % WK_SLOTS;
+  const uint32_t slot = (w + o / WK_WB) % WK_SLOTS;
   return S.ring[(slot * WK_SLOT + threadIdx.x * WK_WB + (o & (WK_WB - 1))) >> 2];
 }
 
@@ -135,18 +155,22 @@ __device__ __forceinline__ uint32_t wk_rd(const WalkLds &S, uint32_t w, uint32_t
 // one dword), little endian
 __device__ __forceinline__ uint64_t wk_rd8(const WalkLds &S, uint32_t w, uint32_t o) {
   const uint32_t d = o & ~3u, sh = (o & 3u) * 8u;
-  const uint32_t a = wk_rd(S, w, d), b = wk_rd(S, w, d + 4), c = (o & 3u) ? wk_rd(S, w, d + 8) : 0u;
+  const uint32_t a = wk_rd(S, w, d), b = wk_rd(S, w, d + 4), c = wk_rd(S, w, d + 8);
   const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh), hi = __builtin_amdgcn_alignbit(c, b, sh);
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-// 8 bytes at absolute position p from the batch (two aligned 8-byte loads; p + 16 <= nbytes)
+// 8 bytes at absolute position p from the batch (two aligned 8-byte loads; p + 16 <= nbytes).
+// The value is waited for here, in the caller's branch: left to the compiler, the wait (a
+// vmcnt(0), which also drains the ring's DMAs in flight) lands where the branch merges with the
+// ring-read path, and every ring read pays for it.
 __device__ __forceinline__ uint64_t g_rd8(const uint8_t *g, uint64_t p) {
   const uint64_t *q = reinterpret_cast<const uint64_t *>(g + (p & ~7ull));
   const uint32_t sh = (uint32_t)(p & 7u) * 8u;
-  const uint64_t a = q[0];
-  if (!sh) return a;
-  return (a >> sh) | (q[1] << (64 - sh));
+  const uint64_t a = q[0], b = q[1];
+  uint64_t x = sh ? (a >> sh) | (b << (64 - sh)) : a;
+  asm volatile("" : "+v"(x));
+  return x;
 }
 
 // A frame header from its first 8 bytes x: the length varint of 1..5 bytes, then the id.
@@ -155,20 +179,16 @@ struct WHdr {
   uint64_t L;
   uint32_t k, id;
 };
-__device__ __forceinline__ WHdr wk_hdr(uint64_t x) {
+__device__ __forceinline__ WHdr wk_hdr(uint64_t x) {  // (branch-free)
   WHdr h;
   const uint64_t tm = ~x & 0x8080808080ull;
-  if (!tm) {
-    h.k = 0;
-    h.L = 0;
-    h.id = 0xFF;
-    return h;
-  }
-  h.k = ((uint32_t)__builtin_ctzll(tm) >> 3) + 1u;
+  const uint32_t k = ((uint32_t)__builtin_ctzll(tm | (1ull << 63)) >> 3) + 1u;  // (8: none)
   const uint64_t v = (x & 0x7Full) | ((x >> 1) & 0x3F80ull) | ((x >> 2) & 0x1FC000ull) | ((x >> 3) & 0xFE00000ull) |
                      ((x >> 4) & 0x7F0000000ull);
-  h.L = v & ((1ull << (7u * h.k)) - 1ull);
-  h.id = (uint32_t)(x >> (8u * h.k)) & 0xFFu;
+  const bool ok = k <= 5u;
+  h.k = ok ? k : 0u;
+  h.L = ok ? v & ((1ull << (7u * k)) - 1ull) : 0ull;
+  h.id = ok ? (uint32_t)(x >> (8u * k)) & 0xFFu : 0xFFu;
   return h;
 }
 
@@ -187,11 +207,22 @@ struct WkReader {
   }
 };
 
+// Byte reader for the region syncs (walk_sync): the batch, read through the caches.
+struct GReader {
+  const uint8_t *g;
+  uint64_t nbytes;
+  __device__ __forceinline__ uint64_t rd8(uint64_t p) const {
+    if (p + 16 > nbytes) return 0;  // (past the batch: parses as nothing valid)
+    return g_rd8(g, p);
+  }
+};
+
 // Sync check of a Change candidate: its payload [po, po + pl) parses in the schema's own shape
 // (one-byte tags with their wire types, in protocol-buffers' field order: [subset] key change
 // from to [value], varint numbers of <= 10 bytes, lengths inside the payload) and its last field
 // ends exactly at the payload end. 1: strong; 0: not a Change of that shape. Prediction only.
-__device__ __forceinline__ uint32_t wk_change_shape(const WkReader &R, uint64_t po, uint64_t pl) {
+template <class Rd>
+__device__ __forceinline__ uint32_t wk_change_shape(const Rd &R, uint64_t po, uint64_t pl) {
   uint64_t off = 0;
   uint32_t last = 0;  // the field number of the previous field (schema order)
 #pragma unroll 1
@@ -231,13 +262,31 @@ __device__ __forceinline__ uint32_t wk_change_shape(const WkReader &R, uint64_t 
   return (off == pl && last >= 5u) ? 1u : 0u;
 }
 
+// A complete Change frame at c whose payload has the schema's shape (wk_change_shape) and whose
+// next header is valid: strong by itself.
+template <class Rd>
+__device__ __forceinline__ bool wk_shaped(const Rd &R, uint64_t c, uint64_t se) {
+  if (c >= se) return false;
+  const WHdr h = wk_hdr(R.rd8(c));
+  if (h.k == 0 || h.id != 1u || h.L <= 1 || h.L - 1 > se - c - h.k - 1) return false;
+  if (!wk_change_shape(R, c + h.k + 1u, h.L - 1u)) return false;
+  const uint64_t n = c + h.k + h.L;
+  if (n >= se) return true;
+  const WHdr g = wk_hdr(R.rd8(n));
+  return g.k != 0 && g.id <= 2u && (g.id == 0 || g.L != 0);
+}
+
 // Does the chain from candidate c survive? A header is valid when its id is <= 2 (and a Change or
 // blob declares a length); a Change frame must start with a Change tag. Steps past the two ring
 // windows read the batch. 1: survives WK_K frames, or ends at the stream end (exactly, or in a
-// tail) after at least two complete frames (a shadow header whose varint swallows a real one's
-// length byte declares a frame of ~1 MB+, which a short batch cuts: no evidence alone).
-__device__ __forceinline__ bool wk_survives(const WkReader &R, uint64_t c, uint64_t se) {
+// tail starting within SY_TAIL of it) after at least two complete frames (a shadow header whose
+// varint swallows a real one's length bytes declares a frame of ~1 MB+, which the batch cuts: no
+// evidence alone).
+// near: no frame of the chain is longer than the two ring windows.
+template <class Rd>
+__device__ __forceinline__ bool wk_survives(const Rd &R, uint64_t c, uint64_t se, bool &near) {
   uint64_t p = c;
+  near = true;
 #pragma unroll 1
   for (uint32_t f = 0; f < WK_K; f++) {
     if (p >= se) return p == se && f >= 2u;
@@ -248,7 +297,11 @@ __device__ __forceinline__ bool wk_survives(const WkReader &R, uint64_t c, uint6
       p += h.k + 1u;
       continue;
     }
-    if (h.L > se - p - h.k) return f >= 2u;  // a tail: the chain ends at the stream end
+    // a tail (the chain ends in a frame the stream end cuts): evidence only close to that end; a
+    // header whose varint swallows a real header's declares a frame of ~64 MB+ (C5: 4 KB frames
+    // with 2-byte lengths), a "tail" wherever it lies
+    if (h.L > se - p - h.k) return f >= 2u && se - p <= SY_TAIL;
+    near = near && h.k + h.L <= SY_NEAR;
     if (h.id == 1) {
       const uint32_t t = (h.k < 7u) ? (uint32_t)(x >> (8u * (h.k + 1u))) & 0xFFu : (uint32_t)R.rd8(p + h.k + 1) & 0xFFu;
       constexpr uint64_t TAGS = (1ull << 0x0a) | (1ull << 0x12) | (1ull << 0x18) | (1ull << 0x20) | (1ull << 0x28) |
@@ -274,6 +327,248 @@ __device__ __forceinline__ uint32_t wk_live16(uint32_t a, uint32_t b, uint32_t c
   return (X | (M & ((X >> 1) | ((M >> 1) & (X >> 2))))) & 0xFFFFu;  // through 0, 1 or 2 MSB bytes
 }
 
+// ---- per-frame records for the record emission (emit_rec) ------------------------------------
+// One delivered frame as 32 bytes: what decode_change and the frame table write for it, so that
+// the emission expands records into columns without reading the wire again.
+//   x: payload offset from the tile's first byte (14 bits) | id << 14 | partial << 16 |
+//      DRP_F_SUBSET << 17 | DRP_F_VALUE << 18        y: payload length (clamped as the column)
+//   z: key_off | subset_off << 8 | key_len << 16     w: value_off | subset_len << 16
+//   then change, from, to (low 32 bits) and their bits 32..41 (10 bits each)
+// Only Change payloads in protocol-buffers' own shape are recorded ([subset] key change from to
+// [value], one-byte tags, lengths of < 2^28 in <= 4 bytes, numbers of < 2^42, the last field
+// ending the payload, every offset and length inside its field); any other frame makes its tile
+// take the wire-reading emission (emit_lean / emit_tiles), as does a region whose records
+// overflow its share of the record buffer.
+constexpr uint32_t WK_REC_BYTES = 64;  // the record buffer holds one record per this many wire bytes
+
+// a varint of <= n bytes from y (little endian): bytes used (0: none ends within n)
+__device__ __forceinline__ uint32_t wk_varint(uint64_t y, uint32_t n, uint64_t &v) {
+  const uint64_t tm = ~y & 0x808080808080ull & ((1ull << (8u * n)) - 1ull);
+  if (!tm) return 0;
+  const uint32_t kb = ((uint32_t)__builtin_ctzll(tm) >> 3) + 1u;
+  v = ((y & 0x7Full) | ((y >> 1) & 0x3F80ull) | ((y >> 2) & 0x1FC000ull) | ((y >> 3) & 0xFE00000ull) |
+       ((y >> 4) & 0x7F0000000ull) | ((y >> 5) & 0x3F800000000ull)) &
+      ((1ull << (7u * kb)) - 1ull);
+  return kb;
+}
+
+// One field at q: its tag byte must be `tag`, then a varint of <= n bytes (into v: 0 when there is
+// none) inside [q, end); returns the field's header bytes (tag + varint), and clears ok when the
+// field is not there. Computed without early exits: the record's checks below run as one
+// straight-line sequence (divergent early returns out of this parse were miscompiled into
+// records with zeroed numbers: change / to columns of 0 on every frame).
+__device__ __forceinline__ uint32_t wk_field(const WkReader &R, uint64_t q, uint64_t end, uint32_t tag, uint32_t n,
+                                             uint64_t &v, bool &ok) {
+  const uint64_t x = R.rd8(q);
+  v = 0;
+  const uint32_t kb = wk_varint(x >> 8, n, v);
+  ok = ok && q < end && (x & 0xFFu) == tag && kb != 0 && 1u + kb <= end - q;
+  return 1u + kb;
+}
+
+__device__ __forceinline__ bool wk_record(const WkReader &R, uint64_t po, uint64_t pl, uint4 &a, uint4 &b) {
+  const uint64_t end = po + pl;
+  uint64_t q = po, slen = 0, klen = 0, nc = 0, nf = 0, nt = 0, vlen = 0;
+  bool ok = true, sub = (R.rd8(q) & 0xFFu) == 0x0Au, sok = true;
+  const uint32_t sh = wk_field(R, q, end, 0x0Au, 4, slen, sok);  // subset (when its tag is there)
+  ok = !sub || (sok && slen <= end - q - sh && slen < 0x10000u);
+  const uint32_t soff = sub ? sh : 0u;
+  slen = sub ? slen : 0u;
+  q = sub && ok ? q + sh + slen : q;
+  const uint32_t kh = wk_field(R, q, end, 0x12u, 4, klen, ok);  // key
+  ok = ok && klen <= end - q - kh && klen < 0x10000u && q - po + kh < 0x100u;
+  const uint32_t koff = (uint32_t)(q - po) + kh;
+  q = ok ? q + kh + klen : end;
+  q += wk_field(R, q, end, 0x18u, 6, nc, ok);  // change
+  q += wk_field(R, q, end, 0x20u, 6, nf, ok);  // from
+  q += wk_field(R, q, end, 0x28u, 6, nt, ok);  // to
+  const bool val = ok && q != end;  // value: the last field
+  bool vok = true;
+  const uint32_t vh = wk_field(R, q, end, 0x32u, 4, vlen, vok);
+  ok = ok && (!val || (vok && vlen == end - q - vh && q - po + vh < 0x10000u));
+  const uint32_t fl = (sub ? DRP_F_SUBSET : 0u) | (val ? DRP_F_VALUE : 0u);
+  a.x |= fl << 17;
+  a.z = koff | (soff << 8) | ((uint32_t)klen << 16);
+  a.w = (val ? (uint32_t)(q - po) + vh : 0u) | ((uint32_t)slen << 16);
+  b.x = (uint32_t)nc;
+  b.y = (uint32_t)nf;
+  b.z = (uint32_t)nt;
+  b.w = (uint32_t)(nc >> 32) | ((uint32_t)(nf >> 32) << 10) | ((uint32_t)(nt >> 32) << 20);
+  return ok;
+}
+
+// s_waitcnt vmcnt(n) for a count known only at run time (wave-uniform): the largest immediate
+// <= n of a small set (waiting for more operations than needed is always safe)
+__device__ __forceinline__ void wk_wait_vm(uint32_t n) {
+  n = __builtin_amdgcn_readfirstlane(n);  // (scalar branches)
+  if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  else if (n >= 28) asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+  else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (n >= 22) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+  else if (n >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  else if (n >= 19) asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
+  else if (n >= 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Region r of the batch: its first tile (t0, at A0), its stream end, its windows, and for a
+// stream's first tile the exact entry.
+struct Region {
+  uint64_t t0, A0, se, entry;
+  uint32_t nw;
+  bool exact;
+};
+__device__ __forceinline__ Region region_of(const DecodeParams &P, uint64_t r) {
+  uint64_t s = 0;
+  if (P.nstreams > 1) {  // walk_rp[s] <= r < walk_rp[s + 1]
+    uint64_t lo = 0, hi = P.nstreams;
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (P.walk_rp[mid] <= r) lo = mid;
+      else hi = mid;
+    }
+    s = lo;
+  }
+  const Interior I = interior(P, s);
+  const uint64_t i0 = I.i_lo + (r - P.walk_rp[s]) * P.walk_tpr;
+  Region G;
+  G.t0 = P.tile_prefix[s] + i0;
+  G.A0 = I.base + i0 * TILE;
+  G.se = I.se;
+  G.nw = (uint32_t)umin64(P.walk_tpr, I.i_lo + I.n - i0) * WK_WPT;
+  G.exact = G.A0 == I.so;
+  G.entry = I.so + (P.entry ? P.entry[s] : 0ull);
+  return G;
+}
+
+// ---- region syncs ----------------------------------------------------------------------------
+// One lane per region: the entry its walker starts from (P.walk_entry[r]; NONE: no chain found in
+// the region, whose tiles then claim identity). A stream's first tile has its exact entry. Else,
+// first, the region's first "shaped" candidate: a complete Change whose payload parses in the
+// schema's own shape and whose next header is valid (random bytes essentially never pass; the
+// checks read only the candidate's own bytes). Before it, a candidate whose chain survives WK_K
+// short frames ("near": <= 256 bytes each, so the checks stay in the cached bytes around it) is
+// taken instead (the region starts in blobs or other frames); a chain that survives by landing on
+// a shaped Change right after its first frame is taken at that Change (the candidate itself is
+// most likely a shadow merging into the real chain). Only a region with no shaped candidate at all
+// (blobs, non-Change data) runs the general scan, which also weighs "far" chains (see
+// sync_general). Prediction only: verification proves the claims.
+template <class Rd>
+__device__ __forceinline__ uint32_t sync_live16(const Rd &R, uint64_t p) {
+  const uint64_t x0 = R.rd8(p), x1 = R.rd8(p + 8);
+  return wk_live16((uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32), (uint32_t)R.rd8(p + 16));
+}
+
+// The general scan (a region without a shaped candidate): windows of 128 bytes in order,
+// candidates through each window and the next one's first 112 bytes. A candidate must survive
+// WK_K frames; it is taken at once when near, else ("far") held back while the scan goes on, up
+// to its successor or its tile's end, and dropped for a near candidate: a header whose length
+// varint swallows a real header's first bytes declares a frame of ~1 MB that lands on the real
+// chain with odds of one in the real frame size, and then "survives". At the held-back chain's
+// successor the scan stops; when the held-back frame is short and its successor is a shaped
+// Change, the chain is taken there.
+__device__ __forceinline__ uint64_t sync_general(const GReader &R, uint64_t A0, uint32_t nsw, uint64_t se) {
+  uint64_t found = ~0ull, far_c = 0, far_n = 0;
+#pragma unroll 1
+  for (uint32_t w = 0; w < nsw && found == ~0ull; w++) {
+    const uint64_t W0 = A0 + (uint64_t)w * SY_WB, W1 = W0 + SY_WB;
+    if (far_c && far_n < W1) return far_c;  // no near candidate up to the held-back chain's successor
+    bool stop = false;
+#pragma unroll 1
+    for (uint32_t c16 = 0; c16 < SY_WB + 112u && !stop; c16 += 16u) {
+      uint32_t live = sync_live16(R, W0 + c16);
+#pragma unroll 1
+      while (live) {
+        const uint32_t o = c16 + (uint32_t)__builtin_ctz(live);
+        live &= live - 1u;
+        const uint64_t c = W0 + o;
+        if (far_c && c >= far_n) {
+          if (far_n - far_c <= SY_NEAR && wk_shaped(R, far_n, se)) found = far_n;
+          stop = true;
+          break;
+        }
+        const WHdr h = wk_hdr(R.rd8(c));
+        if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0)) continue;
+        bool near = false;
+        if (!wk_survives(R, c, se, near)) continue;
+        if (near) {
+          const uint64_t n1 = c + h.k + (h.id ? h.L : 1u);
+          found = n1 < W0 + SY_WB + 112u && wk_shaped(R, n1, se) ? n1 : c;
+          stop = true;
+          break;
+        }
+        if (!far_c && o < SY_WB) {
+          far_c = c;
+          far_n = c + h.k + h.L;
+        }
+      }
+    }
+    if (found == ~0ull && w % (TILE / SY_WB) == TILE / SY_WB - 1 && far_c) found = far_c;  // (its frame leaves the tile)
+  }
+  return found;
+}
+
+__global__ __launch_bounds__(256) void walk_sync(DecodeParams P) {
+  const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (r >= P.walk_rp[P.nstreams]) return;
+  const Region G = region_of(P, r);
+  if (G.exact) {
+    P.walk_entry[r] = G.entry;
+    return;
+  }
+  const GReader R{P.bytes, P.nbytes};
+  const uint64_t se = G.se, end = G.A0 + (uint64_t)(G.nw / WK_WPT) * TILE;
+  // the first shaped candidate
+  uint64_t shaped = ~0ull;
+#pragma unroll 1
+  for (uint64_t c16 = G.A0; c16 < end && shaped == ~0ull; c16 += 16u) {
+    uint32_t live = sync_live16(R, c16);
+#pragma unroll 1
+    while (live) {
+      const uint64_t c = c16 + (uint32_t)__builtin_ctz(live);
+      live &= live - 1u;
+      if (wk_shaped(R, c, se)) {
+        shaped = c;
+        break;
+      }
+    }
+  }
+  uint64_t found = shaped;
+  if (shaped != ~0ull) {
+    // a near chain before it
+#pragma unroll 1
+    for (uint64_t c16 = G.A0; c16 < shaped && found == shaped; c16 += 16u) {
+      uint32_t live = sync_live16(R, c16);
+#pragma unroll 1
+      while (live) {
+        const uint64_t c = c16 + (uint32_t)__builtin_ctz(live);
+        live &= live - 1u;
+        if (c >= shaped) break;
+        const WHdr h = wk_hdr(R.rd8(c));
+        if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0) || h.k + (h.id ? h.L : 1u) > SY_NEAR) continue;
+        bool near = false;
+        if (!wk_survives(R, c, se, near) || !near) continue;
+        const uint64_t n1 = c + h.k + (h.id ? h.L : 1u);
+        found = wk_shaped(R, n1, se) ? n1 : c;
+        break;
+      }
+    }
+  } else {
+    found = sync_general(R, G.A0, G.nw / WK_WPT * (TILE / SY_WB), se);
+  }
+  P.walk_entry[r] = found;
+  if (P.stats && found != ~0ull) atomicAdd(&P.stats[31], 1ull);
+}
+
+// ---- the walkers -----------------------------------------------------------------------------
+// One lane per region, from its entry (walk_sync), frame by frame through the ring. A frame that
+// breaks the grammar ends the region's walk ("death": a mispredicted entry, or a protocol error):
+// its tile and the rest of the region claim identity, and verification walks them exactly.
+template <bool REC>
 __global__ __launch_bounds__(WAVE) void claims_walk(DecodeParams P) {
   __shared__ WalkLds S;
   const uint32_t lane = threadIdx.x;
@@ -281,216 +576,248 @@ __global__ __launch_bounds__(WAVE) void claims_walk(DecodeParams P) {
   const uint64_t r = (uint64_t)blockIdx.x * WAVE + lane;
   if ((uint64_t)blockIdx.x * WAVE >= nreg) return;  // (whole wave)
   // ---- this lane's region ---------------------------------------------------------------------
-  uint64_t t0 = 0, A0 = 0, se = 0, pos = 0;
-  uint32_t nw = 0, mode = WM_DONE;
-  bool rs = false;
+  uint64_t t0 = 0, A0 = 0, se = 0, pos = ~0ull;
+  uint64_t rbase = 0;  // this region's first record slot (P.rec_cap slots per region)
+  uint32_t nw = 0;
   if (r < nreg) {
-    uint64_t s = 0;
-    if (P.nstreams > 1) {  // walk_rp[s] <= r < walk_rp[s + 1]
-      uint64_t lo = 0, hi = P.nstreams;
-      while (hi - lo > 1) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (P.walk_rp[mid] <= r) lo = mid;
-        else hi = mid;
-      }
-      s = lo;
-    }
-    const Interior I = interior(P, s);
-    const uint64_t j = r - P.walk_rp[s];
-    const uint64_t i0 = I.i_lo + j * P.walk_tpr;
-    const uint64_t ntr = umin64(P.walk_tpr, I.i_lo + I.n - i0);
-    t0 = P.tile_prefix[s] + i0;
-    A0 = I.base + i0 * TILE;
-    se = I.se;
-    nw = (uint32_t)ntr * WK_WPT;
-    mode = WM_SYNC;
-    if (A0 == I.so) {  // the stream's first tile: its entry is exact
-      mode = WM_WALK;
-      pos = I.so + (P.entry ? P.entry[s] : 0ull);
-      rs = true;
-    }
+    const Region G = region_of(P, r);
+    t0 = G.t0;
+    A0 = G.A0;
+    se = G.se;
+    nw = G.nw;
+    rbase = r * P.rec_cap;
+    pos = P.walk_entry[r];
   }
+  uint32_t mode = pos != ~0ull ? WM_WALK : WM_DONE;
+  bool rs = true;  // the next frame noted restarts the records' chain
   // ---- DMA addressing: instruction i stages regions 8 i .. 8 i + 7 (16 bytes per lane) ---------
   uint64_t dA[WK_NDMA];
-  uint32_t dN[WK_NDMA];
 #pragma unroll
   for (uint32_t i = 0; i < WK_NDMA; i++) {
-    const int src = (int)(i * 8u + (lane >> 3));
+    const int src = (int)(i * (WAVE / WK_LPR) + lane / WK_LPR);
     const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)A0, src, WAVE), hi = (uint32_t)__shfl((int)(uint32_t)(A0 >> 32), src, WAVE);
-    dA[i] = (((uint64_t)hi << 32) | lo) + (lane & 7u) * 16u;
-    dN[i] = (uint32_t)__shfl((int)nw, src, WAVE);  // windows 0 .. nw (the last: the halo's first bytes)
+    dA[i] = (((uint64_t)hi << 32) | lo) + (lane % WK_LPR) * 16u;
   }
   uint32_t nwmax = nw;
 #pragma unroll
   for (uint32_t d = 1; d < WAVE; d <<= 1) nwmax = max(nwmax, (uint32_t)__shfl_xor((int)nwmax, d, WAVE));
+  nwmax = __builtin_amdgcn_readfirstlane(nwmax);
   // (the LDS-DMA is issued from inline asm: the compiler would otherwise put a vmcnt(0) wait in
   // front of every LDS read, since it cannot tell which slot a pending DMA writes; the one wait
   // the ring needs is the counted one below)
   const uint32_t ring0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)S.ring;
-  auto issue = [&](uint32_t w) {
+  // The regions' windows w into the ring slot w % WK_SLOTS; returns the DMA instructions issued.
+  // Only the windows a walk may read are staged: from the one holding the region's next frame
+  // start on (a region whose frames are long skips the windows inside them; a finished one all).
+  // When every region needs it (dense streams: nearly every step), one unmasked form.
+  const uint64_t act = __ballot(nw != 0);
+  auto issue = [&](uint32_t w) -> uint32_t {
     const uint32_t slot = w % WK_SLOTS;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the slot's last reads, a step ago, are done)
+    const uint64_t need = __ballot(w <= nw && mode == WM_WALK && pos < A0 + (uint64_t)(w + 1u) * WK_WB);
+    if (need == act) {  // (inactive lanes load bytes of the batch's first lines, unread)
 #pragma unroll
-    for (uint32_t i = 0; i < WK_NDMA; i++)
-      if (dN[i] && w <= dN[i]) {
+      for (uint32_t i = 0; i < WK_NDMA; i++) {
         const uint8_t *g = P.bytes + dA[i] + (uint64_t)w * WK_WB;
         const uint32_t l = __builtin_amdgcn_readfirstlane(ring0 + slot * WK_SLOT + i * 1024u);
         asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
       }
-  };
+      return WK_NDMA;
+    }
+    uint32_t n = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < WK_AHEAD; w++) issue(w);
-  // records of the current 4-window group (8 segments: byte j = segment j)
+    for (uint32_t i = 0; i < WK_NDMA; i++) {
+      constexpr uint32_t RPI = WAVE / WK_LPR;  // regions per DMA instruction
+      const uint32_t sub = (uint32_t)(need >> (i * RPI)) & (uint32_t)((1ull << RPI) - 1u);
+      if (sub) {
+        n++;
+        if ((sub >> (lane / WK_LPR)) & 1u) {
+          const uint8_t *g = P.bytes + dA[i] + (uint64_t)w * WK_WB;
+          const uint32_t l = __builtin_amdgcn_readfirstlane(ring0 + slot * WK_SLOT + i * 1024u);
+          asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+        }
+      }
+    }
+    return n;
+  };
+  uint32_t d_pre = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < WK_AHEAD; w++) d_pre = issue(w);
+  // segment records of the current 4-window group (8 segments: byte j = segment j)
   uint64_t ent = ~0ull, fn = 0, fc = 0;
-  bool had = false;        // a chain frame started in the current tile
-  uint64_t term = 0;       // MARK_TERM | p: the tail that ended the chain in the current tile
-  uint32_t from = 0;       // SYNC: the first window-relative offset to scan
-  // SYNC: a strong "far" candidate of this tile (its first frame leaves the ring) held back while
-  // the scan looks for a strong near one: position, successor, id (0: none)
-  uint64_t far_c = 0, far_n = 0;
-  uint32_t far_id = 0;
+  bool had = false;   // a chain frame started in the current tile
+  bool dead = false;  // the chain died in the current tile
+  uint64_t term = 0;  // MARK_TERM | p: the tail that ended the chain in the current tile
+  // records (P.rec): the next slot of the region, the current tile's first one, and whether every
+  // frame of the tile so far has one
+  uint32_t rnext = 0, rtile = 0;
+  bool rok = REC && mode == WM_WALK;
+  // vector-memory operations issued after the DMA of window w + 1 (loads, stores and DMAs count
+  // together, in issue order): the stores of the steps since and the DMAs issued since (lower
+  // bounds, so the wait below is never short)
+  uint32_t st2 = 0, st1 = 0, d1 = d_pre;
 #pragma unroll 1
   for (uint32_t w = 0; w < nwmax; w++) {
-    issue(w + WK_AHEAD);
-    // windows w and w + 1 have landed (only the two youngest steps' DMAs may be in flight)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((WK_AHEAD - 1) * WK_NDMA) : "memory");
-    if (w >= nw) continue;
-    const uint32_t q = w % WK_WPT;  // window of the tile
-    const uint64_t W0 = A0 + (uint64_t)w * WK_WB, W1 = W0 + WK_WB;
-    const uint64_t T0 = A0 + (uint64_t)(w - q) * WK_WB;  // the tile's first byte
-    const uint64_t tcur = t0 + w / WK_WPT;
-    const WkReader R{S, P.bytes, W0, P.nbytes, w};
-    // a frame start p of the current tile (id, delivered) into the segment records: the current
-    // 4-window group's registers, or memory for a group already flushed (a far candidate taken late)
-    auto note = [&](uint64_t p, uint32_t id, bool deliver) {
-      const uint32_t seg = (uint32_t)(p - T0) >> 6, e = ((uint32_t)(p - T0) & 63u) | (rs ? 0x40u : 0u);
-      rs = false;
-      had = true;
-      if ((seg >> 3) != (q >> 2)) {
-        const uint64_t ix = tcur * NT + seg;
-        P.ent[ix] = (uint8_t)e;
-        P.ent_n[ix] = deliver ? 1u : 0u;
-        P.ent_c[ix] = deliver && id == 1u ? 1u : 0u;
-        return;
-      }
-      const uint32_t sh = 8u * (seg & 7u);
-      if (((ent >> sh) & 0xFFull) == 0xFFull) ent = (ent & ~(0xFFull << sh)) | ((uint64_t)e << sh);
-      fn += (uint64_t)(deliver ? 1u : 0u) << sh;
-      fc += (uint64_t)(deliver && id == 1u ? 1u : 0u) << sh;
-    };
-    // the held-back far candidate becomes the chain (its frame noted where it starts)
-    auto take_far = [&]() {
-      rs = true;
-      note(far_c, far_id, far_id != 0u);
-      pos = far_n;
-      mode = WM_WALK;
-      far_c = 0;
-      if (P.stats) atomicAdd(&P.stats[31], 1ull);
-    };
-#pragma unroll 1
-    for (uint32_t guard = 0; guard < 2 * WK_WB; guard++) {  // (a death re-enters the scan)
-      if (mode == WM_SYNC && far_c && far_n < W1) take_far();  // (no near candidate up to its successor)
-      if (mode == WM_SYNC) {
-        // Candidates from `from` on, through this window and the next one's first 112 bytes (both
-        // are in the ring), in order. A complete Change whose payload has the schema's shape and
-        // whose next header is valid is taken at once (random bytes essentially never pass). Any
-        // other candidate must survive WK_K frames; it is taken at once when its first frame stays
-        // in the ring ("near"), else ("far") held back while the scan goes on, up to its successor
-        // or the tile's end, and dropped for any candidate taken at once: a header whose length
-        // varint swallows a real header's first bytes declares a frame of ~1 MB that lands on the
-        // real chain with odds of one in the real frame size (C2: 1/86), and then "survives".
-#pragma unroll 1
-        for (uint32_t c16 = from & ~15u; c16 < WK_WB + 112u; c16 += 16u) {
-          uint32_t live = wk_live16(wk_rd(S, w, c16), wk_rd(S, w, c16 + 4), wk_rd(S, w, c16 + 8), wk_rd(S, w, c16 + 12),
-                                    wk_rd(S, w, c16 + 16));
-          if (c16 < from) live &= ~0u << (from - c16);
-#pragma unroll 1
-          while (live) {
-            const uint32_t o = c16 + (uint32_t)__builtin_ctz(live);
-            live &= live - 1u;
-            const uint64_t c = W0 + o;
-            if (far_c && c >= far_n) break;  // (the held-back chain's successor: it wins from there)
-            const WHdr h = wk_hdr(wk_rd8(S, w, o));
-            if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0)) continue;
-            bool shape = false;
-            if (h.id == 1u && h.L > 1 && h.L - 1 <= se - c - h.k - 1) {  // a complete Change: its shape
-              shape = wk_change_shape(R, c + h.k + 1u, h.L - 1u) != 0;
-              const uint64_t n = c + h.k + h.L;
-              if (shape && n < se) {
-                const WHdr g = wk_hdr(R.rd8(n));
-                shape = g.k != 0 && g.id <= 2u && (g.id == 0 || g.L != 0);
-              }
-            }
-            if (!shape && !wk_survives(R, c, se)) continue;
-            if (shape || h.id == 0 || h.k + h.L <= 2 * WK_WB) {
-              pos = c;
-              mode = WM_WALK;
-              rs = true;
-              far_c = 0;
-              if (P.stats) atomicAdd(&P.stats[31], 1ull);
-              break;
-            }
-            if (!far_c && o < WK_WB) {
-              far_c = c;
-              far_n = c + h.k + h.L;
-              far_id = h.id;
-            }
-          }
-          if (mode == WM_WALK) break;
+    const uint32_t d0 = issue(w + WK_AHEAD);
+    wk_wait_vm(WK_AHEAD == 3 ? st2 + d1 + st1 + d0 : st1 + d0);  // windows w and w + 1 have landed
+    const uint32_t q = w % WK_WPT;  // window of the tile (the same for every lane)
+    uint32_t nrec = 0;              // records this lane stored in this step
+    if (w < nw) {
+      const uint64_t W0 = A0 + (uint64_t)w * WK_WB, W1 = W0 + WK_WB;
+      const uint64_t T0 = A0 + (uint64_t)(w - q) * WK_WB;  // the tile's first byte
+      const WkReader R{S, P.bytes, W0, P.nbytes, w};
+      // a frame start p (in window w, so in the current group) into the segment records
+      auto note = [&](uint64_t p, uint32_t id, bool deliver) {
+        const uint32_t rp = (uint32_t)(p - T0), sh = 8u * ((rp >> 6) & 7u);
+        const uint64_t e = (uint64_t)((rp & 63u) | (rs ? 0x40u : 0u)) << sh;
+        const uint64_t m = ((ent >> sh) & 0xFFull) == 0xFFull ? 0xFFull << sh : 0ull;  // (the segment's first)
+        ent = (ent & ~m) | (e & m);
+        rs = false;
+        had = true;
+        fn += (uint64_t)(deliver ? 1u : 0u) << sh;
+        fc += (uint64_t)(deliver && id == 1u ? 1u : 0u) << sh;
+      };
+      // this frame's record
+      auto record = [&](uint32_t k, uint64_t L, uint32_t id, bool tail) {
+        uint4 a = make_uint4((uint32_t)(pos + k + 1u - T0) | (id << 14) | ((tail ? 1u : 0u) << 16),
+                             (uint32_t)umin64(L - 1u, 0xFFFFFFFFull), 0u, 0u),
+              b = make_uint4(0u, 0u, 0u, 0u);
+        rok = rnext < P.rec_cap && (id != 1u || wk_record(R, pos + k + 1u, L - 1u, a, b));
+        if (rok) {
+          uint4 *d = reinterpret_cast<uint4 *>(P.rec + (rbase + rnext) * 8u);
+          d[0] = a;
+          d[1] = b;
+          rnext++;
+          nrec++;
         }
-        if (mode == WM_SYNC) from = WK_WB;
-      }
-      if (mode == WM_WALK) {
+      };
+      // The straight path: complete Change and blob frames (nearly every frame). A lane stops it
+      // at any other frame (a long varint, a header-only frame, a tail, a death), which the
+      // general step below takes, one frame, before the straight path resumes.
 #pragma unroll 1
-        while (pos < W1) {
-          const uint32_t o = (uint32_t)(pos - W0);
-          WHdr h = wk_hdr(wk_rd8(S, w, o));
-          uint64_t L = h.L;
-          uint32_t k = h.k, id = h.id;
-          if (k == 0) {  // a length varint of 6..10 bytes: the exact grammar
-            const Hdr e = hdr_global(P.bytes, pos, se);
-            if (e.kind == H_VALID || e.kind == H_TAIL_CHANGE || e.kind == H_TAIL_BLOB) {
-              k = e.vlen;
-              L = e.L;
-              id = e.id;
-            } else {
-              id = 0xFF;  // (an error or a cut header: the chain ends)
+      while (__ballot(mode == WM_WALK && pos < W1)) {
+        bool go = mode == WM_WALK && pos < W1;
+#pragma unroll 1
+        while (go) {
+          const WHdr h = wk_hdr(wk_rd8(S, w, (uint32_t)(pos - W0)));
+          const bool plain = (h.k != 0u) & (h.id - 1u < 2u) & (h.L != 0u) & (h.L <= se - pos - h.k);
+          if (plain) {
+            note(pos, h.id, true);
+            if (REC && rok) record(h.k, h.L, h.id, false);
+            pos += h.k + h.L;
+          }
+          go = plain & (pos < W1);
+        }
+        if (mode != WM_WALK || pos >= W1) continue;
+        // the general step: one frame
+        const uint32_t o = (uint32_t)(pos - W0);
+        const WHdr h = wk_hdr(wk_rd8(S, w, o));
+        uint64_t L = h.L;
+        uint32_t k = h.k, id = h.id;
+        if (k == 0) {  // a length varint of 6..10 bytes: the exact grammar
+          const Hdr e = hdr_global(P.bytes, pos, se);
+          if (e.kind == H_VALID || e.kind == H_TAIL_CHANGE || e.kind == H_TAIL_BLOB) {
+            k = e.vlen;
+            L = e.L;
+            id = e.id;
+          } else {
+            id = 0xFF;  // (an error or a cut header: the chain ends)
+          }
+        }
+        if (id > 2u || (id != 0u && L == 0)) {  // the chain dies
+          dead = true;
+          mode = WM_DONE;
+          if (P.stats) {  // (DRP_STATS: deaths; the first one's bytes from LDS and from HBM)
+            if (atomicAdd(&P.stats[32], 1ull) == 0) {
+              P.stats[36] = pos;
+              P.stats[37] = wk_rd8(S, w, o);
+              P.stats[38] = g_rd8(P.bytes, pos);
+              P.stats[39] = ((uint64_t)w << 32) | (lane << 16) | o;
             }
           }
-          if (id > 2u || (id != 0u && L == 0)) {  // the chain dies: scan for a new one after it
-            if (P.stats) {  // (DRP_STATS: deaths; the first one's bytes from LDS and from HBM)
-              if (atomicAdd(&P.stats[32], 1ull) == 0) {
-                P.stats[36] = pos;
-                P.stats[37] = wk_rd8(S, w, o);
-                P.stats[38] = g_rd8(P.bytes, pos);
-                P.stats[39] = ((uint64_t)w << 32) | (lane << 16) | o;
-              }
-            }
-            mode = WM_SYNC;
-            from = o + 1u;
-            break;
-          }
-          if (id == 0u) {
-            note(pos, 0u, false);
-            pos += k + 1u;
-            continue;
-          }
-          if (L > se - pos - k) {  // a tail: the stream ends inside this frame
-            note(pos, id, id == 2u);  // (a cut Change is carried, a cut blob delivered)
+        } else if (id == 0u) {
+          note(pos, 0u, false);
+          pos += k + 1u;
+        } else {
+          const bool tail = L > se - pos - k;  // the stream ends inside this frame
+          note(pos, id, !tail || id == 2u);    // (a cut Change is carried, a cut blob delivered)
+          if (REC && rok && (!tail || id == 2u)) record(k, L, id, tail);
+          if (tail) {
             term = MARK_TERM | pos;
             mode = WM_DONE;
-            break;
+          } else {
+            pos += k + L;
           }
-          note(pos, id, true);
-          pos += k + L;
         }
-        if (mode == WM_SYNC && from < WK_WB) continue;
       }
-      break;
+      if (q % WK_GW == WK_GW - 1) {  // flush the group's 8 segment records
+        const uint64_t ix = (t0 + w / WK_WPT) * NT + (q / WK_GW) * 8u;
+        *reinterpret_cast<uint64_t *>(P.ent + ix) = ent;
+        *reinterpret_cast<uint64_t *>(P.ent_n + ix) = fn;
+        *reinterpret_cast<uint64_t *>(P.ent_c + ix) = fc;
+        ent = ~0ull;
+        fn = 0;
+        fc = 0;
+      }
+      if (q == WK_WPT - 1) {  // the tile's claim
+        // (a dead tile's records mix two chains, which no record marks: identity, so verification
+        // re-walks it from its exact entry; the rest of the region is not walked)
+        uint64_t cl = C_ID;
+        if (term) cl = term;
+        else if (mode == WM_WALK && had) cl = pos;
+        if (dead) cl = C_ID;
+        P.claim[t0 + w / WK_WPT] = cl;
+        if (REC) {  // its first record (or none: the tile takes the wire-reading emission)
+          P.tile_rec[t0 + w / WK_WPT] = rok && !dead ? (uint32_t)(rbase + rtile) : REC_NONE;
+          rtile = rnext;
+          rok = rnext < P.rec_cap && !dead && mode == WM_WALK;
+        }
+        had = false;
+        term = 0;
+        dead = false;
+      }
     }
-    if (q == WK_WPT - 1 && mode == WM_SYNC && far_c) take_far();  // (its frame leaves the tile)
-    if ((q & 3u) == 3u) {  // flush the group's 8 segment records
-      const uint64_t ix = tcur * NT + (q >> 2) * 8u;
+    // this step's stores (at least one lane is active: the one with nwmax windows)
+    uint32_t st = (q % WK_GW == WK_GW - 1 ? 3u : 0u) + (q == WK_WPT - 1 ? (REC ? 2u : 1u) : 0u);
+    if (REC) {
+#pragma unroll
+      for (uint32_t d = 1; d < WAVE; d <<= 1) nrec = max(nrec, (uint32_t)__shfl_xor((int)nrec, d, WAVE));
+      st += 2u * __builtin_amdgcn_readfirstlane(nrec);
+    }
+    st2 = st1;
+    st1 = st;
+    d1 = d0;
+  }
+}
+
+// ---- the hop walkers --------------------------------------------------------------------------
+// One lane per region, from its entry (walk_sync), frame to frame with a direct read of each
+// header (two 8-byte loads through the caches; nothing staged): a frame costs one dependent load
+// and ~60 instructions, and a frame of any length costs the same (C5's 4 KB values are never
+// read). Enough regions (lanes) keep enough loads in flight for the stream to be read at the HBM
+// rate (a 128-byte line holds ~1.5 C2 headers: the wire is read about once). Outputs as
+// claims_walk: per tile its claim, per 64-byte segment its record (flushed 8 segments at a
+// time), the same death and tail rules.
+__global__ __launch_bounds__(256) void claims_hop(DecodeParams P) {
+  const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (r >= P.walk_rp[P.nstreams]) return;
+  const Region G = region_of(P, r);
+  const uint64_t A0 = G.A0, se = G.se;
+  const uint32_t ntr = G.nw / WK_WPT;       // tiles
+  const uint64_t end = A0 + (uint64_t)ntr * TILE;
+  uint64_t pos = P.walk_entry[r];
+  uint32_t mode = pos != ~0ull ? WM_WALK : WM_DONE;
+  bool rs = true;     // the next frame noted restarts the records' chain
+  bool had = false;   // a chain frame started in the current tile
+  bool dead = false;  // the chain died in the current tile
+  uint64_t term = 0;  // MARK_TERM | p: the tail that ended the chain in the current tile
+  uint64_t ent = ~0ull, fn = 0, fc = 0;  // records of the current group of 8 segments (512 bytes)
+  uint32_t gcur = 0, tcur = 0;           // current group and tile of the region
+  // groups [gcur, gto) to memory (the registers, then empty groups)
+  auto flush_to = [&](uint32_t gto) {
+#pragma unroll 1
+    for (; gcur < gto; gcur++) {
+      const uint64_t ix = (G.t0 + gcur / 16u) * NT + (gcur % 16u) * 8u;
       *reinterpret_cast<uint64_t *>(P.ent + ix) = ent;
       *reinterpret_cast<uint64_t *>(P.ent_n + ix) = fn;
       *reinterpret_cast<uint64_t *>(P.ent_c + ix) = fc;
@@ -498,15 +825,118 @@ __global__ __launch_bounds__(WAVE) void claims_walk(DecodeParams P) {
       fn = 0;
       fc = 0;
     }
-    if (q == WK_WPT - 1) {  // the tile's claim
+  };
+  // tiles [tcur, tto) end before pos: their claims (a dead tile's records mix two chains: identity,
+  // so verification re-walks it from its exact entry; the region is not walked further)
+  auto close_to = [&](uint32_t tto) {
+#pragma unroll 1
+    for (; tcur < tto; tcur++) {
       uint64_t cl = C_ID;
       if (term) cl = term;
       else if (mode == WM_WALK && had) cl = pos;
-      P.claim[tcur] = cl;
+      if (dead) cl = C_ID;
+      P.claim[G.t0 + tcur] = cl;
       had = false;
       term = 0;
+      dead = false;
     }
-    if (mode == WM_SYNC) from = 0;
+  };
+  auto note = [&](uint32_t rel, uint32_t id, bool deliver) {
+    const uint32_t sh = 8u * ((rel >> 6) & 7u);
+    const uint64_t e = (uint64_t)((rel & 63u) | (rs ? 0x40u : 0u)) << sh;
+    const uint64_t m = ((ent >> sh) & 0xFFull) == 0xFFull ? 0xFFull << sh : 0ull;  // (the segment's first)
+    ent = (ent & ~m) | (e & m);
+    rs = false;
+    had = true;
+    fn += (uint64_t)(deliver ? 1u : 0u) << sh;
+    fc += (uint64_t)(deliver && id == 1u ? 1u : 0u) << sh;
+  };
+#pragma unroll 1
+  while (mode == WM_WALK && pos < end) {
+    const uint64_t x = g_rd8(P.bytes, pos);
+    const uint32_t rel = (uint32_t)(pos - A0);
+    if (rel / TILE > tcur) close_to(rel / TILE);
+    if (rel / 512u > gcur) flush_to(rel / 512u);
+    const WHdr h = wk_hdr(x);
+    if ((h.k != 0u) & (h.id - 1u < 2u) & (h.L != 0u) & (h.L <= se - pos - h.k)) {  // (nearly every frame)
+      note(rel % TILE, h.id, true);
+      pos += h.k + h.L;
+      continue;
+    }
+    uint64_t L = h.L;
+    uint32_t k = h.k, id = h.id;
+    if (k == 0) {  // a length varint of 6..10 bytes: the exact grammar
+      const Hdr e = hdr_global(P.bytes, pos, se);
+      if (e.kind == H_VALID || e.kind == H_TAIL_CHANGE || e.kind == H_TAIL_BLOB) {
+        k = e.vlen;
+        L = e.L;
+        id = e.id;
+      } else {
+        id = 0xFF;  // (an error or a cut header: the chain ends)
+      }
+    }
+    if (id > 2u || (id != 0u && L == 0)) {  // the chain dies
+      dead = true;
+      mode = WM_DONE;
+      if (P.stats) atomicAdd(&P.stats[32], 1ull);
+    } else if (id == 0u) {
+      note(rel % TILE, 0u, false);
+      pos += k + 1u;
+    } else {
+      const bool tail = L > se - pos - k;  // the stream ends inside this frame
+      note(rel % TILE, id, !tail || id == 2u);  // (a cut Change is carried, a cut blob delivered)
+      if (tail) {
+        term = MARK_TERM | pos;
+        mode = WM_DONE;
+      } else {
+        pos += k + L;
+      }
+    }
+  }
+  flush_to(ntr * 16u);
+  close_to(ntr);
+}
+
+// ---- record emission ---------------------------------------------------------------------------
+// The tiles verification lets it take (tile_recok: every frame of the tile has a record and its
+// first record is the frame at e_t): rows [tile_base, + tile_count) from the tile's records, a wave
+// per tile, in XCD-contiguous order (neighbouring tiles' column lines meet in one L2). Reads
+// 32 bytes per row and writes the columns; the wire is not read again.
+constexpr uint32_t ER_WAVES = 4;
+__global__ __launch_bounds__(ER_WAVES * WAVE) void emit_rec(DecodeParams P) {
+  if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  uint64_t g;
+  {
+    const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = blockIdx.x % 8u;
+    g = (uint64_t)x * q + min(x, r) + blockIdx.x / 8u;
+  }
+  const uint64_t t = g * ER_WAVES + wid;
+  if (t >= P.tile_prefix[P.nstreams] || !P.tile_recok[t]) return;  // (whole wave)
+  const uint64_t base = P.tile_base[t], n = P.tile_count[t];
+  const uint64_t r0 = P.tile_rec[t];
+  const uint64_t A = tile_geo(P, t).A;
+#pragma unroll 1
+  for (uint64_t i = lane; i < n; i += WAVE) {
+    const uint64_t f = base + i;
+    if (f >= P.cap) break;
+    const uint4 *src = reinterpret_cast<const uint4 *>(P.rec + (r0 + i) * 8u);
+    const uint4 a = src[0], b = src[1];
+    const uint32_t id = (a.x >> 14) & 3u, fl = (a.x >> 17) & 3u;
+    P.payload_off[f] = A + (a.x & 0x3FFFu);
+    P.payload_len[f] = a.y;
+    P.type[f] = (uint8_t)(id | (((a.x >> 16) & 1u) ? DRP_FRAME_PARTIAL : 0u));
+    if (id != 1u) continue;
+    P.key_off[f] = a.z & 0xFFu;
+    P.subset_off[f] = (a.z >> 8) & 0xFFu;
+    P.key_len[f] = a.z >> 16;
+    P.value_off[f] = a.w & 0xFFFFu;
+    P.subset_len[f] = a.w >> 16;
+    P.value_len[f] = (fl & DRP_F_VALUE) ? a.y - (a.w & 0xFFFFu) : 0u;
+    P.change[f] = b.x | ((uint64_t)(b.w & 0x3FFu) << 32);
+    P.from[f] = b.y | ((uint64_t)((b.w >> 10) & 0x3FFu) << 32);
+    P.to[f] = b.z | ((uint64_t)((b.w >> 20) & 0x3FFu) << 32);
+    P.flags[f] = (uint8_t)fl;
   }
 }
 
@@ -515,17 +945,34 @@ __global__ __launch_bounds__(WAVE) void claims_walk(DecodeParams P) {
 
 using namespace drp;
 
+extern "C" hipError_t drp_launch_emit_rec(const DecodeParams *P, uint64_t nt_max, hipStream_t st) {
+  if (nt_max == 0 || !P->rec) return hipSuccess;
+  hipLaunchKernelGGL(spec::emit_rec, dim3((uint32_t)((nt_max + spec::ER_WAVES - 1) / spec::ER_WAVES)),
+                     dim3(spec::ER_WAVES * WAVE), 0, st, *P);
+  return hipGetLastError();
+}
+
+// record slots per region (P->rec_cap) for tpr tiles per region
+extern "C" uint64_t drp_walk_rec_cap(uint32_t tpr) { return (uint64_t)tpr * spec::TILE / spec::WK_REC_BYTES; }
+
 // Region walkers in place of claims_fast: the region list (and the edge tiles onto P->work), then
 // the walkers. P->walk_rp: nstreams + 1 words; P->walk_tpr: tiles per region.
 extern "C" hipError_t drp_launch_claims_walk(const DecodeParams *P, uint64_t nt_max, hipStream_t st) {
   if (nt_max == 0) return hipSuccess;
   hipLaunchKernelGGL(spec::walk_regions, dim3(1), dim3(1024), 0, st, *P);
   const uint64_t maxr = nt_max / P->walk_tpr + P->nstreams + 1;
-  hipLaunchKernelGGL(spec::claims_walk, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
+  hipLaunchKernelGGL(spec::walk_sync, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
+  if (P->walk_hop) {
+    hipLaunchKernelGGL(spec::claims_hop, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
+    return hipGetLastError();
+  }
+  if (P->rec) hipLaunchKernelGGL(spec::claims_walk<true>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
+  else hipLaunchKernelGGL(spec::claims_walk<false>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
   return hipGetLastError();
 }
 
-extern "C" uint32_t drp_walk_tiles_per_region(uint64_t nt_max) {
-  const uint64_t t = (nt_max + spec::WK_REGIONS - 1) / spec::WK_REGIONS;
+extern "C" uint32_t drp_walk_tiles_per_region(uint64_t nt_max, int hop) {
+  const uint64_t nr = hop ? spec::HOP_REGIONS : spec::WK_REGIONS;
+  const uint64_t t = (nt_max + nr - 1) / nr;
   return (uint32_t)(t ? t : 1);
 }

@@ -1,19 +1,23 @@
 // Decoder: the reference's streaming decode API (decode.js:63-142 of
 // mafintosh/dat-replication-protocol v4.1.2) over the gfx950 batch codec.
 //
-// Writes are coalesced (everything written before the event loop comes round again, up to
-// MAX_BATCH bytes) and decoded on the GPU in one call on a worker thread (frame split +
-// Change decode, libdrp via lib/drp.node). The returned frame table is replayed here with the
-// reference's callback discipline: a change/blob callback increments _pending, and replay stops
-// while _pending > 0 and resumes from _down (decode.js:89-99, 144-169). The event sequence is
-// the reference's; only the timing of write callbacks differs (a write below the batch
-// threshold is acknowledged when queued; one that fills a batch when that batch has been
-// delivered, which is the backpressure).
+// Writes reach _write one at a time, as in the reference; the ones buffered behind the write
+// being consumed (the stream's highWaterMark is MAX_BATCH) are read ahead: up to PIECE bytes of
+// them form a batch, decoded on the GPU in one call on a worker thread (frame split + Change
+// decode, libdrp via lib/drp.node, the written chunks handed over as they are: libdrp gathers
+// the ranges it stages, so nothing is concatenated here). While one batch is replayed the next
+// is decoded. The replay keeps the reference's discipline exactly: a frame is delivered while
+// the write holding its last byte is consumed, a change/blob callback increments _pending and
+// delivery stops while _pending > 0 (decode.js:89-99, 144-169), and a write's callback fires
+// once every frame it completes has been delivered and acknowledged (decode.js:167-168), so
+// producers see the reference's backpressure and the callbacks interleave as they do there.
 //
 // Carry across batches (decode.js:75-81): an incomplete header (<= 10 bytes) is prepended to
 // the next batch; an incomplete Change frame is collected once into a buffer of its declared
 // size (as _onchangedata fills _buffer, decode.js:229-247) and decoded when complete; the
 // bytes of an open blob continue through the next batch as pass-through (never sent to HBM).
+// Change values and blob pieces are slices of the written chunks (decode.js:179-202, 205-214
+// slice the chunk they were given); only a frame that straddles two writes is copied.
 'use strict'
 
 var stream = require('stream')
@@ -21,12 +25,13 @@ var util = require('util')
 var native = require('./native')
 
 var FLUSH = Buffer.from([0]) // identity-compared end sentinel (decode.js:6, :125)
-var MAX_BATCH = Number(process.env.DRP_MAX_BATCH) || 64 * 1024 * 1024
-var PIECE = Number(process.env.DRP_PIECE) || 16 * 1024 * 1024 // bytes per GPU call
+var MAX_BATCH = Number(process.env.DRP_MAX_BATCH) || 64 * 1024 * 1024 // bytes written ahead
+var PIECE = Math.min(MAX_BATCH, Number(process.env.DRP_PIECE) || 16 * 1024 * 1024) // bytes per GPU call
 var MAX_FRAME = require('buffer').constants.MAX_LENGTH
 
-// a batch whose frames average at most TEXT_PER_FRAME bytes is turned into one latin1 string
-// for its ASCII keys (cheaper than a string per key); larger frames keep one string per key
+// a batch whose frames average at most TEXT_PER_FRAME bytes has its ASCII keys cut from one
+// latin1 string per written chunk (cheaper than a string per key); larger frames keep one
+// string per key
 var TEXT_PER_FRAME = 512
 var TEXT_MAX = 256 * 1024 * 1024 // (below V8's string length limit)
 var TYPE_MASK = 0x3f
@@ -70,18 +75,6 @@ BlobStream.prototype._read = function () {
   if (fn) fn()
 }
 
-// The chunks of a batch in one buffer: a page-locked staging block from the addon when one is
-// free (the GPU copy then runs by DMA at the PCIe rate), else ordinary memory. The block is not
-// reused while any slice of this batch is alive (native.js / drp_napi.c pinnedBuffer).
-function coalesce (chunks) {
-  var total = 0
-  for (var i = 0; i < chunks.length; i++) total += chunks[i].length
-  var out = native.pinnedBuffer ? native.pinnedBuffer(total) : null
-  if (out === null) return Buffer.concat(chunks, total)
-  for (var j = 0, at = 0; j < chunks.length; j++) at += chunks[j].copy(out, at)
-  return out
-}
-
 // --- default handlers (decode.js:50-61) -------------------------------------------
 function noopFinalize (cb) { cb() }
 function noopChange (change, cb) { cb() }
@@ -95,6 +88,9 @@ var ERRORS = {
   5: function () { return 'Decoded message is not valid' }
 }
 
+// the decode result of a batch that needs no GPU call (its bytes only fill a carried frame)
+var NOTHING = { n: 0, errCode: 0, tailKind: 0, consumed: 0, blobRemaining: 0, frameBytes: 0 }
+
 // opts (not in the reference, whose constructor takes none):
 //   keyHash: true  - every change object also carries keyHash, the XXH64 of its key bytes as
 //                    a BigInt, computed on the GPU (drp_keys.hip)
@@ -102,7 +98,7 @@ var ERRORS = {
 //                    streams are spread over a node's GPUs this way (index.js: shard)
 function Decoder (opts) {
   if (!(this instanceof Decoder)) return new Decoder(opts)
-  stream.Writable.call(this)
+  stream.Writable.call(this, { highWaterMark: MAX_BATCH })
   this._keyPost = !!(opts && opts.keyHash)
 
   this.destroyed = false
@@ -111,36 +107,35 @@ function Decoder (opts) {
   this.blobs = 0
 
   this._pending = 0
-  this._paused = false    // replay stopped at a callback that has not been acknowledged
+  this._paused = false    // delivery stopped at a callback that has not been acknowledged
 
   this._onchange = noopChange
   this._onblob = drainBlob
   this._onfinalize = noopFinalize
 
   this._ctx = native.context(opts && opts.device)
-  this._queue = []        // written chunks not yet handed to the GPU
-  this._queued = 0
-  this._scheduled = false
-  this._inflight = false  // a batch is on the GPU (worker thread)
-  this._ready = null      // a decoded batch waiting for the one being replayed
+  // read-ahead: the write being consumed and the stream's buffered writes behind it
+  this._cw = null         // the write being consumed (_write's chunk) and its callback
+  this._wcb = null
+  this._slots = []        // writes whose last byte is in a batch, not yet consumed: {chunk, batch, end}
+  this._q = []            // written chunks; [_qh, ...) not yet taken by _write
+  this._qh = 0
+  this._taken = 0         // of those, how many are already placed (whole or in part) in batches
+  this._rest = null       // the part of a write not yet in a batch: {chunk, off}
+  this._batches = []      // formed batches in order; [0] is the one delivered from
+  this._inflight = null   // the batch on the GPU (worker thread)
   this._halt = false      // a batch ended in an error: nothing after it is decoded
-  this._held = null       // write callback held back until its batch is on the GPU
-  this._final = null      // end(): finalize once everything before it is delivered
   this._carry = null      // an incomplete frame header (<= 10 bytes)
   this._partial = null    // an incomplete Change frame of known size: {buf, filled}
   this._blobLeft = 0      // payload bytes of the open blob still to come
   this._blob = null       // the open BlobStream
-  this._res = null        // decoded batch being replayed
-  this._buf = null        // its bytes
-  this._chunks = null     // the written chunks it was made of, and where each starts in it
-  this._starts = null
-  this._ck = 0            // the chunk holding the blob bytes delivered next
+  // delivery position in _batches[0]
+  this._next = 0          // next frame
+  this._ck = 0            // chunk holding the bytes delivered next
   this._blobPos = -1      // batch offset of the next piece of a blob row being delivered
-  this._text = null       // its bytes as one latin1 string (ASCII keys are cut from it)
-  this._tooBig = 0        // its carried Change frame was larger than a Buffer can hold
-  this._next = 0          // next frame to deliver
-  // ms, summed (and the bytes staged into HBM / blob payload bytes that stayed in host memory)
-  this.timing = { batches: 0, h2d: 0, gpu: 0, d2h: 0, convert: 0, replay: 0, h2dBytes: 0, h2dSkipped: 0 }
+  // ms, summed; bytes staged into HBM, blob payload bytes left in host memory, bytes copied on
+  // the host (gathered for HBM, frames straddling two writes, carried frames)
+  this.timing = { batches: 0, h2d: 0, gpu: 0, d2h: 0, convert: 0, replay: 0, h2dBytes: 0, h2dSkipped: 0, hostCopied: 0 }
 
   var self = this
   this._up = function () {
@@ -150,11 +145,7 @@ function Decoder (opts) {
   this._down = function () {
     if (--self._pending > 0 || !self._paused) return
     self._paused = false
-    self._replay()
-  }
-  this._kickFn = function () {
-    self._scheduled = false
-    self._kick()
+    self._deliver()
   }
 }
 util.inherits(Decoder, stream.Writable)
@@ -172,25 +163,27 @@ Decoder.prototype.blob = function (fn) { this._onblob = fn }
 Decoder.prototype.finalize = function (fn) { this._onfinalize = fn }
 
 Decoder.prototype._write = function (data, enc, cb) {
-  if (data === FLUSH) {
-    this._final = cb
-    return this._kick()
+  var q = this._q
+  while (this._qh < q.length && q[this._qh] !== data) this._qh++ // (chunks the stream refused)
+  if (this._qh < q.length) this._qh++
+  if (this._qh > 4096 && this._qh * 2 > q.length) {
+    this._q = q.slice(this._qh)
+    this._qh = 0
+  }
+  if (data === FLUSH) { // every write before it has been consumed (decode.js:121-124)
+    this._onfinalize(cb)
+    return
   }
   this.bytes += data.length
-  this._queue.push(data)
-  this._queued += data.length
-  if (this._queued >= MAX_BATCH) {
-    // backpressure: acknowledged once every queued byte has been handed to the GPU (_kick), so at
-    // most one batch on the GPU, one decoded and waiting, one replaying and MAX_BATCH queued bytes
-    // are held in memory at a time
-    this._held = cb
-    return this._kick()
+  this._cw = data
+  this._wcb = cb
+  if (this._taken > 0) {
+    this._taken-- // (read ahead into a batch already)
+  } else {
+    this._rest = { chunk: data, off: 0 }
+    this._form()
   }
-  cb()
-  if (!this._scheduled) {
-    this._scheduled = true
-    setImmediate(this._kickFn)
-  }
+  this._deliver()
 }
 
 Decoder.prototype.end = function (data, enc, cb) {
@@ -201,95 +194,126 @@ Decoder.prototype.end = function (data, enc, cb) {
   stream.Writable.prototype.end.call(this, cb)
 }
 
-// Hand the queued bytes to the GPU (one batch), or finish when nothing is left. At most one
-// batch is on the GPU and one waits decoded while another is replayed: batch k + 1 is split and
-// decoded on the worker thread while batch k's callbacks run here.
-Decoder.prototype._kick = function () {
-  if (this._inflight || this._ready || this._halt || this.destroyed) return
-  if (!this._queued) {
-    var held = this._held
-    this._held = null
-    if (held) held()
-    if (this._final && !this._queued && !this._res && !this._inflight) {
-      var fin = this._final
-      this._final = null
-      this._onfinalize(fin) // decode.js:125-128
-    }
-    return
+// Every written chunk is also queued here (write() below) until _write takes it: the writes
+// behind the one being consumed are read ahead from this queue, not from the stream's internals.
+Decoder.prototype.write = function (chunk, enc, cb) {
+  if (typeof chunk === 'string') chunk = Buffer.from(chunk, typeof enc === 'string' ? enc : 'utf8')
+  else if (chunk instanceof Uint8Array && !Buffer.isBuffer(chunk)) {
+    chunk = Buffer.from(chunk.buffer, chunk.byteOffset, chunk.byteLength)
   }
-  // at most PIECE bytes go to the GPU at a time (a big write is cut into pieces, so the decode of
-  // piece k + 1 overlaps the replay of piece k); the rest stays queued
-  var chunks = this._queue
-  if (this._queued <= PIECE) {
-    this._queue = []
-    this._queued = 0
-  } else {
-    var took = 0
-    var k = 0
-    while (took < PIECE) took += chunks[k++].length
-    var last = chunks[k - 1]
-    var over = took - PIECE
-    this._queue = chunks.slice(k)
-    if (over > 0) { // (slices share the write's memory: no copy)
-      chunks[k - 1] = last.slice(0, last.length - over)
-      this._queue.unshift(last.slice(last.length - over))
-    }
-    chunks = chunks.slice(0, k)
-    this._queued -= PIECE
-  }
-  var p = this._partial
-  if (p) {
-    // collect the rest of a Change frame of known size: each byte is copied once
-    var k = 0
-    while (k < chunks.length && p.filled < p.buf.length) {
-      var c = chunks[k]
-      var take = Math.min(c.length, p.buf.length - p.filled)
-      c.copy(p.buf, p.filled, 0, take)
-      p.filled += take
-      if (take < c.length) chunks[k] = c.slice(take)
-      else k++
-    }
-    if (p.filled < p.buf.length) return this._kick() // nothing else to decode yet (or the rest of the queue)
-    this._partial = null
-    chunks = [p.buf].concat(chunks.slice(k))
-  } else if (this._carry) {
-    chunks.unshift(this._carry)
-    this._carry = null
-  }
-  var batch = chunks.length === 1 ? chunks[0] : coalesce(chunks)
-  // where each chunk starts in the batch: blob payloads are delivered as slices of the written
-  // chunks themselves (decode.js:179-202 slices the chunk it was given), not of the batch copy
-  var starts = new Array(chunks.length)
-  for (var j = 0, at = 0; j < chunks.length; j++) {
-    starts[j] = at
-    at += chunks[j].length
-  }
-  this._inflight = true
-  var held = this._queued ? null : this._held // all of its bytes are on their way to the GPU now
-  if (held) this._held = null
-  var self = this
-  native.decode(this._ctx, batch, this._blobLeft, function (err, res) {
-    self._ondecoded(err, res, batch, chunks, starts)
-  }, this._keyPost)
-  if (held) held()
+  if (Buffer.isBuffer(chunk) && !this._writableState.ended && !this.destroyed) this._q.push(chunk)
+  return stream.Writable.prototype.write.call(this, chunk, typeof enc === 'string' ? null : enc, cb)
 }
 
-Decoder.prototype._ondecoded = function (err, res, batch, chunks, starts) {
-  this._inflight = false
+Decoder.prototype._bufferedFirst = function () {
+  return this._q[this._qh]
+}
+
+Decoder.prototype._bufferedNext = function () {
+  return this._q[this._qh + this._taken]
+}
+
+// Form the next batch: up to PIECE bytes of the unplaced writes (the rest of a write cut at a
+// batch edge, then the buffered writes in order), behind the carry of the batch before, and hand
+// it to the GPU. One batch is on the GPU at a time (the next one's carry depends on it).
+Decoder.prototype._form = function () {
+  if (this._inflight || this._halt || this.destroyed) return
+  var segs = [] // {chunk, a, b, write}: bytes [a, b) of a written chunk; write: its last byte is here
+  var size = 0
+  while (size < PIECE) {
+    var r = this._rest
+    if (!r) {
+      var e = this._bufferedNext()
+      if (!e || e === FLUSH) break
+      this._taken++
+      r = this._rest = { chunk: e, off: 0 }
+    }
+    var take = Math.min(r.chunk.length - r.off, PIECE - size)
+    var last = r.off + take === r.chunk.length
+    segs.push({ chunk: r.chunk, a: r.off, b: r.off + take, write: last, first: r.off === 0 })
+    size += take
+    if (last) this._rest = null
+    else r.off += take
+  }
+  if (!segs.length) return
+  var chunks = []
+  var starts = []
+  var at = 0
+  var slots = []
+  var first = [] // the writes whose first byte is in this batch
+  for (var q = 0; q < segs.length; q++) if (segs[q].first) first.push(segs[q].chunk)
+  var p = this._partial
+  var i = 0
+  if (p) {
+    // collect the rest of a Change frame of known size: each byte is copied once (a write that
+    // ends inside it ends at its position in that frame's buffer, the batch's first chunk)
+    while (i < segs.length && p.filled < p.buf.length) {
+      var s = segs[i]
+      var n = Math.min(s.b - s.a, p.buf.length - p.filled)
+      s.chunk.copy(p.buf, p.filled, s.a, s.a + n)
+      p.filled += n
+      this.timing.hostCopied += n
+      s.a += n
+      if (s.a < s.b) break // (the frame ends inside this segment; the rest follows it)
+      if (s.write) slots.push({ chunk: s.chunk, end: p.filled })
+      i++
+    }
+    if (p.filled < p.buf.length) { // nothing to decode yet: these writes only fill the frame
+      this._queueBatch({ chunks: [], starts: [], size: 0, res: NOTHING, tooBig: 0, texts: null, first: first }, slots)
+      return this._form()
+    }
+    this._partial = null
+    chunks.push(p.buf)
+    starts.push(0)
+    at = p.buf.length
+  } else if (this._carry) {
+    chunks.push(this._carry)
+    starts.push(0)
+    at = this._carry.length
+    this._carry = null
+  }
+  for (; i < segs.length; i++) {
+    var g = segs[i]
+    if (g.b > g.a) {
+      chunks.push(g.a === 0 && g.b === g.chunk.length ? g.chunk : g.chunk.slice(g.a, g.b)) // (slices: no copy)
+      starts.push(at)
+      at += g.b - g.a
+    }
+    if (g.write) slots.push({ chunk: g.chunk, end: at })
+  }
+  var batch = { chunks: chunks, starts: starts, size: at, res: null, tooBig: 0, texts: null, first: first }
+  this._queueBatch(batch, slots)
+  this._inflight = batch
+  var self = this
+  native.decode(this._ctx, chunks.length === 1 ? chunks[0] : chunks, this._blobLeft, function (err, res) {
+    self._ondecoded(err, res, batch)
+  }, this._keyPost)
+}
+
+Decoder.prototype._queueBatch = function (batch, slots) {
+  this._batches.push(batch)
+  for (var k = 0; k < slots.length; k++) {
+    slots[k].batch = batch
+    this._slots.push(slots[k])
+  }
+}
+
+Decoder.prototype._ondecoded = function (err, res, batch) {
+  this._inflight = null
   if (this.destroyed) return
   if (err) return this.destroy(err)
   // the carry into the next batch (decode.js:75-81) is known now, before the replay
   var tooBig = 0
   if (!res.errCode) {
-    var rest = batch.length - res.consumed
+    var rest = batch.size - res.consumed
     if (res.tailKind === TAIL_HEADER) {
-      this._carry = Buffer.from(batch.slice(res.consumed)) // copied, as into _header
+      this._carry = this._gather(batch, res.consumed, batch.size) // copied, as into _header
     } else if (res.tailKind === TAIL_CHANGE) {
       if (res.frameBytes > MAX_FRAME) {
         tooBig = res.frameBytes // reported after the frames before it (the reference throws)
       } else {
         var buf = Buffer.allocUnsafe(res.frameBytes) // decode.js:227 allocates _buffer the same way
-        batch.copy(buf, 0, res.consumed)
+        this._copyOut(batch, res.consumed, batch.size, buf, 0)
         this._partial = { buf: buf, filled: rest }
       }
     }
@@ -306,42 +330,92 @@ Decoder.prototype._ondecoded = function (err, res, batch, chunks, starts) {
     tm.convert += t.convert
     tm.h2dBytes += t.h2dBytes || 0
     tm.h2dSkipped += t.h2dSkipped || 0
+    tm.hostCopied += t.hostCopied || 0
   }
-  var entry = { res: res, buf: batch, chunks: chunks, starts: starts, tooBig: tooBig }
-  if (this._res) {
-    this._ready = entry
-    return
-  }
-  this._play(entry)
+  batch.res = res
+  batch.tooBig = tooBig
+  batch.texts = res.asciiKeys && res.n * TEXT_PER_FRAME >= batch.size ? [] : null
+  this._form() // the next batch goes to the GPU before this one's callbacks run
+  this._deliver()
 }
 
-Decoder.prototype._play = function (e) {
-  var res = e.res
-  var batch = e.buf
-  this._res = res
-  this._buf = batch
-  this._chunks = e.chunks
-  this._starts = e.starts
+// bytes [a, b) of a batch into dst at d (they may span chunks)
+Decoder.prototype._copyOut = function (batch, a, b, dst, d) {
+  var chunks = batch.chunks
+  var starts = batch.starts
+  var k = 0
+  while (k + 1 < chunks.length && starts[k + 1] <= a) k++
+  this.timing.hostCopied += b - a
+  for (; a < b; k++) {
+    var n = Math.min(b, starts[k] + chunks[k].length) - a
+    chunks[k].copy(dst, d, a - starts[k], a - starts[k] + n)
+    d += n
+    a += n
+  }
+}
+
+Decoder.prototype._gather = function (batch, a, b) {
+  var out = Buffer.allocUnsafe(b - a)
+  this._copyOut(batch, a, b, out, 0)
+  return out
+}
+
+// Deliver frames of the front batch while no callback is outstanding, up to the end of the
+// write being consumed; then acknowledge that write (decode.js:144-169).
+Decoder.prototype._deliver = function () {
+  while (!this.destroyed && this._pending <= 0) {
+    var batch = this._batches[0]
+    var slot = this._slots[0]
+    if (!this._cw) return // (no write being consumed: wait for _write)
+    if (slot && slot.chunk === this._cw && slot.batch === batch && batch && batch.res) {
+      if (!this._replay(batch, slot.end)) return
+      // every frame the write completes has been delivered and acknowledged; its callback lets
+      // the stream hand over the next buffered write at once, whose frames the reference then
+      // delivers before this callback returns: so that batch must be decoded first
+      if (this._nextOnGpu()) return // (resumed by _ondecoded)
+      this._slots.shift()
+      var cb = this._wcb
+      this._cw = null
+      this._wcb = null
+      cb()
+      return
+    }
+    if (!batch || !batch.res) return // (the write's frames are still on the GPU)
+    // the write ends in a later batch: this one is delivered whole
+    if (!this._replay(batch, Infinity)) return
+    this._retire()
+  }
+}
+
+// Is the first byte of the next buffered write still on its way (not yet decoded)?
+Decoder.prototype._nextOnGpu = function () {
+  if (this._halt) return false
+  var e = this._bufferedFirst()
+  if (!e || e === FLUSH) return false
+  if (this._taken === 0) this._form() // (not read ahead yet: now)
+  if (this._taken === 0) return true // (behind the batch on the GPU)
+  var b = this._inflight
+  return b !== null && b.first.indexOf(e) >= 0
+}
+
+Decoder.prototype._retire = function () {
+  this._batches.shift()
+  this._next = 0
   this._ck = 0
   this._blobPos = -1
-  this._tooBig = e.tooBig
-  this._text = res.asciiKeys && batch.length <= TEXT_MAX && batch.length <= TEXT_PER_FRAME * res.n
-    ? batch.toString('latin1') : null
-  this._next = 0
-  this._kick() // the next batch goes to the GPU before this one's callbacks run
-  this._replay()
 }
 
-// Deliver decoded frames in order while no callback is outstanding (decode.js:144-169).
+// Deliver the batch's frames completed before batch offset `lim` (the end of the write being
+// consumed). false: stopped at a callback not yet acknowledged, or the stream ended.
 // Change frames are built inline (the hot loop: one object, one key string, one value slice per
-// frame); keys the GPU flagged ASCII are cut from one latin1 string of the batch (the same string
-// buf.toString('utf8', ...) would give, without a UTF-8 decode per key).
-Decoder.prototype._replay = function () {
-  var res = this._res
-  var buf = this._buf
+// frame); keys the GPU flagged ASCII are cut from one latin1 string of their written chunk (the
+// same string buf.toString('utf8', ...) would give, without a UTF-8 decode per key).
+Decoder.prototype._replay = function (batch, lim) {
+  var res = batch.res
   var n = res.n
   var type = res.type
   var off = res.off
+  var len = res.len
   var flags = res.flags
   var ko = res.ko
   var kl = res.kl
@@ -353,97 +427,136 @@ Decoder.prototype._replay = function () {
   var cf = res.from
   var ct = res.to
   var keyHash = res.keyHash
-  var text = this._text
+  var chunks = batch.chunks
+  var starts = batch.starts
+  var texts = batch.texts
   var down = this._down
   var i = this._next
+  var k = this._ck
   var t0 = process.hrtime()
-  // (no callback can re-enter this loop: _down only resumes a paused replay)
   while (i < n && this._pending <= 0) {
+    var o = off[i]
     if ((type[i] & TYPE_MASK) !== 1) {
-      if (this._deliverBlob(i)) i++ // (one push per written chunk the payload spans)
+      if (o > lim) break // (its header ends in a later write)
+      var r = this._deliverBlob(batch, i, lim)
+      if (this._ck > k) k = this._ck
+      if (r === 0) break // (the next piece is in a later write)
+      if (r === 2) i++
       if (this.destroyed) break
       continue
     }
+    var e = o + len[i]
+    if (e > lim) break // (its last byte is in a later write)
     // messages.Change.decode result shape: {subset, key, change, from, to, value}
-    var o = off[i]
+    while (k + 1 < chunks.length && starts[k + 1] <= o) k++
+    var c = chunks[k]
+    var base = starts[k]
+    var inChunk = e <= base + c.length
+    if (!inChunk) { // (the frame straddles two writes: its payload is copied once)
+      c = this._gather(batch, o, e)
+      base = o
+    }
     var f = flags[i]
-    var k0 = o + ko[i]
+    var k0 = o + ko[i] - base
     var k1 = k0 + kl[i]
-    var vo = o + vcol[i]
+    var v0 = o + vcol[i] - base
+    var key
+    if (texts !== null && inChunk && (f & KEY_ASCII)) {
+      var s = texts[k]
+      if (s === undefined) s = texts[k] = c.length <= TEXT_MAX ? c.toString('latin1') : null
+      key = s !== null ? s.substring(k0, k1) : c.toString('utf8', k0, k1)
+    } else {
+      key = c.toString('utf8', k0, k1)
+    }
     var change = {
-      subset: (f & 1) ? buf.toString('utf8', o + so[i], o + so[i] + sl[i]) : '',
-      key: (text !== null && (f & KEY_ASCII)) ? text.substring(k0, k1) : buf.toString('utf8', k0, k1),
+      subset: (f & 1) ? c.toString('utf8', o + so[i] - base, o + so[i] - base + sl[i]) : '',
+      key: key,
       change: cc[i],
       from: cf[i],
       to: ct[i],
-      value: (f & 2) ? buf.slice(vo, vo + vl[i]) : null
+      value: (f & 2) ? c.slice(v0, v0 + vl[i]) : null
     }
     if (keyHash) change.keyHash = keyHash[i]
     this.changes++
     this._pending++ // released by the handler's cb (_up, decode.js:89-93)
+    this._next = i + 1
+    this._ck = k
     this._onchange(change, down)
     i++
     if (this.destroyed) break
   }
   this._next = i
+  this._ck = k
   var dt = process.hrtime(t0)
   this.timing.replay += dt[0] * 1e3 + dt[1] * 1e-6
-  if (this.destroyed) return
+  if (this.destroyed) return false
   if (this._pending > 0) {
     this._paused = true // resumed by _down
-    return
+    return false
   }
-  if (res.errCode) return this.destroy(new Error(ERRORS[res.errCode](res.errDetail)))
-  if (this._tooBig) {
-    return this.destroy(new RangeError('Change frame of ' + this._tooBig + ' bytes exceeds the maximum Buffer size'))
+  if (i < n) return true // (the rest completes in later writes)
+  if (res.errCode && this._errPos(batch) < lim) {
+    this.destroy(new Error(ERRORS[res.errCode](res.errDetail)))
+    return false
   }
-  this._res = null
-  this._buf = null
-  this._chunks = null
-  this._starts = null
-  this._text = null
-  var next = this._ready
-  this._ready = null
-  if (next) this._play(next)
-  else this._kick()
+  if (batch.tooBig && batch.size <= lim) {
+    this.destroy(new RangeError('Change frame of ' + batch.tooBig + ' bytes exceeds the maximum Buffer size'))
+    return false
+  }
+  return true
+}
+
+// where a batch's protocol error is met: past its last delivered frame (the malformed Change
+// itself when the error is in a Change payload)
+Decoder.prototype._errPos = function (batch) {
+  var res = batch.res
+  var n = res.n
+  var bad = res.errCode === 4 || res.errCode === 5
+  if (bad) return res.off[n] + res.len[n] - 1
+  return n ? res.off[n - 1] + Math.min(res.len[n - 1], batch.size - res.off[n - 1]) : 0
 }
 
 // One piece of blob frame i (or of the continuation of one opened in an earlier batch): the
 // part of its payload inside the next written chunk, pushed as a slice of that chunk with one
-// callback, as _onblobdata pushes each chunk's part (decode.js:179-202); true once the frame's
-// last piece is delivered (and the blob ended, unless it continues past the batch).
-Decoder.prototype._deliverBlob = function (i) {
-  var res = this._res
+// callback, as _onblobdata pushes each chunk's part (decode.js:179-202). 2: the frame's last
+// piece is delivered (and the blob ended, unless it continues past the batch); 1: a piece was
+// delivered; 0: the next piece lies in a later write.
+Decoder.prototype._deliverBlob = function (batch, i, lim) {
+  var res = batch.res
   var type = res.type[i]
   var off = res.off[i]
-  var end = off + Math.min(res.len[i], this._buf.length - off)
+  var end = off + Math.min(res.len[i], batch.size - off)
   var pos = this._blobPos
   if (pos < 0) {
     pos = off
     if (!(type & CONT)) {
       this.blobs++
       this._blob = new BlobStream(this)
-      this._onblob(this._blob, this._down)
+      this._onblob(this._blob, this._down) // (its cb balances the _pending++ at the blob's end)
     }
   }
-  var chunks = this._chunks
-  var starts = this._starts
+  if (pos < end && pos >= lim) {
+    this._blobPos = pos
+    return 0
+  }
+  var chunks = batch.chunks
+  var starts = batch.starts
   var k = this._ck
   while (k + 1 < chunks.length && starts[k + 1] <= pos) k++
   this._ck = k
   var stop = Math.min(end, starts[k] + chunks[k].length)
-  var data = pos < stop ? chunks[k].slice(pos - starts[k], stop - starts[k]) : this._buf.slice(pos, pos)
+  var data = pos < stop ? chunks[k].slice(pos - starts[k], stop - starts[k]) : Buffer.alloc(0)
   var blob = this._blob
   var last = stop >= end
   this._blobPos = last ? -1 : stop
   blob._push(data, this._up())
-  if (!last) return false
+  if (!last) return 1
   if (!(type & PARTIAL)) { // decode.js:171-177
     this._pending++ // released by the blob handler's cb
     this._blob = null
     blob._end()
   }
-  return true
+  return 2
 }
 
 module.exports = Decoder

@@ -43,5 +43,4 @@ exports.decode = addon.decode
 exports.decodeSync = addon.decodeSync
 exports.encode = addon.encode
 exports.indexAllgather = addon.indexAllgather
-exports.pinnedBuffer = addon.pinnedBuffer
 exports.abiVersion = addon.abiVersion

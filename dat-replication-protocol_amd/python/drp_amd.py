@@ -23,7 +23,7 @@ EXPORTS = [
     "drp_abi_version", "drp_open", "drp_close", "drp_stream", "drp_synchronize",
     "drp_last_timing", "drp_set_tile", "drp_set_strict", "drp_set_exact", "drp_set_key_post",
     "drp_set_blob_skip", "drp_decode_scratch_bytes",
-    "drp_decode_device", "drp_decode_batch", "drp_decode_stage", "drp_decode_fetch",
+    "drp_decode_device", "drp_decode_batch", "drp_decode_stage", "drp_decode_stage_v", "drp_decode_fetch",
     "drp_encode_size", "drp_encode_device",
     "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results", "drp_device",
     "drp_comm_id", "drp_comm_init_rank", "drp_comm_init_all", "drp_comm_destroy",
@@ -68,11 +68,15 @@ class StreamStats(C.Structure):
     _fields_ = [("frames", U64), ("changes", U64), ("blobs", U64), ("wire_bytes", U64)]
 
 
+class Chunk(C.Structure):
+    _fields_ = [("bytes", P), ("n", U64)]
+
+
 class Timing(C.Structure):
     _fields_ = [("decode_ms", C.c_float), ("finalize_ms", C.c_float), ("total_ms", C.c_float),
                 ("strict_reruns", U32), ("spec_repairs", U32), ("exact_retries", U32), ("verify_relisted", U32),
                 ("seg_repairs", U32), ("reserved", U32), ("h2d_ms", C.c_float), ("d2h_ms", C.c_float),
-                ("h2d_bytes", U64), ("h2d_skipped", U64)]
+                ("h2d_bytes", U64), ("h2d_skipped", U64), ("host_copied", U64)]
 
 
 _lib = None
@@ -107,6 +111,8 @@ def lib():
                                        C.POINTER(U32), C.POINTER(U32)]
         L.drp_decode_stage.argtypes = [P, P, U64, C.POINTER(Carry), C.POINTER(U64), C.POINTER(U64),
                                        C.POINTER(U32), C.POINTER(U32)]
+        L.drp_decode_stage_v.argtypes = [P, C.POINTER(Chunk), U64, C.POINTER(Carry), C.POINTER(U64), C.POINTER(U64),
+                                         C.POINTER(U32), C.POINTER(U32)]
         L.drp_decode_fetch.argtypes = [P, C.POINTER(Frames), C.POINTER(Changes), U64, U64]
         L.drp_encode_size.argtypes = [P, C.POINTER(ChangeSrc), U64, C.POINTER(U64)]
         L.drp_encode_device.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, P, U64]
@@ -128,7 +134,7 @@ def lib():
         for f in ["drp_open", "drp_synchronize", "drp_last_timing", "drp_set_tile",
                   "drp_set_strict", "drp_set_exact", "drp_set_key_post", "drp_set_blob_skip", "drp_decode_device",
                   "drp_decode_batch",
-                  "drp_decode_stage", "drp_decode_fetch", "drp_encode_size",
+                  "drp_decode_stage", "drp_decode_stage_v", "drp_decode_fetch", "drp_encode_size",
                   "drp_encode_device", "drp_encode_batch", "drp_index_scan",
                   "drp_stream_stats_from_results", "drp_device", "drp_comm_id", "drp_comm_init_rank",
                   "drp_comm_init_all", "drp_index_allgather", "drp_index_allgather_multi",
@@ -275,15 +281,22 @@ class Ctx:
 
     def decode_staged(self, wire, blob_remaining=0, pieces=1, key_hash=False):
         """drp_decode_stage, then drp_decode_fetch of the rows in `pieces` consecutive
-        fetches into host columns sized from the frame count (the N-API addon's path)."""
-        w = np.frombuffer(bytes(wire), np.uint8) if not isinstance(wire, np.ndarray) else wire
-        n = int(w.size)
+        fetches into host columns sized from the frame count (the N-API addon's path). `wire`
+        as a list of byte strings: the batch is those chunks end to end (drp_decode_stage_v)."""
         carry = Carry(blob_remaining, 0, 0, 0, 0)
         nf, ef, ec, ed = U64(), U64(), U32(), U32()
-        buf = w if n else np.zeros(16, np.uint8)
         _chk("drp_set_key_post", self.L.drp_set_key_post(self.h, KEY_POST_HASH if key_hash else KEY_POST_OFF))
-        _chk("drp_decode_stage", self.L.drp_decode_stage(self.h, _p(buf), n, C.byref(carry), C.byref(nf),
-                                                         C.byref(ef), C.byref(ec), C.byref(ed)))
+        if isinstance(wire, (list, tuple)):
+            arrs = [np.frombuffer(bytes(c), np.uint8) if len(c) else np.zeros(1, np.uint8) for c in wire]
+            ch = (Chunk * max(1, len(arrs)))(*[Chunk(_p(a), len(c)) for a, c in zip(arrs, wire)])
+            _chk("drp_decode_stage_v", self.L.drp_decode_stage_v(self.h, ch, len(arrs), C.byref(carry), C.byref(nf),
+                                                                 C.byref(ef), C.byref(ec), C.byref(ed)))
+        else:
+            w = np.frombuffer(bytes(wire), np.uint8) if not isinstance(wire, np.ndarray) else wire
+            n = int(w.size)
+            buf = w if n else np.zeros(16, np.uint8)
+            _chk("drp_decode_stage", self.L.drp_decode_stage(self.h, _p(buf), n, C.byref(carry), C.byref(nf),
+                                                             C.byref(ef), C.byref(ec), C.byref(ed)))
         rows = int(nf.value) + (1 if ec.value in (ERR_CHANGE, ERR_REQUIRED) else 0)
         o = alloc_host_outputs(rows, key_hash)
         bounds = np.linspace(0, rows, pieces + 1).astype(np.int64)

@@ -37,7 +37,7 @@ extern "C" {
 /* libdrp is built with -fvisibility=hidden: the declarations below are its only exports. */
 #pragma GCC visibility push(default)
 
-#define DRP_ABI_VERSION 4
+#define DRP_ABI_VERSION 5
 
 /* ---- return codes -------------------------------------------------------- */
 #define DRP_OK 0
@@ -164,6 +164,7 @@ typedef struct drp_timing {
   float d2h_ms;   /* copying the columns back (drp_decode_fetch) */
   uint64_t h2d_bytes;   /* bytes of the last host batch staged into HBM */
   uint64_t h2d_skipped; /* its blob payload bytes never staged (pass-through, drp_set_blob_skip) */
+  uint64_t host_copied; /* bytes of a chunked batch gathered on the host (drp_decode_stage_v) */
 } drp_timing;
 
 /* ---- context ------------------------------------------------------------- */
@@ -252,6 +253,19 @@ int drp_decode_stage(drp_ctx *ctx, const uint8_t *bytes, uint64_t n, drp_carry *
                      uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail);
 int drp_decode_fetch(drp_ctx *ctx, const drp_frames *frames, const drp_changes *cols, uint64_t first,
                      uint64_t rows);
+/* drp_decode_stage over a batch the caller holds as chunks (its queued writes), laid end to end:
+ * the caller never concatenates them. The ranges the decode stages into HBM (all of the batch,
+ * or with blob skipping everything but the blob payloads) are gathered from the chunks into
+ * page-locked memory of the ctx and copied by DMA; drp_timing.host_copied reports the bytes
+ * gathered, so blob payloads are copied neither on the host nor to the device. Offsets in the
+ * result are batch offsets (the chunks' concatenation). Replaces the per-write _consume loop's
+ * input side (decode.js:144-169: each written chunk is parsed in place). */
+typedef struct drp_chunk {
+  const uint8_t *bytes;
+  uint64_t n;
+} drp_chunk;
+int drp_decode_stage_v(drp_ctx *ctx, const drp_chunk *chunks, uint64_t nchunks, drp_carry *carry,
+                       uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail);
 
 /* ---- encode -------------------------------------------------------------- */
 /* Wire size of encoding rows [0,n) as change frames (varint(len+1) 0x01 payload). */

@@ -10,6 +10,8 @@
 //   node ref_run.js encode <ops.json>   -> JSON {wire: hex, changes, blobs, bytes, drains}
 //        ops: [{op:'change', key, change, from, to, value(hex)?, subset?} |
 //              {op:'blob', len, writes:[hex,...]} | {op:'finalize'}]
+//   node ref_run.js acks <wire file> <write sizes> <burst|paced>
+//        -> the callback order of tests/js/ack_driver.js (write acknowledgements vs async handlers)
 //   node ref_run.js bench <wire file> <chunk> <seconds>   (DRP_REF_CODEC=full)
 //        -> JSON {frames_per_s, bytes_per_s, frames, reps}
 'use strict'
@@ -128,6 +130,9 @@ if (cmd === 'decode') {
 } else if (cmd === 'encode') {
   var ops = JSON.parse(fs.readFileSync(process.argv[3], 'utf8'))
   encodeOps(ops, function (r) { process.stdout.write(JSON.stringify(r) + '\n') })
+} else if (cmd === 'acks') { // node ref_run.js acks <wire file> <write sizes> <burst|paced>
+  require(path.join(__dirname, '..', '..', 'tests', 'js', 'ack_driver.js'))(protocol, fs.readFileSync(process.argv[3]),
+    process.argv[4].split(',').map(Number), process.argv[5], function (log) { process.stdout.write(JSON.stringify(log) + '\n') })
 } else if (cmd === 'bench') {
   bench(fs.readFileSync(process.argv[3]), Number(process.argv[4]), Number(process.argv[5]))
 } else {

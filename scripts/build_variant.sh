@@ -6,8 +6,8 @@ NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/exp/$NAME
 mkdir -p $OUT/build
-SRCS="drp_decode drp_decode_spec drp_encode drp_keys drp_comm drp_api"
-FLAGS="-O3 -std=c++17 -fPIC -fno-strict-aliasing --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value $*"
+SRCS="drp_decode drp_decode_spec drp_walk drp_encode drp_keys drp_comm drp_api"
+FLAGS="-O3 -std=c++17 -fPIC -fvisibility=hidden -fno-strict-aliasing --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value $*"
 pids=""
 for s in $SRCS; do
   /opt/rocm/bin/hipcc $FLAGS -c $ROOT/dat-replication-protocol_amd/csrc/$s.hip -o $OUT/build/$s.o &

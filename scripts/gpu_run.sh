@@ -13,7 +13,7 @@
 #   ab:<variant>   quick C2 + C5 lines with exp/<variant>/libdrp.so (scripts/build_variant.sh)
 #   probe:<script> python3 scripts/<script> (a measurement script)
 #   env:K=V        export K=V for the steps that follow (unenv:K unsets it)
-#   c2             the C2 line alone (no sub-lines, no CPU legs)
+#   c2 / c4 / c5   that workload's line alone (no sub-lines, no CPU legs), appended to <step>.log
 set -e
 export TMPDIR=/tmp
 TAG=$1
@@ -75,9 +75,9 @@ for step in "$@"; do
     unenv:*)
       unset "${step#unenv:}"
       ;;
-    c2)
-      timeout -k 10 300 python -u bench.py --no-cpu --no-sub --steps 10 --warmup 2 >> $OUT/c2.log 2>&1
-      echo "c2 (${DRP_CLAIMS:-auto}): $(tail -1 $OUT/c2.log | cut -c1-400)"
+    c2 | c5 | c4)
+      timeout -k 10 300 python -u bench.py --workload $step --no-cpu --no-sub --steps 10 --warmup 2 >> $OUT/$step.log 2>&1
+      echo "$step (${DRP_CLAIMS:-auto} ${DRP_LIB:-}): $(tail -1 $OUT/$step.log | cut -c1-400)"
       ;;
     *)
       echo "unknown step $step"

@@ -17,11 +17,11 @@ import drp_amd  # noqa: E402
 import numpy as np  # noqa: E402
 
 
-def wire_for(kind, n):
+def wire_for(kind, n, seed=1):
     if kind == "c2":
-        return S.c2_stream(n).tobytes()
+        return S.c2_stream(n, seed=seed).tobytes()
     if kind == "c5":
-        return S.c5_stream(random.Random(5), n)
+        return S.c5_stream(random.Random(seed), n)
     if kind == "random":
         return S.random_stream(random.Random(9), n)
     raise SystemExit(kind)
@@ -57,7 +57,7 @@ def run(mode, wire, stats):
 def main():
     kind = sys.argv[1] if len(sys.argv) > 1 else "c2"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
-    wire = wire_for(kind, n)
+    wire = wire_for(kind, n, int(sys.argv[3]) if len(sys.argv) > 3 else 1)
     print(f"{kind}: {n} frames, {len(wire)} bytes", flush=True)
     a = run("walk", wire, True)
     b = run("fast", wire, False)

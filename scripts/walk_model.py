@@ -60,23 +60,40 @@ def shape(w, po, pl):
     return off == pl and last >= 5
 
 
+def shaped(w, c, se):
+    if c >= se:
+        return False
+    k, L, i = hdr(w, c)
+    if k == 0 or i != 1 or L <= 1 or L - 1 > se - c - k - 1:
+        return False
+    if not shape(w, c + k + 1, L - 1):
+        return False
+    n = c + k + L
+    if n >= se:
+        return True
+    k2, L2, i2 = hdr(w, n)
+    return k2 != 0 and i2 <= 2 and (i2 == 0 or L2 != 0)
+
+
 def survives(w, c, se):
-    p = c
+    """(survives, near: every frame of the chain within the two ring windows)"""
+    p, near = c, True
     for f in range(K):
         if p >= se:
-            return p == se and f >= 2
+            return p == se and f >= 2, near
         k, L, i = hdr(w, p)
         if k == 0 or i > 2 or (i and L == 0):
-            return False
+            return False, near
         if i == 0:
             p += k + 1
             continue
         if L > se - p - k:
-            return f >= 2
+            return f >= 2 and se - p <= 16384, near  # (SY_TAIL)
+        near = near and k + L <= 2 * WB
         if i == 1 and L > 1 and w[p + k + 1] not in (0x0A, 0x12, 0x18, 0x20, 0x28, 0x32):
-            return False
+            return False, near
         p += k + L
-    return True
+    return True, near
 
 
 def live(w, p):
@@ -95,25 +112,24 @@ def sync_tile(w, A, se, verbose=True):
         for o in range(0, WB + 112):
             c = W0 + o
             if far and c >= far[1]:
+                if far[1] - far[0] <= 2 * WB and shaped(w, far[1], se):
+                    return ("far-successor", far[1])
                 break
             if not live(w, c):
                 continue
             k, L, i = hdr(w, c)
             if k == 0 or i > 2 or (i and L == 0):
                 continue
-            sh = False
-            if i == 1 and L > 1 and L - 1 <= se - c - k - 1:
-                sh = shape(w, c + k + 1, L - 1)
-                n = c + k + L
-                if sh and n < se:
-                    k2, L2, i2 = hdr(w, n)
-                    sh = k2 != 0 and i2 <= 2 and (i2 == 0 or L2 != 0)
-            sv = False if sh else survives(w, c, se)
+            sh = shaped(w, c, se)
+            sv, near = (False, False) if sh else survives(w, c, se)
             if verbose and (sh or sv):
                 print(f"  q={q} o={o} c={c:#x} k={k} L={L} id={i} shape={sh} survives={sv}")
             if not sh and not sv:
                 continue
-            if sh or i == 0 or k + L <= 2 * WB:
+            if sh or near:
+                n1 = c + k + (L if i else 1)
+                if not sh and n1 < W0 + WB + 112 and shaped(w, n1, se):
+                    return ("taken-next", n1)
                 return ("taken", c)
             if not far and o < WB:
                 far = (c, c + k + L)

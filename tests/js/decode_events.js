@@ -69,7 +69,7 @@ d.on('finish', function () {
   out.push({ t: 'finish', changes: d.changes, blobs: d.blobs, bytes: d.bytes })
   if (mode === 'h2d') {
     out.push({ t: 'timing', h2dBytes: d.timing.h2dBytes, h2dSkipped: d.timing.h2dSkipped,
-      blobPieces: pieces, blobPiecesShared: shared })
+      hostCopied: d.timing.hostCopied, blobPieces: pieces, blobPiecesShared: shared })
   }
   done()
 })

@@ -178,12 +178,12 @@ exports.install = function (pkgDir) {
       deviceContext: function () { return {} },
       deviceCount: function () { return 0 },
       nextDevice: function () { return 0 },
-      decode: function (ctx, batch, brem, cb) {
-        var r = decodeBatch(batch, brem)
+      decode: function (ctx, batch, brem, cb) { // (batch: a Buffer, or the written chunks end to end)
+        var r = decodeBatch(Array.isArray(batch) ? Buffer.concat(batch) : batch, brem)
         setImmediate(function () { cb(null, r) })
       },
       decodeSync: function (ctx, batch, brem) { return decodeBatch(batch, brem) },
-      abiVersion: 3
+      abiVersion: 5
     }
   }
 }

@@ -23,10 +23,14 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+# the walkers under test: "walk" (ring walkers) or "hop" (hop walkers); DRP_TEST_WALKERS picks
+WALKERS = os.environ.get("DRP_TEST_WALKERS", "walk")
+
+
 def walk_ctx(**env):
     from _gpu import drp_amd
     keep = {k: os.environ.get(k) for k in ["DRP_CLAIMS", "DRP_WALK_MIN", *env]}
-    os.environ.update({"DRP_CLAIMS": "walk", "DRP_WALK_MIN": "0", **env})
+    os.environ.update({"DRP_CLAIMS": WALKERS, "DRP_WALK_MIN": "0", **env})
     try:
         return drp_amd.Ctx(0)
     finally:
