@@ -31,6 +31,9 @@ import drp_amd  # noqa: E402
 import drp_dist  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# the speculative decode's kernels (drp_decode_spec.hip, drp_walk.hip) for batches of >= 32768 tiles
+DECODE_PATH = ("speculative decode: walk_regions + walk_sync + region walkers (ring or hop, chosen on the device) "
+               "+ spec_claims + verify_lite + tile scans + emit")
 FRAME = 86
 
 
@@ -429,15 +432,39 @@ def run_c5(args, dev, rank=0, world=1, steps=None, warmup=None, cpu=True):
     if dist:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    t = ctx.timing()
     if dist:
         cdev = dev if args.backend == "nccl" else torch.device("cpu")
         tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(tt.item())
+    # the same context right after a dense C2 batch: the claims form is chosen per launch on the
+    # device (walk_sync's density sample), not from the context's previous decode
+    after_c2 = None
+    if rank == 0:
+        nf2 = 10_000_000
+        w2 = c2_on_device(nf2, seed=99, dev=dev)
+        so2 = torch.tensor([0, w2.numel()], dtype=torch.int64, device=dev)
+        o2 = alloc_outputs(nf2 + 64, dev)
+        r2 = torch.zeros(C.sizeof(drp_amd.StreamResult), dtype=torch.uint8, device=dev)
+        ms = []
+        with torch.cuda.stream(ext):
+            for _ in range(3):
+                ctx.decode_device(w2, so2, None, o2, nf2 + 64, r2)
+                evs[1].record(ext)
+                ctx.decode_device(wire, stream_off, None, outs, cap, res)
+                evs[2].record(ext)
+                torch.cuda.synchronize(dev)
+                ms.append(evs[1].elapsed_time(evs[2]))
+        t2 = ctx.timing()
+        verify_c5(cols, heap, wire, outs, res, n, dev)
+        after_c2 = {"ms": float(np.median(ms)), "exact_fallbacks": t2.strict_reruns, "repair_passes": t2.spec_repairs,
+                    "segmented_repairs": t2.seg_repairs, "note": "C5 decode right after a 10M-frame C2 decode on the "
+                    "same context (median of 3)"}
+        del w2, o2, r2
     H = int(heap.numel())
     e, d = float(np.mean(enc_ms)) / 1e3, float(np.mean(dec_ms)) / 1e3
     b_enc, b_dec = 49 * n + H + W, W + 13 * n + 49 * n
-    t = ctx.timing()
     gather = ("drp_index_allgather (RCCL) of the 32 B stream stats + index scan" if args.backend == "nccl" else
               "gloo all-gather of the 32 B stream stats + index scan") if dist else "no collective (1 GPU)"
     out_line = {
@@ -458,7 +485,7 @@ def run_c5(args, dev, rank=0, world=1, steps=None, warmup=None, cpu=True):
         "encode": {"ms": e * 1e3, "GBps": b_enc / e / 1e9, "frac": b_enc / e / 1e9 / HBM_PEAK_GBPS},
         "decode": {"ms": d * 1e3, "GBps": b_dec / d / 1e9, "frac": b_dec / d / 1e9 / HBM_PEAK_GBPS,
                    "exact_fallbacks": t.strict_reruns, "repair_passes": t.spec_repairs,
-                   "segmented_repairs": t.seg_repairs},
+                   "segmented_repairs": t.seg_repairs, "after_c2": after_c2},
     }
     if rank == 0 and world == 1 and cpu and not args.no_cpu:
         out_line["cpu_baseline"] = cpu_baseline_c5()
@@ -466,6 +493,114 @@ def run_c5(args, dev, rank=0, world=1, steps=None, warmup=None, cpu=True):
     del cols, heap, out, outs, foff
     torch.cuda.empty_cache()
     return out_line if rank == 0 else None
+
+
+def c2_host(nframes, start, seed):
+    """C2 frames in host memory (the layout of c2_on_device)."""
+    i = np.arange(start, start + nframes, dtype=np.int64)
+    a = np.zeros((nframes, FRAME), np.uint8)
+    a[:, 0], a[:, 1], a[:, 2], a[:, 3] = 85, 1, 0x12, 10
+    for k in range(10):
+        a[:, 4 + k] = 48 + (i // 10 ** (9 - k)) % 10
+    a[:, 14], a[:, 15], a[:, 16], a[:, 17] = 0x18, (i % 100) + 1, 0x20, i % 128
+    a[:, 18], a[:, 19], a[:, 20], a[:, 21] = 0x28, (i + 1) % 128, 0x32, 64
+    a[:, 22:] = np.random.default_rng(seed).integers(0, 256, size=(nframes, 64), dtype=np.uint8)
+    return a.reshape(-1)
+
+
+C3_UNIT_FRAMES, C3_BLOB = 1000, 1 << 20
+
+
+def c3_host(units, seed=3):
+    """C3 (BASELINE configs[2]): units of [1000 C2 frames + one 1 MiB blob], so C2
+    frames straddle the blobs' 64 KiB chunk edges; returns the wire as a numpy array."""
+    hdr = bytes([(C3_BLOB + 1) & 0x7F | 0x80, ((C3_BLOB + 1) >> 7) & 0x7F | 0x80, (C3_BLOB + 1) >> 14, 2])
+    unit = C3_UNIT_FRAMES * FRAME + len(hdr) + C3_BLOB
+    out = np.empty(units * unit, np.uint8)
+    rng = np.random.default_rng(seed)
+    for u in range(units):
+        o = u * unit
+        out[o:o + C3_UNIT_FRAMES * FRAME] = c2_host(C3_UNIT_FRAMES, u * C3_UNIT_FRAMES, seed + u)
+        b = o + C3_UNIT_FRAMES * FRAME
+        out[b:b + len(hdr)] = np.frombuffer(hdr, np.uint8)
+        out[b + len(hdr):o + unit] = rng.integers(0, 256, size=C3_BLOB, dtype=np.uint8)
+    return out
+
+
+def cpu_baseline_c3(units=16, min_seconds=10.0):
+    """The C restatement of decode.js (oracle/, 1 thread) over a C3 sample in 64 KiB writes."""
+    O, _ = _oracle_modules()
+    wire = c3_host(units, seed=5).tobytes()
+    nf = units * (C3_UNIT_FRAMES + 1)
+    outs = O.alloc_outputs(nf + 16)
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < min_seconds:
+        r = O.decode_batch(wire, chunk=65536, outs=outs)
+        assert r["nframes"] == nf
+        reps += 1
+    dt = time.perf_counter() - t0
+    return {"value": reps * nf / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+            "wire_GBps": reps * len(wire) / dt / 1e9,
+            "sample": f"C3 sample of {units} units ({len(wire)} B) decoded {reps}x in 64 KiB writes by "
+                      f"oracle/drp_oracle.c, {dt:.1f} s on 1 host core"}
+
+
+def run_c3(args, dev, steps, warmup, cpu):
+    """C3 through the host-batch path: a ~1 GiB C3 stream in pinned host memory decoded by
+    drp_decode_batch (what the Node addon runs per batch) with blob skipping: only the pieces
+    around the blobs' headers are staged into HBM, the blob payloads stay in host memory as
+    pass-through ranges (decode.js:179-202 only slices them). One step = one decode of the whole
+    stream, host columns out. Reports the staged bytes and the H2D time apart; the roofline prices
+    the device kernels over the staged bytes."""
+    units = args.c3_units
+    host = c3_host(units)
+    pinned = torch.empty(host.size, dtype=torch.uint8, pin_memory=True)
+    pinned.numpy()[:] = host
+    wire = pinned.numpy()
+    del host
+    nf = units * (C3_UNIT_FRAMES + 1)
+    nc = units * C3_UNIT_FRAMES
+    outs = drp_amd.alloc_host_outputs(nf + 64)
+    ctx = drp_amd.Ctx(dev.index)
+    for _ in range(max(1, warmup)):  # (the first batch learns that the stream is blob-heavy)
+        r = ctx.decode_batch(wire, outs=outs)
+    assert (r["nframes"], r["err_code"], r["consumed"]) == (nf, 0, wire.size), (r["nframes"], r["err_code"])
+    ty = r["type"]
+    assert int((ty == 1).sum()) == nc and int((ty == 2).sum()) == units
+    assert np.array_equal(r["payload_len"][ty == 2], np.full(units, C3_BLOB, np.uint32))
+    t_step, t_dec, t_h2d, t_d2h, staged, skipped = [], [], [], [], 0, 0
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        ctx.decode_batch(wire, outs=outs)
+        t_step.append(time.perf_counter() - t0)
+        t = ctx.timing()
+        t_dec.append(t.total_ms)
+        t_h2d.append(t.h2d_ms)
+        t_d2h.append(t.d2h_ms)
+        staged, skipped = int(t.h2d_bytes), int(t.h2d_skipped)
+    ctx.close()
+    step_s = float(np.mean(t_step))
+    dec_s = float(np.mean(t_dec)) / 1e3
+    b_dev = staged + 13 * nf + 49 * nc
+    line = {
+        "value": nf / step_s, "unit": "frames/s", "steps": steps, "warmup": warmup, "ms_per_step": step_s * 1e3,
+        "data": "synthetic: C3 generator (seeded), in pinned host memory (the Node path's input side)",
+        "config": {"workload": f"C3: {units} units of [1000 C2 frames + one 1 MiB blob], one "
+                               f"{wire.size / 2**30:.2f} GiB host stream, drp_decode_batch with blob skipping",
+                   "wire_bytes": int(wire.size), "frames": nf},
+        "wire_GBps": wire.size / step_s / 1e9,
+        "h2d": {"staged_bytes": staged, "staged_frac": staged / wire.size, "skipped_bytes": skipped,
+                "ms": float(np.mean(t_h2d))},
+        "d2h_ms": float(np.mean(t_d2h)),
+        "roofline": {"bound": "hbm", "achieved": b_dev / dec_s / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": b_dev / dec_s / 1e9 / HBM_PEAK_GBPS, "traffic": None,
+                     "kernel": "the staged pieces' device decode (claims + verify + emit), summed", "kernel_ms": dec_s * 1e3,
+                     "bytes_model": "staged + 13*frames + 49*changes"},
+    }
+    if cpu:
+        line["cpu_baseline"] = cpu_baseline_c3()
+    del pinned, wire, outs
+    return line
 
 
 def run_decode(args, dev, rank, world, workload, steps, warmup):
@@ -554,8 +689,7 @@ def run_decode(args, dev, rank, world, workload, steps, warmup):
     achieved = b_dec / dec_avg_s / 1e9
     tile = args.tile or 8192
     exact = os.environ.get("DRP_DECODE") == "exact"
-    kname = (f"decode_tiles<{tile // 64}>" if exact else
-             "speculative decode: claims_fast + verify_lite + tile scans + emit_tiles")
+    kname = f"decode_tiles<{tile // 64}>" if exact else DECODE_PATH
     gather = ("; drp_index_allgather (RCCL) of 32 B stream stats + index scan" if args.backend == "nccl" else
               "; gloo all-gather of 32 B stream stats + index scan") if dist else "; no collective (1 GPU)"
     if workload == "c2":
@@ -602,11 +736,12 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--frames", type=int, default=100_000_000, help="C2 frames per GPU")
-    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2")
     ap.add_argument("--c5-changes", type=int, default=1_000_000, help="C5 Changes per step")
     ap.add_argument("--streams", type=int, default=8192, help="C4 streams across all GPUs")
     ap.add_argument("--sub-steps", type=int, default=5, help="timed steps of the c4/c5 sub-lines")
-    ap.add_argument("--no-sub", action="store_true", help="C2 only: no c4/c5 sub-lines")
+    ap.add_argument("--no-sub", action="store_true", help="C2 only: no c3/c4/c5 sub-lines")
+    ap.add_argument("--c3-units", type=int, default=947, help="C3 units (1000 C2 frames + 1 MiB blob) per step")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse "
@@ -645,6 +780,8 @@ def main():
 
     if args.workload == "c5":
         out = run_c5(args, dev, rank, world)
+    elif args.workload == "c3":
+        out = run_c3(args, dev, args.steps, args.warmup, cpu)
     else:
         out = run_decode(args, dev, rank, world, args.workload, args.steps, args.warmup)
         if cpu:
@@ -658,13 +795,14 @@ def main():
             # CPU baseline); the top-level value stays C2's
             c4 = run_decode(args, dev, rank, world, "c4", args.sub_steps, args.warmup)
             c5 = run_c5(args, dev, rank, world, steps=args.sub_steps, warmup=args.warmup, cpu=cpu)
+            c3 = run_c3(args, dev, args.sub_steps, args.warmup, cpu)  # (per rank, no collective)
             if rank == 0:
                 if cpu:
                     c4["cpu_baseline"] = out["cpu_baseline_all_cores"]
                 for k in ("metric", "higher_is_better", "scaling", "vs_baseline", "dtype", "n_gpus"):
                     c4.pop(k, None)
                     c5.pop(k, None)
-                out["c4"], out["c5"] = c4, c5
+                out["c4"], out["c5"], out["c3"] = c4, c5, c3
         if cpu:
             out["h2d"] = h2d_rate(dev)
             if args.workload == "c2":
@@ -677,19 +815,38 @@ def main():
 
 
 TRAFFIC_SOURCE = ("not measured in this run: profiles/pmc_%s.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per "
-                  "frame over the path's kernels, separate --pmc passes of scripts/gpu_pmc.sh) x this launch's frames")
+                  "frame over the path's kernels, separate --pmc passes of scripts/gpu_pmc.sh) x this launch's "
+                  "frames; null when that summary was measured on other kernel sources (code_hash)")
+
+
+DECODE_SOURCES = ["drp_api.hip", "drp_decode_spec.hip", "drp_walk.hip", "drp_spec.h", "drp_device.h", "drp_kernels.h",
+                  "drp_encode.hip", "drp_keys.hip"]
+
+
+def decode_code_hash():
+    """Hash of the kernel sources of the measured path: a PMC summary is used only for the code
+    it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in DECODE_SOURCES:
+        with open(os.path.join(ROOT, "dat-replication-protocol_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def traffic_from_profile(workload, nframes):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload's decode
     path (profiles/pmc_<workload>.json: FETCH_SIZE x2 + WRITE_SIZE per frame summed over the
     path's kernels, guide §HBM), times this launch's frames; None when no such summary exists
-    (a per-frame figure of one workload is never applied to another)."""
+    (a per-frame figure of one workload is never applied to another) or when it was measured on
+    other kernel sources (its code_hash differs from decode_code_hash())."""
     p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     try:
         with open(p) as f:
             d = json.load(f)
     except (OSError, ValueError):
+        return None
+    if d.get("code_hash") != decode_code_hash():
         return None
     return d["hbm_bytes_per_frame"] * nframes if d.get("hbm_bytes_per_frame") else None
 

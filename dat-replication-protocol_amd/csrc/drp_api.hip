@@ -348,7 +348,7 @@ int drp_set_blob_skip(drp_ctx *c, int mode) {
 // scratch layout for a decode of `nbytes` over `ns` streams
 struct DecLayout {
   uint64_t ntiles_max;
-  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, tstream, ent, tk, tsp, fmiss, segw, scan_tmp, walk, went, trec, trok, total;
+  size_t tile_prefix, rec, sgrp, tiles, perr, scount, ctrl, tstream, ent, tk, tsp, fmiss, segw, scan_tmp, walk, went, wdense, trec, trok, total;
   uint64_t nsg;
 };
 static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
@@ -374,6 +374,7 @@ static DecLayout dec_layout(uint32_t B, uint64_t nbytes, uint64_t ns) {
   L.scan_tmp = o; o += al((L.ntiles_max / 4096 + 2) * 8);  // tile scans: block sums
   L.walk = o; o += al((ns + 2) * 8);                         // region walkers: per-stream region prefix
   L.went = o; o += al((L.ntiles_max + ns + 2) * 8);          // region walkers: entries
+  L.wdense = o; o += 64;                                     // region walkers: density sample
   L.trec = o; o += al(L.ntiles_max * 4);                     // first record per tile (region walkers)
   L.trok = o; o += al(L.ntiles_max);                         // record emission marks (verify_lite)
   L.total = o;
@@ -648,7 +649,8 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   if (c->claims_mode == 1 || c->claims_mode == 3 || (c->claims_mode == 0 && NT >= c->walk_min)) {
     P.walk_rp = c->scratch.at<uint64_t>(L.walk);
     P.walk_entry = c->scratch.at<uint64_t>(L.went);
-    P.walk_hop = c->claims_mode == 3 ? 1u : 0u;
+    P.walk_dense = c->scratch.at<unsigned long long>(L.wdense);
+    P.walk_hop = c->claims_mode == 3 ? 1u : c->claims_mode == 1 ? 0u : 2u;  // 2: by the density sample
     P.walk_tpr = drp_walk_tiles_per_region(NT, (int)P.walk_hop);
     // per-frame records: the record emission instead of reading the wire again (DRP_WALK_REC=0:
     // off; a record buffer that cannot be had: off)
@@ -676,6 +678,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     add(P.dstamp, NT * 4, 0);
     add(P.first_miss, ns * 8, 0xFF);
     if (P.tile_rec) add(P.tile_rec, NT * 4, 0xFF);
+    if (P.walk_dense) add(P.walk_dense, 16, 0);
     if (dstats) add(dstats, 64 * 8, 0);
     CHK(drp_launch_prologue(B, stream_off, ns, tile_prefix, &cs, st));
   }
@@ -788,6 +791,11 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
       if (const int rt = launch_tail()) return rt;
   }
   const bool retry = (h[1] & drp_spec_retry_mask()) != 0;
+  if (retry && pass) {  // (the timings then cover the repair passes too, not just the first tail)
+    CHK(hipEventRecord(c->ev[2], st));
+    CHK(hipEventRecord(c->ev[3], st));
+    CHK(hipStreamSynchronize(st));
+  }
   if (!retry && c->change_checks_env < 0)  // (h[3]: the call's frames, from stream_counts)
     c->change_checks = h[3] == 0 || nbytes / h[3] >= 512 ? 1 : 0;
   if (retry) h[1] |= miss;

@@ -77,7 +77,8 @@ struct DecodeParams {
   // region walkers (drp_walk.hip): per-stream region prefix [nstreams + 1], tiles per region
   uint64_t *walk_rp;
   uint64_t *walk_entry;  // region walkers: each region's entry (walk_sync)
-  uint32_t walk_hop;      // 1: the hop walkers (claims_hop), 0: the ring walkers (claims_walk)
+  uint32_t walk_hop;      // 1: the hop walkers (claims_hop), 0: the ring walkers (claims_walk), 2: by walk_dense
+  unsigned long long *walk_dense;  // walk_sync's density sample: bytes, frames after the entries
   uint32_t walk_tpr;
   // per-frame records (null: none): rec_cap 32-byte slots per region; per tile its first record
   // (REC_NONE: none, the tile takes the wire-reading emission) and whether verification lets the

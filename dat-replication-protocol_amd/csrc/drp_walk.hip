@@ -39,6 +39,7 @@ constexpr uint32_t WK_LPR = WK_WB / 16;          // lanes of one DMA instruction
 constexpr uint32_t SY_WB = 128;                  // the syncs' scan window
 constexpr uint32_t SY_NEAR = 256;                // a "near" sync chain's longest frame
 constexpr uint64_t SY_TAIL = 16384;              // a sync chain's tail counts this close to the stream end
+constexpr uint64_t SY_MERGE = 1024;              // a region's entry before its first shaped Change: this close
 #ifndef DRP_WK_SLOTS
 #define DRP_WK_SLOTS 4
 #define DRP_WK_AHEAD 3
@@ -445,6 +446,15 @@ __device__ __forceinline__ Region region_of(const DecodeParams &P, uint64_t r) {
   return G;
 }
 
+// The walkers' form for this batch: the ring walkers for dense streams (frames of <= 512 bytes
+// on average after the regions' entries), the hop walkers for sparse ones (every frame costs
+// one read of its header, so long frames cost nothing extra).
+constexpr uint32_t HOP_FRAME = 512;
+__device__ __forceinline__ bool walk_hops(const DecodeParams &P) {
+  if (P.walk_hop != 2u) return P.walk_hop == 1u;
+  return P.walk_dense[0] > (unsigned long long)HOP_FRAME * P.walk_dense[1];
+}
+
 // ---- region syncs ----------------------------------------------------------------------------
 // One lane per region: the entry its walker starts from (P.walk_entry[r]; NONE: no chain found in
 // the region, whose tiles then claim identity). A stream's first tile has its exact entry. Else,
@@ -512,55 +522,140 @@ __device__ __forceinline__ uint64_t sync_general(const GReader &R, uint64_t A0, 
   return found;
 }
 
+// live positions of 64 bytes [p, p + 64) (4 masks of 16; the loads issued together)
+__device__ __forceinline__ uint64_t sync_live64(const GReader &R, uint64_t p) {
+  uint64_t x[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) x[i] = R.rd8(p + 8u * i);
+  uint64_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    m |= (uint64_t)wk_live16((uint32_t)x[2 * i], (uint32_t)(x[2 * i] >> 32), (uint32_t)x[2 * i + 1],
+                             (uint32_t)(x[2 * i + 1] >> 32), (uint32_t)x[2 * i + 2]) << (16 * i);
+  return m;
+}
+
+// Positions of 16 bytes (from 20: dwords a..e) that can start a Change header followed by the
+// schema's first tag: a length varint of 1..3 bytes, the id 1, then 0x0a (subset) or 0x12 (key).
+// Every shaped candidate is one; random bytes give one in ~2^15 positions, so the shape check's
+// reads are only made for these.
+__device__ __forceinline__ uint32_t wk_shape16(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e) {
+  auto zero8 = [](uint32_t y) { return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u; };  // (exact)
+  auto g4 = [](uint32_t x) { return ((x >> 7) & 1u) | ((x >> 14) & 2u) | ((x >> 21) & 4u) | ((x >> 28) & 8u); };
+  const uint32_t w[5] = {a, b, c, d, e};
+  uint32_t HI = 0, E1 = 0, T = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    HI |= g4(w[i] & 0x80808080u) << (4 * i);
+    E1 |= g4(zero8(w[i] ^ 0x01010101u)) << (4 * i);
+    T |= g4(zero8(w[i] ^ 0x0a0a0a0au) | zero8(w[i] ^ 0x12121212u)) << (4 * i);
+  }
+  const uint32_t LO = ~HI;
+  const uint32_t m1 = LO & (E1 >> 1) & (T >> 2);
+  const uint32_t m2 = HI & (LO >> 1) & (E1 >> 2) & (T >> 3);
+  const uint32_t m3 = HI & (HI >> 1) & (LO >> 2) & (E1 >> 3) & (T >> 4);
+  return (m1 | m2 | m3) & 0xFFFFu;
+}
+
+// shape-candidate positions of 128 bytes [p, p + 128) (the loads issued together)
+__device__ __forceinline__ uint64_t sync_shape128(const GReader &R, uint64_t p, uint64_t &hi) {
+  uint64_t x[17];
+#pragma unroll
+  for (int i = 0; i < 17; i++) x[i] = R.rd8(p + 8u * i);
+  uint64_t lo = 0;
+  hi = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t m = wk_shape16((uint32_t)x[2 * i], (uint32_t)(x[2 * i] >> 32), (uint32_t)x[2 * i + 1],
+                                  (uint32_t)(x[2 * i + 1] >> 32), (uint32_t)x[2 * i + 2]);
+    if (i < 4) lo |= m << (16 * i);
+    else hi |= m << (16 * (i - 4));
+  }
+  return lo;
+}
+
+// Does the chain from c reach exactly `to` (every frame complete before it, <= 16 frames)?
+__device__ __forceinline__ bool sync_merges(const GReader &R, uint64_t c, uint64_t to) {
+  uint64_t p = c;
+#pragma unroll 1
+  for (uint32_t f = 0; f < 16u && p < to; f++) {
+    const WHdr h = wk_hdr(R.rd8(p));
+    if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0)) return false;
+    p += h.k + (h.id ? h.L : 1u);
+  }
+  return p == to;
+}
+
 __global__ __launch_bounds__(256) void walk_sync(DecodeParams P) {
   const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (r >= P.walk_rp[P.nstreams]) return;
   const Region G = region_of(P, r);
-  if (G.exact) {
-    P.walk_entry[r] = G.entry;
-    return;
-  }
   const GReader R{P.bytes, P.nbytes};
   const uint64_t se = G.se, end = G.A0 + (uint64_t)(G.nw / WK_WPT) * TILE;
-  // the first shaped candidate
-  uint64_t shaped = ~0ull;
-#pragma unroll 1
-  for (uint64_t c16 = G.A0; c16 < end && shaped == ~0ull; c16 += 16u) {
-    uint32_t live = sync_live16(R, c16);
-#pragma unroll 1
-    while (live) {
-      const uint64_t c = c16 + (uint32_t)__builtin_ctz(live);
-      live &= live - 1u;
-      if (wk_shaped(R, c, se)) {
-        shaped = c;
-        break;
-      }
-    }
-  }
-  uint64_t found = shaped;
-  if (shaped != ~0ull) {
-    // a near chain before it
-#pragma unroll 1
-    for (uint64_t c16 = G.A0; c16 < shaped && found == shaped; c16 += 16u) {
-      uint32_t live = sync_live16(R, c16);
-#pragma unroll 1
-      while (live) {
-        const uint64_t c = c16 + (uint32_t)__builtin_ctz(live);
-        live &= live - 1u;
-        if (c >= shaped) break;
-        const WHdr h = wk_hdr(R.rd8(c));
-        if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0) || h.k + (h.id ? h.L : 1u) > SY_NEAR) continue;
-        bool near = false;
-        if (!wk_survives(R, c, se, near) || !near) continue;
-        const uint64_t n1 = c + h.k + (h.id ? h.L : 1u);
-        found = wk_shaped(R, n1, se) ? n1 : c;
-        break;
-      }
-    }
+  uint64_t found = ~0ull;
+  if (G.exact) {
+    found = G.entry;
   } else {
-    found = sync_general(R, G.A0, G.nw / WK_WPT * (TILE / SY_WB), se);
+    // the first shaped candidate
+    uint64_t shaped = ~0ull;
+#pragma unroll 1
+    for (uint64_t c128 = G.A0; c128 < end && shaped == ~0ull; c128 += 128u) {
+      uint64_t hi;
+      uint64_t m = sync_shape128(R, c128, hi);
+#pragma unroll 1
+      for (uint32_t half = 0; half < 2u && shaped == ~0ull; half++, m = hi) {
+#pragma unroll 1
+        while (m) {
+          const uint64_t c = c128 + 64u * half + (uint32_t)__builtin_ctzll(m);
+          m &= m - 1u;
+          if (wk_shaped(R, c, se)) {
+            shaped = c;
+            break;
+          }
+        }
+      }
+    }
+    found = shaped;
+    if (shaped != ~0ull) {
+      // an earlier candidate (up to SY_MERGE bytes before it) whose chain lands exactly on it:
+      // the region starts in other frames (blobs, short frames)
+      const uint64_t from = shaped - G.A0 > SY_MERGE ? (shaped - SY_MERGE) & ~63ull : G.A0;
+#pragma unroll 1
+      for (uint64_t c64 = from; c64 < shaped && found == shaped; c64 += 64u) {
+        uint64_t live = sync_live64(R, c64);
+#pragma unroll 1
+        while (live) {
+          const uint64_t c = c64 + (uint32_t)__builtin_ctzll(live);
+          live &= live - 1u;
+          if (c >= shaped) break;
+          const WHdr h = wk_hdr(R.rd8(c));
+          if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0) || c + h.k + (h.id ? h.L : 1u) > shaped) continue;
+          if (sync_merges(R, c, shaped)) {
+            found = c;
+            break;
+          }
+        }
+      }
+    } else {
+      found = sync_general(R, G.A0, G.nw / WK_WPT * (TILE / SY_WB), se);
+    }
   }
   P.walk_entry[r] = found;
+  // the batch's frame density, from two frames after each entry (the walkers' form: P.walk_dense)
+  if (found != ~0ull && found < se) {
+    uint64_t p = found;
+    uint32_t nf = 0;
+#pragma unroll 1
+    for (; nf < 2u; nf++) {
+      const WHdr h = wk_hdr(R.rd8(p));
+      if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0) || p + h.k + h.L >= se) break;
+      p += h.k + (h.id ? h.L : 1u);
+    }
+    if (nf) {
+      atomicAdd(&P.walk_dense[0], (unsigned long long)(p - found));
+      atomicAdd(&P.walk_dense[1], (unsigned long long)nf);
+    }
+  }
   if (P.stats && found != ~0ull) atomicAdd(&P.stats[31], 1ull);
 }
 
@@ -574,7 +669,7 @@ __global__ __launch_bounds__(WAVE) void claims_walk(DecodeParams P) {
   const uint32_t lane = threadIdx.x;
   const uint64_t nreg = P.walk_rp[P.nstreams];
   const uint64_t r = (uint64_t)blockIdx.x * WAVE + lane;
-  if ((uint64_t)blockIdx.x * WAVE >= nreg) return;  // (whole wave)
+  if ((uint64_t)blockIdx.x * WAVE >= nreg || walk_hops(P)) return;  // (whole wave)
   // ---- this lane's region ---------------------------------------------------------------------
   uint64_t t0 = 0, A0 = 0, se = 0, pos = ~0ull;
   uint64_t rbase = 0;  // this region's first record slot (P.rec_cap slots per region)
@@ -800,7 +895,7 @@ __global__ __launch_bounds__(WAVE) void claims_walk(DecodeParams P) {
 // time), the same death and tail rules.
 __global__ __launch_bounds__(256) void claims_hop(DecodeParams P) {
   const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (r >= P.walk_rp[P.nstreams]) return;
+  if (r >= P.walk_rp[P.nstreams] || !walk_hops(P)) return;
   const Region G = region_of(P, r);
   const uint64_t A0 = G.A0, se = G.se;
   const uint32_t ntr = G.nw / WK_WPT;       // tiles
@@ -962,17 +1057,15 @@ extern "C" hipError_t drp_launch_claims_walk(const DecodeParams *P, uint64_t nt_
   hipLaunchKernelGGL(spec::walk_regions, dim3(1), dim3(1024), 0, st, *P);
   const uint64_t maxr = nt_max / P->walk_tpr + P->nstreams + 1;
   hipLaunchKernelGGL(spec::walk_sync, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
-  if (P->walk_hop) {
-    hipLaunchKernelGGL(spec::claims_hop, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
-    return hipGetLastError();
-  }
+  if (P->walk_hop) hipLaunchKernelGGL(spec::claims_hop, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
+  if (P->walk_hop == 1) return hipGetLastError();
   if (P->rec) hipLaunchKernelGGL(spec::claims_walk<true>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
   else hipLaunchKernelGGL(spec::claims_walk<false>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
   return hipGetLastError();
 }
 
 extern "C" uint32_t drp_walk_tiles_per_region(uint64_t nt_max, int hop) {
-  const uint64_t nr = hop ? spec::HOP_REGIONS : spec::WK_REGIONS;
+  const uint64_t nr = hop == 1 ? spec::HOP_REGIONS : spec::WK_REGIONS;  // (2: either form, by density)
   const uint64_t t = (nt_max + nr - 1) / nr;
   return (uint32_t)(t ? t : 1);
 }

@@ -255,14 +255,17 @@ class Ctx:
         return t
 
     # ---- host-buffer batch decode (the N-API addon's path) -----------------------------
-    def decode_batch(self, wire, blob_remaining=0, cap=None, key_hash=False):
+    def decode_batch(self, wire, blob_remaining=0, cap=None, key_hash=False, outs=None):
         """drp_decode_batch into host columns; key_hash=True also asks for the key hash
-        column and the DRP_F_KEY_ASCII / DRP_F_KEY_UTF8 flags."""
+        column and the DRP_F_KEY_ASCII / DRP_F_KEY_UTF8 flags. outs: host columns to reuse
+        (alloc_host_outputs(cap))."""
         w = np.frombuffer(bytes(wire), np.uint8) if not isinstance(wire, np.ndarray) else wire
         n = int(w.size)
-        if cap is None:
+        if outs is not None:
+            cap = int(outs["payload_off"].size)
+        elif cap is None:
             cap = n // 2 + 2
-        o = alloc_host_outputs(cap, key_hash)
+        o = outs if outs is not None else alloc_host_outputs(cap, key_hash)
         fr, co = _structs(o, _p)
         carry = Carry(blob_remaining, 0, 0, 0, 0)
         nf, ef, ec, ed = U64(), U64(), U32(), U32()

