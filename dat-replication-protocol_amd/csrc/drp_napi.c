@@ -144,7 +144,7 @@ typedef struct colblock {
   env_state *st;
   void *p;
   size_t cap;
-  int refs; /* ArrayBuffers over it still alive */
+  int refs; /* (1 while a Buffer holds it) */
 } colblock;
 
 static colblock *col_get(env_state *st, size_t need) {
@@ -203,11 +203,10 @@ static void col_put(colblock *b) {
   env_unref(st);
 }
 
-/* finalizer of a column ArrayBuffer (JS thread) */
+/* finalizer of a batch's column Buffer (JS thread) */
 static void col_finalize(napi_env env, void *data, void *hint) {
   (void)data;
   colblock *b = (colblock *)hint;
-  if (--b->refs > 0) return;
   int64_t adj;
   if (!b->st->closing) napi_adjust_external_memory(env, -(int64_t)b->cap, &adj);
   col_put(b);
@@ -257,7 +256,9 @@ typedef struct {
   uint64_t nf, ef, rows;
   uint32_t ec, ed;
   drp_carry carry;
-  colblock *blk;  /* the pinned block the columns live in (NULL: malloc'd columns) */
+  colblock *blk;  /* the pinned block the columns live in (NULL: the malloc'd block `mem`) */
+  void *mem;
+  size_t bytes;   /* the columns' block: all columns at 64-byte aligned offsets */
   void *col[NCOL];
   int key_post;   /* also the key hash column (drp_set_key_post; the key flags are always on) */
   void *khash;
@@ -267,14 +268,10 @@ typedef struct {
 } dec_job;
 
 static void free_cols(dec_job *j) {
-  if (j->blk) {
-    colblock *b = j->blk;
-    j->blk = NULL;
-    if (b->refs == 0) col_put(b); /* (never handed to JS) */
-  } else {
-    for (int i = 0; i < NCOL; i++) free(j->col[i]);
-    free(j->khash);
-  }
+  if (j->blk) col_put(j->blk); /* (never handed to JS) */
+  free(j->mem);
+  j->blk = NULL;
+  j->mem = NULL;
   for (int i = 0; i < NCOL; i++) j->col[i] = NULL;
   j->khash = NULL;
 }
@@ -294,24 +291,20 @@ static double now_ms(void) {
 
 static size_t al64(size_t x) { return (x + 63) & ~(size_t)63; }
 
-/* host columns for j->rows rows: one pinned block (the fetch then runs by DMA), else malloc */
+/* host columns for j->rows rows in one block: pinned (the fetch then runs by DMA), else malloc */
 static int alloc_cols(dec_job *j) {
   size_t need = 0;
   for (int i = 0; i < NCOL; i++) need += al64(j->rows * COL_W[i] + 8);
   if (j->key_post) need += al64(j->rows * 8 + 8);
+  j->bytes = need;
   j->blk = j->st ? col_get(j->st, need) : NULL;
-  if (j->blk) {
-    char *p = (char *)j->blk->p;
-    for (int i = 0; i < NCOL; i++) {
-      j->col[i] = p;
-      p += al64(j->rows * COL_W[i] + 8);
-    }
-    if (j->key_post) j->khash = p;
-    return DRP_OK;
+  char *p = j->blk ? (char *)j->blk->p : (char *)(j->mem = malloc(need));
+  if (!p) return DRP_E_NOMEM;
+  for (int i = 0; i < NCOL; i++) {
+    j->col[i] = p;
+    p += al64(j->rows * COL_W[i] + 8);
   }
-  for (int i = 0; i < NCOL; i++)
-    if (!(j->col[i] = malloc(j->rows * COL_W[i] + 8))) return DRP_E_NOMEM;
-  if (j->key_post && !(j->khash = malloc(j->rows * 8 + 8))) return DRP_E_NOMEM;
+  if (j->key_post) j->khash = p;
   return DRP_OK;
 }
 
@@ -369,20 +362,6 @@ static void set_num(napi_env env, napi_value obj, const char *k, double v) {
   napi_set_named_property(env, obj, k, x);
 }
 
-/* one column as an external ArrayBuffer + typed array (JS thread): over the pinned block (its
-   last collected ArrayBuffer returns the block to the pool) or a malloc'd array */
-static int col_array(napi_env env, dec_job *j, void **slot, size_t bytes, napi_typedarray_type ty, napi_value *out) {
-  napi_value ab;
-  if (j->blk) {
-    if (napi_create_external_arraybuffer(env, *slot, bytes, col_finalize, j->blk, &ab) != napi_ok) return 0;
-    j->blk->refs++;
-  } else {
-    if (napi_create_external_arraybuffer(env, *slot, bytes, free_finalizer, NULL, &ab) != napi_ok) return 0;
-    *slot = NULL; /* owned by the ArrayBuffer now */
-  }
-  return napi_create_typedarray(env, ty, j->rows, ab, 0, out) == napi_ok;
-}
-
 /* build the JS result object; the columns move into external ArrayBuffers (JS thread) */
 static napi_value dec_result(napi_env env, dec_job *j) {
   napi_value res;
@@ -409,33 +388,43 @@ static napi_value dec_result(napi_env env, dec_job *j) {
     set_num(env, t, "pinnedColumns", j->blk ? 1 : 0);
     napi_set_named_property(env, res, "t", t);
   }
+  /* the columns' block as one external Buffer (one finalizer returns it: a pinned block to its
+     pool, a malloc'd one to the allocator) and each column a typed array over its ArrayBuffer */
+  napi_value buf, ab;
+  void *base = j->blk ? j->blk->p : j->mem;
+  napi_status stt;
   if (j->blk) {
-    int64_t adj;
-    napi_adjust_external_memory(env, (int64_t)j->blk->cap, &adj); /* (so V8 collects spent batches early) */
-    j->blk->refs++; /* (held while the arrays are made: a failure part way leaves it to free_cols) */
-  }
-  int ok = 1;
-  for (int i = 0; i < NCOL && ok; i++) {
-    napi_value ta;
-    ok = col_array(env, j, &j->col[i], j->rows * COL_W[i] + 8, COL_T[i], &ta);
-    if (ok) napi_set_named_property(env, res, COL_NAME[i], ta);
-  }
-  if (ok && j->khash) {
-    napi_value ta;
-    ok = col_array(env, j, &j->khash, j->rows * 8 + 8, napi_biguint64_array, &ta);
-    if (ok) napi_set_named_property(env, res, "keyHash", ta);
-  }
-  if (j->blk) {
-    colblock *b = j->blk;
-    j->blk = NULL; /* (the arrays own it now) */
-    for (int i = 0; i < NCOL; i++) j->col[i] = NULL;
-    j->khash = NULL;
-    if (--b->refs == 0) { /* (no array was made) */
-      b->refs = 1;
-      col_finalize(env, NULL, b);
+    stt = napi_create_external_buffer(env, j->bytes, base, col_finalize, j->blk, &buf);
+    if (stt == napi_ok) {
+      int64_t adj;
+      napi_adjust_external_memory(env, (int64_t)j->blk->cap, &adj); /* (so V8 collects spent batches early) */
+      j->blk->refs = 1;
+      j->blk = NULL; /* (the Buffer owns it now) */
     }
+  } else {
+    stt = napi_create_external_buffer(env, j->bytes, base, free_finalizer, NULL, &buf);
+    if (stt == napi_ok) j->mem = NULL;
   }
-  return ok ? res : NULL;
+  if (stt != napi_ok) return NULL;
+  size_t blen = 0, boff = 0;
+  void *bdata = NULL;
+  napi_typedarray_type bty;
+  if (napi_get_typedarray_info(env, buf, &bty, &blen, &bdata, &ab, &boff) != napi_ok) return NULL;
+  size_t off = boff;
+  for (int i = 0; i < NCOL; i++) {
+    napi_value ta;
+    if (napi_create_typedarray(env, COL_T[i], j->rows, ab, off, &ta) != napi_ok) return NULL;
+    napi_set_named_property(env, res, COL_NAME[i], ta);
+    off += al64(j->rows * COL_W[i] + 8);
+  }
+  if (j->khash) {
+    napi_value ta;
+    if (napi_create_typedarray(env, napi_biguint64_array, j->rows, ab, off, &ta) != napi_ok) return NULL;
+    napi_set_named_property(env, res, "keyHash", ta);
+  }
+  for (int i = 0; i < NCOL; i++) j->col[i] = NULL;
+  j->khash = NULL;
+  return res;
 }
 
 static void dec_execute(napi_env env, void *data) {

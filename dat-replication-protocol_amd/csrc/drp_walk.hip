@@ -36,10 +36,12 @@ constexpr uint32_t WK_WB = DRP_WK_WB;            // window bytes per region and 
 constexpr uint32_t WK_WPT = TILE / WK_WB;        // windows per tile
 constexpr uint32_t WK_GW = 512 / WK_WB;          // windows per group of 8 segment records
 constexpr uint32_t WK_LPR = WK_WB / 16;          // lanes of one DMA instruction per region
-constexpr uint32_t SY_WB = 128;                  // the syncs' scan window
 constexpr uint32_t SY_NEAR = 256;                // a "near" sync chain's longest frame
 constexpr uint64_t SY_TAIL = 16384;              // a sync chain's tail counts this close to the stream end
 constexpr uint64_t SY_MERGE = 1024;              // a region's entry before its first shaped Change: this close
+constexpr uint64_t SY_SHAPE = 8192;              // how far a region's first shaped Change is looked for
+constexpr uint64_t SY_GENERAL = 2048;            // how far the general scan looks (else: no entry, the
+                                                 // region's tiles claim identity and verification walks them)
 #ifndef DRP_WK_SLOTS
 #define DRP_WK_SLOTS 4
 #define DRP_WK_AHEAD 3
@@ -473,55 +475,6 @@ __device__ __forceinline__ uint32_t sync_live16(const Rd &R, uint64_t p) {
   return wk_live16((uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32), (uint32_t)R.rd8(p + 16));
 }
 
-// The general scan (a region without a shaped candidate): windows of 128 bytes in order,
-// candidates through each window and the next one's first 112 bytes. A candidate must survive
-// WK_K frames; it is taken at once when near, else ("far") held back while the scan goes on, up
-// to its successor or its tile's end, and dropped for a near candidate: a header whose length
-// varint swallows a real header's first bytes declares a frame of ~1 MB that lands on the real
-// chain with odds of one in the real frame size, and then "survives". At the held-back chain's
-// successor the scan stops; when the held-back frame is short and its successor is a shaped
-// Change, the chain is taken there.
-__device__ __forceinline__ uint64_t sync_general(const GReader &R, uint64_t A0, uint32_t nsw, uint64_t se) {
-  uint64_t found = ~0ull, far_c = 0, far_n = 0;
-#pragma unroll 1
-  for (uint32_t w = 0; w < nsw && found == ~0ull; w++) {
-    const uint64_t W0 = A0 + (uint64_t)w * SY_WB, W1 = W0 + SY_WB;
-    if (far_c && far_n < W1) return far_c;  // no near candidate up to the held-back chain's successor
-    bool stop = false;
-#pragma unroll 1
-    for (uint32_t c16 = 0; c16 < SY_WB + 112u && !stop; c16 += 16u) {
-      uint32_t live = sync_live16(R, W0 + c16);
-#pragma unroll 1
-      while (live) {
-        const uint32_t o = c16 + (uint32_t)__builtin_ctz(live);
-        live &= live - 1u;
-        const uint64_t c = W0 + o;
-        if (far_c && c >= far_n) {
-          if (far_n - far_c <= SY_NEAR && wk_shaped(R, far_n, se)) found = far_n;
-          stop = true;
-          break;
-        }
-        const WHdr h = wk_hdr(R.rd8(c));
-        if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0)) continue;
-        bool near = false;
-        if (!wk_survives(R, c, se, near)) continue;
-        if (near) {
-          const uint64_t n1 = c + h.k + (h.id ? h.L : 1u);
-          found = n1 < W0 + SY_WB + 112u && wk_shaped(R, n1, se) ? n1 : c;
-          stop = true;
-          break;
-        }
-        if (!far_c && o < SY_WB) {
-          far_c = c;
-          far_n = c + h.k + h.L;
-        }
-      }
-    }
-    if (found == ~0ull && w % (TILE / SY_WB) == TILE / SY_WB - 1 && far_c) found = far_c;  // (its frame leaves the tile)
-  }
-  return found;
-}
-
 // live positions of 64 bytes [p, p + 64) (4 masks of 16; the loads issued together)
 __device__ __forceinline__ uint64_t sync_live64(const GReader &R, uint64_t p) {
   uint64_t x[9];
@@ -533,6 +486,45 @@ __device__ __forceinline__ uint64_t sync_live64(const GReader &R, uint64_t p) {
     m |= (uint64_t)wk_live16((uint32_t)x[2 * i], (uint32_t)(x[2 * i] >> 32), (uint32_t)x[2 * i + 1],
                              (uint32_t)(x[2 * i + 1] >> 32), (uint32_t)x[2 * i + 2]) << (16 * i);
   return m;
+}
+
+// The general scan (a region without a shaped candidate near its start): candidates in order. A
+// candidate must survive WK_K frames; it is taken at once when near, else ("far") the first one
+// is held back while the scan goes on, up to its successor or its tile's end, and dropped for a
+// near candidate: a header whose length varint swallows a real header's first bytes declares a
+// frame of ~1 MB that lands on the real chain with odds of one in the real frame size, and then
+// "survives". At the held-back chain's successor the scan stops: when the held-back frame is
+// short and its successor is a shaped Change, the chain is taken there, else at the held-back
+// candidate.
+__device__ __forceinline__ uint64_t sync_general(const GReader &R, uint64_t A0, uint64_t end, uint64_t se) {
+  uint64_t far_c = 0, far_n = 0, far_t = 0;
+#pragma unroll 1
+  for (uint64_t c64 = A0; c64 < end; c64 += 64u) {
+    uint64_t live = sync_live64(R, c64);
+#pragma unroll 1
+    while (live) {
+      const uint64_t c = c64 + (uint32_t)__builtin_ctzll(live);
+      live &= live - 1u;
+      if (far_c && (c >= far_n || c >= far_t)) {
+        if (c >= far_n && far_n - far_c <= SY_NEAR && wk_shaped(R, far_n, se)) return far_n;
+        return far_c;
+      }
+      const WHdr h = wk_hdr(R.rd8(c));
+      if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0)) continue;
+      bool near = false;
+      if (!wk_survives(R, c, se, near)) continue;
+      if (near) {
+        const uint64_t n1 = c + h.k + (h.id ? h.L : 1u);
+        return n1 - c <= SY_NEAR && wk_shaped(R, n1, se) ? n1 : c;
+      }
+      if (!far_c) {
+        far_c = c;
+        far_n = c + h.k + h.L;
+        far_t = ((c - A0) / TILE + 1) * TILE + A0;  // (its tile's end)
+      }
+    }
+  }
+  return far_c ? far_c : ~0ull;
 }
 
 // Positions of 16 bytes (from 20: dwords a..e) that can start a Change header followed by the
@@ -596,10 +588,12 @@ __global__ __launch_bounds__(256) void walk_sync(DecodeParams P) {
   if (G.exact) {
     found = G.entry;
   } else {
-    // the first shaped candidate
+    // the first shaped candidate (within SY_SHAPE bytes: a stream without Changes goes on to the
+    // general scan soon)
     uint64_t shaped = ~0ull;
+    const uint64_t aend = umin64(end, G.A0 + SY_SHAPE);
 #pragma unroll 1
-    for (uint64_t c128 = G.A0; c128 < end && shaped == ~0ull; c128 += 128u) {
+    for (uint64_t c128 = G.A0; c128 < aend && shaped == ~0ull; c128 += 128u) {
       uint64_t hi;
       uint64_t m = sync_shape128(R, c128, hi);
 #pragma unroll 1
@@ -637,7 +631,7 @@ __global__ __launch_bounds__(256) void walk_sync(DecodeParams P) {
         }
       }
     } else {
-      found = sync_general(R, G.A0, G.nw / WK_WPT * (TILE / SY_WB), se);
+      found = sync_general(R, G.A0, umin64(end, G.A0 + SY_GENERAL), se);
     }
   }
   P.walk_entry[r] = found;
