@@ -1604,8 +1604,10 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   const TileGeo G = tile_geo(P, t);
   if (t >= ntiles) return;  // (whole workgroup)
+  // (a large batch's sparse streams take the hop walkers instead; walk_regions lists the edge tiles)
+  if (P.walk_rp && walk_hops(P)) return;
   if (G.A < G.so || G.A + IMG > G.se) {  // edge tile: the general kernel
-    push_work(P, t);
+    if (!P.walk_rp) push_work(P, t);
     return;
   }
   uint32_t eb, en, ecn;
@@ -3379,6 +3381,8 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
     const hipError_t e = drp_launch_claims_walk(&Q, nt_max, st);
     if (e != hipSuccess) return e;
     drp_dbg_mark("claims_walk", st);
+    if (Q.walk_hop == 2u)  // (dense streams: claims_fast; it exits at once when the batch is sparse)
+      hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
   } else if (Q.change_checks)
     hipLaunchKernelGGL(spec::claims_fast<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
   else

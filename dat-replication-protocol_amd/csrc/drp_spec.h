@@ -132,5 +132,16 @@ __device__ __forceinline__ Hdr hdr_global(const uint8_t *g, uint64_t p, uint64_t
   return parse_win(w0, w1, p, se);
 }
 
+
+// The claims form of a large batch, chosen on the device per launch from the region syncs'
+// density sample (drp_walk.hip walk_sync): streams averaging <= HOP_FRAME bytes per frame after
+// the regions' entries take claims_fast, sparser ones the hop walkers (claims_hop: one header read
+// per frame, so long frames cost nothing extra). P.walk_hop: 1 / 0 force the hop / ring walkers.
+constexpr uint32_t HOP_FRAME = 512;
+__device__ __forceinline__ bool walk_hops(const DecodeParams &P) {
+  if (P.walk_hop != 2u) return P.walk_hop == 1u;
+  return P.walk_dense[0] > (unsigned long long)HOP_FRAME * P.walk_dense[1];
+}
+
 }  // namespace spec
 }  // namespace drp

@@ -448,15 +448,6 @@ __device__ __forceinline__ Region region_of(const DecodeParams &P, uint64_t r) {
   return G;
 }
 
-// The walkers' form for this batch: the ring walkers for dense streams (frames of <= 512 bytes
-// on average after the regions' entries), the hop walkers for sparse ones (every frame costs
-// one read of its header, so long frames cost nothing extra).
-constexpr uint32_t HOP_FRAME = 512;
-__device__ __forceinline__ bool walk_hops(const DecodeParams &P) {
-  if (P.walk_hop != 2u) return P.walk_hop == 1u;
-  return P.walk_dense[0] > (unsigned long long)HOP_FRAME * P.walk_dense[1];
-}
-
 // ---- region syncs ----------------------------------------------------------------------------
 // One lane per region: the entry its walker starts from (P.walk_entry[r]; NONE: no chain found in
 // the region, whose tiles then claim identity). A stream's first tile has its exact entry. Else,
@@ -1052,7 +1043,7 @@ extern "C" hipError_t drp_launch_claims_walk(const DecodeParams *P, uint64_t nt_
   const uint64_t maxr = nt_max / P->walk_tpr + P->nstreams + 1;
   hipLaunchKernelGGL(spec::walk_sync, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
   if (P->walk_hop) hipLaunchKernelGGL(spec::claims_hop, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
-  if (P->walk_hop == 1) return hipGetLastError();
+  if (P->walk_hop) return hipGetLastError();  // (2: dense batches take claims_fast, launched by the caller)
   if (P->rec) hipLaunchKernelGGL(spec::claims_walk<true>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
   else hipLaunchKernelGGL(spec::claims_walk<false>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
   return hipGetLastError();

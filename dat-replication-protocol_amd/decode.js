@@ -30,7 +30,8 @@ var PIECE = Math.min(MAX_BATCH, Number(process.env.DRP_PIECE) || 16 * 1024 * 102
 var MAX_FRAME = require('buffer').constants.MAX_LENGTH
 
 // a batch whose frames average at most TEXT_PER_FRAME bytes has its ASCII keys cut from one
-// latin1 string per written chunk (cheaper than a string per key); larger frames keep one
+// latin1 string of the batch (cheaper than a string per key; one string per written chunk would
+// put 64 KiB strings in V8's young generation, whose scavenges copy them); larger frames keep one
 // string per key
 var TEXT_PER_FRAME = 512
 var TEXT_MAX = 256 * 1024 * 1024 // (below V8's string length limit)
@@ -259,7 +260,7 @@ Decoder.prototype._form = function () {
       i++
     }
     if (p.filled < p.buf.length) { // nothing to decode yet: these writes only fill the frame
-      this._queueBatch({ chunks: [], starts: [], size: 0, res: NOTHING, tooBig: 0, texts: null, first: first }, slots)
+      this._queueBatch({ chunks: [], starts: [], size: 0, res: NOTHING, tooBig: 0, text: null, first: first }, slots)
       return this._form()
     }
     this._partial = null
@@ -281,7 +282,7 @@ Decoder.prototype._form = function () {
     }
     if (g.write) slots.push({ chunk: g.chunk, end: at })
   }
-  var batch = { chunks: chunks, starts: starts, size: at, res: null, tooBig: 0, texts: null, first: first }
+  var batch = { chunks: chunks, starts: starts, size: at, res: null, tooBig: 0, text: null, first: first }
   this._queueBatch(batch, slots)
   this._inflight = batch
   var self = this
@@ -334,7 +335,7 @@ Decoder.prototype._ondecoded = function (err, res, batch) {
   }
   batch.res = res
   batch.tooBig = tooBig
-  batch.texts = res.asciiKeys && res.n * TEXT_PER_FRAME >= batch.size ? [] : null
+  batch.text = res.asciiKeys && res.n * TEXT_PER_FRAME >= batch.size && batch.size <= TEXT_MAX ? undefined : null
   this._form() // the next batch goes to the GPU before this one's callbacks run
   this._deliver()
 }
@@ -408,8 +409,8 @@ Decoder.prototype._retire = function () {
 // Deliver the batch's frames completed before batch offset `lim` (the end of the write being
 // consumed). false: stopped at a callback not yet acknowledged, or the stream ended.
 // Change frames are built inline (the hot loop: one object, one key string, one value slice per
-// frame); keys the GPU flagged ASCII are cut from one latin1 string of their written chunk (the
-// same string buf.toString('utf8', ...) would give, without a UTF-8 decode per key).
+// frame); keys the GPU flagged ASCII are cut from one latin1 string of the batch (the same string
+// buf.toString('utf8', ...) would give, without a UTF-8 decode per key).
 Decoder.prototype._replay = function (batch, lim) {
   var res = batch.res
   var n = res.n
@@ -429,7 +430,13 @@ Decoder.prototype._replay = function (batch, lim) {
   var keyHash = res.keyHash
   var chunks = batch.chunks
   var starts = batch.starts
-  var texts = batch.texts
+  var text = batch.text
+  if (text === undefined) { // (one latin1 string of the batch, its chunks joined: V8 copies it once)
+    var parts = new Array(chunks.length)
+    for (var q = 0; q < chunks.length; q++) parts[q] = chunks[q].toString('latin1')
+    text = batch.text = parts.join('')
+    this.timing.hostCopied += batch.size
+  }
   var down = this._down
   var i = this._next
   var k = this._ck
@@ -461,10 +468,8 @@ Decoder.prototype._replay = function (batch, lim) {
     var k1 = k0 + kl[i]
     var v0 = o + vcol[i] - base
     var key
-    if (texts !== null && inChunk && (f & KEY_ASCII)) {
-      var s = texts[k]
-      if (s === undefined) s = texts[k] = c.length <= TEXT_MAX ? c.toString('latin1') : null
-      key = s !== null ? s.substring(k0, k1) : c.toString('utf8', k0, k1)
+    if (text !== null && (f & KEY_ASCII)) {
+      key = text.substring(o + ko[i], o + ko[i] + kl[i])
     } else {
       key = c.toString('utf8', k0, k1)
     }
