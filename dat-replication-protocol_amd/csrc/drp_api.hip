@@ -244,7 +244,12 @@ int drp_open(int device, drp_ctx **out) {
   if (!out) return DRP_E_INVAL;
   *out = nullptr;
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return DRP_E_NODEV;
+  const hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= device || device < 0) {
+    if (getenv("DRP_DEBUG"))
+      fprintf(stderr, "drp_open(%d): hipGetDeviceCount -> %s, %d devices\n", device, hipGetErrorString(e), n);
+    return DRP_E_NODEV;
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return DRP_E_NODEV;
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return DRP_E_NODEV;

@@ -1604,10 +1604,8 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   const TileGeo G = tile_geo(P, t);
   if (t >= ntiles) return;  // (whole workgroup)
-  // (a large batch's sparse streams take the hop walkers instead; walk_regions lists the edge tiles)
-  if (P.walk_rp && walk_hops(P)) return;
   if (G.A < G.so || G.A + IMG > G.se) {  // edge tile: the general kernel
-    if (!P.walk_rp) push_work(P, t);
+    push_work(P, t);
     return;
   }
   uint32_t eb, en, ecn;
@@ -3377,13 +3375,23 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
   }
   // interior tiles in the fast form (or by the region walkers); the edge and dense tiles they list
   // in the general one
+  if (Q.walk_rp && Q.walk_hop == 2u) {
+    // the claims form of a large batch, per launch: a density sample from the streams' exact
+    // entries (one small kernel and a 16-byte read back): sparse streams (> HOP_FRAME bytes per
+    // frame) take the hop walkers, dense ones claims_fast
+    unsigned long long d[2] = {0, 0};
+    hipError_t e = drp_launch_walk_density(&Q, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d, Q.walk_dense, 16, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+    if (d[0] > (unsigned long long)spec::HOP_FRAME * d[1]) Q.walk_hop = 1u;
+    else Q.walk_rp = nullptr;
+  }
   if (Q.walk_rp) {
     const hipError_t e = drp_launch_claims_walk(&Q, nt_max, st);
     if (e != hipSuccess) return e;
     drp_dbg_mark("claims_walk", st);
-    if (Q.walk_hop == 2u)  // (dense streams: claims_fast; it exits at once when the batch is sparse)
-      hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
-  } else if (Q.change_checks)
+  } else if (Q.change_checks && !P->walk_rp)
     hipLaunchKernelGGL(spec::claims_fast<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
   else
     hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);

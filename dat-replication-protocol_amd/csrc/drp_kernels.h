@@ -78,7 +78,7 @@ struct DecodeParams {
   uint64_t *walk_rp;
   uint64_t *walk_entry;  // region walkers: each region's entry (walk_sync)
   uint32_t walk_hop;      // 1: the hop walkers (claims_hop), 0: the ring walkers (claims_walk), 2: by walk_dense
-  unsigned long long *walk_dense;  // walk_sync's density sample: bytes, frames after the entries
+  unsigned long long *walk_dense;  // walk_density's sample: bytes, frames after stream entries
   uint32_t walk_tpr;
   // per-frame records (null: none): rec_cap 32-byte slots per region; per tile its first record
   // (REC_NONE: none, the tile takes the wire-reading emission) and whether verification lets the
@@ -131,6 +131,7 @@ uint32_t drp_spec_miss_bit(void);
 uint32_t drp_spec_cascade_bit(void);
 hipError_t drp_launch_claims_walk(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t st);
 uint32_t drp_walk_tiles_per_region(uint64_t nt_max, int hop);
+hipError_t drp_launch_walk_density(const drp::DecodeParams *P, hipStream_t st);
 hipError_t drp_launch_emit_rec(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t st);
 uint64_t drp_walk_rec_cap(uint32_t tpr);
 hipError_t drp_launch_spec_head(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,

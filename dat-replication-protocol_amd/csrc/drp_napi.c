@@ -205,9 +205,11 @@ static void col_put(colblock *b) {
 
 /* finalizer of a batch's column Buffer (JS thread) */
 static void col_finalize(napi_env env, void *data, void *hint) {
-  (void)env;
   (void)data;
-  col_put((colblock *)hint);
+  colblock *b = (colblock *)hint;
+  int64_t adj;
+  if (!b->st->closing) napi_adjust_external_memory(env, -(int64_t)b->cap, &adj);
+  col_put(b);
 }
 
 static void comm_cache_clear(env_state *st) {
@@ -394,9 +396,8 @@ static napi_value dec_result(napi_env env, dec_job *j) {
   if (j->blk) {
     stt = napi_create_external_buffer(env, j->bytes, base, col_finalize, j->blk, &buf);
     if (stt == napi_ok) {
-      /* (not reported to V8 as external memory: a batch's block would count its full size against
-         the heap limit and every few batches force a full collection, ~1/3 of the JS replay time;
-         the small Buffer objects die young and go with the scavenges) */
+      int64_t adj;
+      napi_adjust_external_memory(env, (int64_t)j->blk->cap, &adj); /* (so V8 collects spent batches soon) */
       j->blk->refs = 1;
       j->blk = NULL; /* (the Buffer owns it now) */
     }

@@ -133,15 +133,12 @@ __device__ __forceinline__ Hdr hdr_global(const uint8_t *g, uint64_t p, uint64_t
 }
 
 
-// The claims form of a large batch, chosen on the device per launch from the region syncs'
-// density sample (drp_walk.hip walk_sync): streams averaging <= HOP_FRAME bytes per frame after
-// the regions' entries take claims_fast, sparser ones the hop walkers (claims_hop: one header read
-// per frame, so long frames cost nothing extra). P.walk_hop: 1 / 0 force the hop / ring walkers.
+// The claims form of a large batch (drp_launch_spec_head chooses it per launch from a density
+// sample, walk_density): streams averaging <= HOP_FRAME bytes per frame take claims_fast, sparser
+// ones the hop walkers (claims_hop: one header read per frame, so long frames cost nothing
+// extra). P.walk_hop: 1 the hop walkers, 0 the ring walkers (forced: DRP_CLAIMS=hop / walk).
 constexpr uint32_t HOP_FRAME = 512;
-__device__ __forceinline__ bool walk_hops(const DecodeParams &P) {
-  if (P.walk_hop != 2u) return P.walk_hop == 1u;
-  return P.walk_dense[0] > (unsigned long long)HOP_FRAME * P.walk_dense[1];
-}
+__device__ __forceinline__ bool walk_hops(const DecodeParams &P) { return P.walk_hop == 1u; }
 
 }  // namespace spec
 }  // namespace drp

@@ -176,6 +176,15 @@ __device__ __forceinline__ uint64_t g_rd8(const uint8_t *g, uint64_t p) {
   return x;
 }
 
+// 8 bytes at absolute position p from one 16-byte load at p's dword (the hop walkers: one memory
+// request per frame; p + 16 <= nbytes + 3)
+typedef uint32_t wk_u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ uint64_t g_rd8x(const uint8_t *g, uint64_t p) {
+  const wk_u32x4 v = *reinterpret_cast<const wk_u32x4 *>(g + (p & ~3ull));
+  const uint32_t sh = (uint32_t)(p & 3u) * 8u;
+  return (uint64_t)__builtin_amdgcn_alignbit(v.y, v.x, sh) | ((uint64_t)__builtin_amdgcn_alignbit(v.z, v.y, sh) << 32);
+}
+
 // A frame header from its first 8 bytes x: the length varint of 1..5 bytes, then the id.
 // k = 0: a longer varint (L >= 2^35: the slow path decides).
 struct WHdr {
@@ -569,79 +578,82 @@ __device__ __forceinline__ bool sync_merges(const GReader &R, uint64_t c, uint64
   return p == to;
 }
 
+// The entry of region G (see above).
+__device__ __forceinline__ uint64_t sync_entry(const DecodeParams &P, const Region &G) {
+  if (G.exact) return G.entry;
+  const GReader R{P.bytes, P.nbytes};
+  const uint64_t se = G.se, end = G.A0 + (uint64_t)(G.nw / WK_WPT) * TILE;
+  // the first shaped candidate (within SY_SHAPE bytes: a stream without Changes goes on to the
+  // general scan soon)
+  uint64_t shaped = ~0ull;
+  const uint64_t aend = umin64(end, G.A0 + SY_SHAPE);
+#pragma unroll 1
+  for (uint64_t c128 = G.A0; c128 < aend && shaped == ~0ull; c128 += 128u) {
+    uint64_t hi;
+    uint64_t m = sync_shape128(R, c128, hi);
+#pragma unroll 1
+    for (uint32_t half = 0; half < 2u && shaped == ~0ull; half++, m = hi) {
+#pragma unroll 1
+      while (m) {
+        const uint64_t c = c128 + 64u * half + (uint32_t)__builtin_ctzll(m);
+        m &= m - 1u;
+        if (wk_shaped(R, c, se)) {
+          shaped = c;
+          break;
+        }
+      }
+    }
+  }
+  if (shaped == ~0ull) return sync_general(R, G.A0, umin64(end, G.A0 + SY_GENERAL), se);
+  // an earlier candidate (up to SY_MERGE bytes before it) whose chain lands exactly on it: the
+  // region starts in other frames (blobs, short frames)
+  const uint64_t from = shaped - G.A0 > SY_MERGE ? (shaped - SY_MERGE) & ~63ull : G.A0;
+#pragma unroll 1
+  for (uint64_t c64 = from; c64 < shaped; c64 += 64u) {
+    uint64_t live = sync_live64(R, c64);
+#pragma unroll 1
+    while (live) {
+      const uint64_t c = c64 + (uint32_t)__builtin_ctzll(live);
+      live &= live - 1u;
+      if (c >= shaped) break;
+      const WHdr h = wk_hdr(R.rd8(c));
+      if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0) || c + h.k + (h.id ? h.L : 1u) > shaped) continue;
+      if (sync_merges(R, c, shaped)) return c;
+    }
+  }
+  return shaped;
+}
+
 __global__ __launch_bounds__(256) void walk_sync(DecodeParams P) {
   const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (r >= P.walk_rp[P.nstreams]) return;
   const Region G = region_of(P, r);
-  const GReader R{P.bytes, P.nbytes};
-  const uint64_t se = G.se, end = G.A0 + (uint64_t)(G.nw / WK_WPT) * TILE;
-  uint64_t found = ~0ull;
-  if (G.exact) {
-    found = G.entry;
-  } else {
-    // the first shaped candidate (within SY_SHAPE bytes: a stream without Changes goes on to the
-    // general scan soon)
-    uint64_t shaped = ~0ull;
-    const uint64_t aend = umin64(end, G.A0 + SY_SHAPE);
-#pragma unroll 1
-    for (uint64_t c128 = G.A0; c128 < aend && shaped == ~0ull; c128 += 128u) {
-      uint64_t hi;
-      uint64_t m = sync_shape128(R, c128, hi);
-#pragma unroll 1
-      for (uint32_t half = 0; half < 2u && shaped == ~0ull; half++, m = hi) {
-#pragma unroll 1
-        while (m) {
-          const uint64_t c = c128 + 64u * half + (uint32_t)__builtin_ctzll(m);
-          m &= m - 1u;
-          if (wk_shaped(R, c, se)) {
-            shaped = c;
-            break;
-          }
-        }
-      }
-    }
-    found = shaped;
-    if (shaped != ~0ull) {
-      // an earlier candidate (up to SY_MERGE bytes before it) whose chain lands exactly on it:
-      // the region starts in other frames (blobs, short frames)
-      const uint64_t from = shaped - G.A0 > SY_MERGE ? (shaped - SY_MERGE) & ~63ull : G.A0;
-#pragma unroll 1
-      for (uint64_t c64 = from; c64 < shaped && found == shaped; c64 += 64u) {
-        uint64_t live = sync_live64(R, c64);
-#pragma unroll 1
-        while (live) {
-          const uint64_t c = c64 + (uint32_t)__builtin_ctzll(live);
-          live &= live - 1u;
-          if (c >= shaped) break;
-          const WHdr h = wk_hdr(R.rd8(c));
-          if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0) || c + h.k + (h.id ? h.L : 1u) > shaped) continue;
-          if (sync_merges(R, c, shaped)) {
-            found = c;
-            break;
-          }
-        }
-      }
-    } else {
-      found = sync_general(R, G.A0, umin64(end, G.A0 + SY_GENERAL), se);
-    }
-  }
+  const uint64_t found = sync_entry(P, G), se = G.se;
   P.walk_entry[r] = found;
-  // the batch's frame density, from two frames after each entry (the walkers' form: P.walk_dense)
-  if (found != ~0ull && found < se) {
-    uint64_t p = found;
-    uint32_t nf = 0;
-#pragma unroll 1
-    for (; nf < 2u; nf++) {
-      const WHdr h = wk_hdr(R.rd8(p));
-      if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0) || p + h.k + h.L >= se) break;
-      p += h.k + (h.id ? h.L : 1u);
-    }
-    if (nf) {
-      atomicAdd(&P.walk_dense[0], (unsigned long long)(p - found));
-      atomicAdd(&P.walk_dense[1], (unsigned long long)nf);
-    }
-  }
   if (P.stats && found != ~0ull) atomicAdd(&P.stats[31], 1ull);
+}
+
+// The batch's frame density, sampled before the claims form is chosen (drp_launch_spec_head):
+// four frames from the exact entries of up to 256 streams spread over the batch
+// (P.walk_dense: bytes, frames).
+__global__ __launch_bounds__(256) void walk_density(DecodeParams P) {
+  const uint64_t ns = P.nstreams, k = threadIdx.x;
+  if (k >= ns || k >= 256u) return;
+  const uint64_t s = k * ns / umin64(ns, 256u);
+  const uint64_t e = P.stream_off[s] + (P.entry ? P.entry[s] : 0ull), se = P.stream_off[s + 1];
+  const GReader R{P.bytes, P.nbytes};
+  uint64_t p = e;
+  uint32_t nf = 0;
+#pragma unroll 1
+  for (; nf < 4u && p < se; nf++) {
+    const WHdr h = wk_hdr(R.rd8(p));
+    if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0) || p + h.k + h.L > se) break;
+    p += h.k + (h.id ? h.L : 1u);
+  }
+  if (nf) {
+    atomicAdd(&P.walk_dense[0], (unsigned long long)(p - e));
+    atomicAdd(&P.walk_dense[1], (unsigned long long)nf);
+  }
 }
 
 // ---- the walkers -----------------------------------------------------------------------------
@@ -933,7 +945,7 @@ __global__ __launch_bounds__(256) void claims_hop(DecodeParams P) {
   };
 #pragma unroll 1
   while (mode == WM_WALK && pos < end) {
-    const uint64_t x = g_rd8(P.bytes, pos);
+    const uint64_t x = g_rd8x(P.bytes, pos);
     const uint32_t rel = (uint32_t)(pos - A0);
     if (rel / TILE > tcur) close_to(rel / TILE);
     if (rel / 512u > gcur) flush_to(rel / 512u);
@@ -1046,6 +1058,11 @@ extern "C" hipError_t drp_launch_claims_walk(const DecodeParams *P, uint64_t nt_
   if (P->walk_hop) return hipGetLastError();  // (2: dense batches take claims_fast, launched by the caller)
   if (P->rec) hipLaunchKernelGGL(spec::claims_walk<true>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
   else hipLaunchKernelGGL(spec::claims_walk<false>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t drp_launch_walk_density(const DecodeParams *P, hipStream_t st) {
+  hipLaunchKernelGGL(spec::walk_density, dim3(1), dim3(256), 0, st, *P);
   return hipGetLastError();
 }
 

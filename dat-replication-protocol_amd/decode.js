@@ -27,6 +27,7 @@ var native = require('./native')
 var FLUSH = Buffer.from([0]) // identity-compared end sentinel (decode.js:6, :125)
 var MAX_BATCH = Number(process.env.DRP_MAX_BATCH) || 64 * 1024 * 1024 // bytes written ahead
 var PIECE = Math.min(MAX_BATCH, Number(process.env.DRP_PIECE) || 16 * 1024 * 1024) // bytes per GPU call
+var FIRST_PIECE = 1024 * 1024 // the first batch after the decoder ran dry
 var MAX_FRAME = require('buffer').constants.MAX_LENGTH
 
 // a batch whose frames average at most TEXT_PER_FRAME bytes has its ASCII keys cut from one
@@ -136,7 +137,7 @@ function Decoder (opts) {
   this._blobPos = -1      // batch offset of the next piece of a blob row being delivered
   // ms, summed; bytes staged into HBM, blob payload bytes left in host memory, bytes copied on
   // the host (gathered for HBM, frames straddling two writes, carried frames)
-  this.timing = { batches: 0, h2d: 0, gpu: 0, d2h: 0, convert: 0, replay: 0, h2dBytes: 0, h2dSkipped: 0, hostCopied: 0 }
+  this.timing = { batches: 0, h2d: 0, gpu: 0, d2h: 0, convert: 0, replay: 0, h2dBytes: 0, h2dSkipped: 0, hostCopied: 0, d2hMax: 0, pinnedBatches: 0 }
 
   var self = this
   this._up = function () {
@@ -147,6 +148,12 @@ function Decoder (opts) {
     if (--self._pending > 0 || !self._paused) return
     self._paused = false
     self._deliver()
+  }
+  this._scheduled = false
+  this._formFn = function () {
+    self._scheduled = false
+    self._form()
+    self._deliver() // (a batch that only filled a carried frame needs no GPU call)
   }
 }
 util.inherits(Decoder, stream.Writable)
@@ -181,8 +188,13 @@ Decoder.prototype._write = function (data, enc, cb) {
   if (this._taken > 0) {
     this._taken-- // (read ahead into a batch already)
   } else {
+    // not read ahead: a batch from it and the writes made in the same turn of the event loop
+    // (a producer writes its next chunks right after this call returns)
     this._rest = { chunk: data, off: 0 }
-    this._form()
+    if (!this._scheduled) {
+      this._scheduled = true
+      setImmediate(this._formFn)
+    }
   }
   this._deliver()
 }
@@ -221,7 +233,10 @@ Decoder.prototype._form = function () {
   if (this._inflight || this._halt || this.destroyed) return
   var segs = [] // {chunk, a, b, write}: bytes [a, b) of a written chunk; write: its last byte is here
   var size = 0
-  while (size < PIECE) {
+  // a decoder with nothing decoded to replay starts with a small batch, so its callbacks start
+  // after a short GPU call; the batches behind it are decoded while it is replayed
+  var piece = this._batches.length ? PIECE : Math.min(PIECE, FIRST_PIECE)
+  while (size < piece) {
     var r = this._rest
     if (!r) {
       var e = this._bufferedNext()
@@ -229,7 +244,7 @@ Decoder.prototype._form = function () {
       this._taken++
       r = this._rest = { chunk: e, off: 0 }
     }
-    var take = Math.min(r.chunk.length - r.off, PIECE - size)
+    var take = Math.min(r.chunk.length - r.off, piece - size)
     var last = r.off + take === r.chunk.length
     segs.push({ chunk: r.chunk, a: r.off, b: r.off + take, write: last, first: r.off === 0 })
     size += take
@@ -328,6 +343,8 @@ Decoder.prototype._ondecoded = function (err, res, batch) {
     tm.h2d += t.h2d
     tm.gpu += t.gpu
     tm.d2h += t.d2h
+    if (t.d2h > tm.d2hMax) tm.d2hMax = t.d2h
+    tm.pinnedBatches += t.pinnedColumns || 0
     tm.convert += t.convert
     tm.h2dBytes += t.h2dBytes || 0
     tm.h2dSkipped += t.h2dSkipped || 0
@@ -431,11 +448,10 @@ Decoder.prototype._replay = function (batch, lim) {
   var chunks = batch.chunks
   var starts = batch.starts
   var text = batch.text
-  if (text === undefined) { // (one latin1 string of the batch, its chunks joined: V8 copies it once)
-    var parts = new Array(chunks.length)
-    for (var q = 0; q < chunks.length; q++) parts[q] = chunks[q].toString('latin1')
-    text = batch.text = parts.join('')
-    this.timing.hostCopied += batch.size
+  if (text === undefined) { // (one latin1 string of the batch; from one buffer, so V8 makes it in
+    // large-object space at once: strings per chunk would be young objects its scavenges copy)
+    text = batch.text = (chunks.length === 1 ? chunks[0] : Buffer.concat(chunks, batch.size)).toString('latin1')
+    this.timing.hostCopied += chunks.length === 1 ? batch.size : 2 * batch.size
   }
   var down = this._down
   var i = this._next

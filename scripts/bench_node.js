@@ -45,7 +45,7 @@ function once (done) {
     // running the callbacks) on the main thread
     var b = breakdown.slice(1)
     var ms = {}
-    ;['h2d', 'gpu', 'd2h', 'convert', 'replay', 'batches'].forEach(function (k) {
+    ;['h2d', 'gpu', 'd2h', 'd2hMax', 'pinnedBatches', 'convert', 'replay', 'batches'].forEach(function (k) {
       ms[k] = b.reduce(function (a, x) { return a + x[k] }, 0) / b.length
     })
     process.stdout.write(JSON.stringify({ write_bytes: write, max_batch: Number(process.env.DRP_MAX_BATCH || 0) ||
