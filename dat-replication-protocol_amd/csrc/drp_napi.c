@@ -262,7 +262,11 @@ typedef struct {
   void *col[NCOL];
   int key_post;   /* also the key hash column (drp_set_key_post; the key flags are always on) */
   void *khash;
-  double t_h2d, t_gpu, t_d2h, t_convert; /* ms: batch to HBM, decode kernels, columns back, u64 -> Number */
+  uint32_t *kp;   /* each row's key position in `keys` (rows with an ASCII key) */
+  char *keys;     /* the batch's ASCII keys end to end (malloc'd; a latin1 string on the JS thread) */
+  uint64_t nkeys; /* its length; ~0: too long for one string (the JS layer decodes keys one by one) */
+  double t_h2d, t_gpu, t_d2h, t_convert; /* ms: batch to HBM, decode kernels, columns back,
+                                            u64 -> Number + the key text */
   double h2d_bytes, h2d_skipped, host_copied; /* bytes staged into HBM / blob payload bytes left in host
                                                  memory / bytes gathered from the chunks on the host */
 } dec_job;
@@ -270,10 +274,13 @@ typedef struct {
 static void free_cols(dec_job *j) {
   if (j->blk) col_put(j->blk); /* (never handed to JS) */
   free(j->mem);
+  free(j->keys);
   j->blk = NULL;
   j->mem = NULL;
+  j->keys = NULL;
   for (int i = 0; i < NCOL; i++) j->col[i] = NULL;
   j->khash = NULL;
+  j->kp = NULL;
 }
 
 static void free_job(dec_job *j) {
@@ -295,6 +302,7 @@ static size_t al64(size_t x) { return (x + 63) & ~(size_t)63; }
 static int alloc_cols(dec_job *j) {
   size_t need = 0;
   for (int i = 0; i < NCOL; i++) need += al64(j->rows * COL_W[i] + 8);
+  need += al64(j->rows * 4 + 8);
   if (j->key_post) need += al64(j->rows * 8 + 8);
   j->bytes = need;
   j->blk = j->st ? col_get(j->st, need) : NULL;
@@ -304,7 +312,50 @@ static int alloc_cols(dec_job *j) {
     j->col[i] = p;
     p += al64(j->rows * COL_W[i] + 8);
   }
+  j->kp = (uint32_t *)p;
+  p += al64(j->rows * 4 + 8);
   if (j->key_post) j->khash = p;
+  return DRP_OK;
+}
+
+/* The ASCII keys of the batch's Change rows end to end, copied from the written chunks, and
+   each row's position in them: the JS thread makes one latin1 string of them and cuts every such
+   key as a substring (a string per key from the chunk, toString('utf8'), costs a UTF-8 decode and
+   a native call per frame; a string of the whole batch copies every byte, values included) */
+#define KEYS_MAX ((uint64_t)256 << 20) /* (well below V8's string length limit) */
+
+static int key_text(dec_job *j) {
+  const uint64_t *off = (const uint64_t *)j->col[C_OFF];
+  const uint32_t *ko = (const uint32_t *)j->col[C_KO], *kl = (const uint32_t *)j->col[C_KL];
+  const uint8_t *ty = (const uint8_t *)j->col[C_TYPE], *fl = (const uint8_t *)j->col[C_FL];
+  uint32_t *kp = j->kp;
+  uint64_t tot = 0;
+  for (uint64_t r = 0; r < j->rows; r++) {
+    const int on = (ty[r] & 0x3f) == DRP_TYPE_CHANGE && (fl[r] & (DRP_F_KEY_ASCII | DRP_F_BAD)) == DRP_F_KEY_ASCII;
+    kp[r] = (uint32_t)tot;
+    tot += on ? kl[r] : 0;
+    if (tot > KEYS_MAX) {
+      j->nkeys = ~(uint64_t)0;
+      return DRP_OK;
+    }
+  }
+  j->nkeys = tot;
+  j->keys = (char *)malloc(tot ? tot : 1);
+  if (!j->keys) return DRP_E_NOMEM;
+  uint64_t k = 0, s0 = 0; /* the chunk holding batch offset a, and its start */
+  for (uint64_t r = 0; r < j->rows; r++) {
+    if (!((ty[r] & 0x3f) == DRP_TYPE_CHANGE && (fl[r] & (DRP_F_KEY_ASCII | DRP_F_BAD)) == DRP_F_KEY_ASCII)) continue;
+    uint64_t a = off[r] + ko[r], n = kl[r];
+    char *d = j->keys + kp[r];
+    while (n) {
+      while (k + 1 < j->nchunks && s0 + j->chunks[k].n <= a) s0 += j->chunks[k++].n;
+      const uint64_t take = n < s0 + j->chunks[k].n - a ? n : s0 + j->chunks[k].n - a;
+      memcpy(d, j->chunks[k].bytes + (a - s0), take);
+      d += take;
+      a += take;
+      n -= take;
+    }
+  }
   return DRP_OK;
 }
 
@@ -339,8 +390,12 @@ static void dec_run(dec_job *j) {
     free_cols(j);
     return;
   }
-  /* u64 -> JS Number, in place (varint.decode yields Numbers) */
   const double t0 = now_ms();
+  if ((j->rc = key_text(j)) != DRP_OK) {
+    free_cols(j);
+    return;
+  }
+  /* u64 -> JS Number, in place (varint.decode yields Numbers) */
   const int conv[] = {C_OFF, C_CH, C_FR, C_TO};
   for (size_t k = 0; k < sizeof conv / sizeof conv[0]; k++) {
     uint64_t *u = (uint64_t *)j->col[conv[k]];
@@ -374,9 +429,15 @@ static napi_value dec_result(napi_env env, dec_job *j) {
   set_num(env, res, "tailKind", j->carry.tail_kind);
   set_num(env, res, "blobRemaining", (double)j->carry.blob_remaining);
   set_num(env, res, "frameBytes", (double)j->carry.frame_bytes);
-  napi_value yes, t;
-  napi_get_boolean(env, true, &yes);
-  napi_set_named_property(env, res, "asciiKeys", yes); /* flags carry DRP_F_KEY_ASCII */
+  napi_value t, kt;
+  if (j->keys) {
+    if (napi_create_string_latin1(env, j->keys, j->nkeys, &kt) != napi_ok) return NULL;
+    free(j->keys);
+    j->keys = NULL;
+  } else {
+    napi_get_null(env, &kt);
+  }
+  napi_set_named_property(env, res, "keyText", kt);
   if (napi_create_object(env, &t) == napi_ok) {
     set_num(env, t, "h2d", j->t_h2d);
     set_num(env, t, "h2dBytes", j->h2d_bytes);
@@ -417,6 +478,10 @@ static napi_value dec_result(napi_env env, dec_job *j) {
     napi_set_named_property(env, res, COL_NAME[i], ta);
     off += al64(j->rows * COL_W[i] + 8);
   }
+  napi_value kpa;
+  if (napi_create_typedarray(env, napi_uint32_array, j->rows, ab, off, &kpa) != napi_ok) return NULL;
+  napi_set_named_property(env, res, "kp", kpa);
+  off += al64(j->rows * 4 + 8);
   if (j->khash) {
     napi_value ta;
     if (napi_create_typedarray(env, napi_biguint64_array, j->rows, ab, off, &ta) != napi_ok) return NULL;
@@ -424,6 +489,7 @@ static napi_value dec_result(napi_env env, dec_job *j) {
   }
   for (int i = 0; i < NCOL; i++) j->col[i] = NULL;
   j->khash = NULL;
+  j->kp = NULL;
   return res;
 }
 

@@ -30,12 +30,6 @@ var PIECE = Math.min(MAX_BATCH, Number(process.env.DRP_PIECE) || 16 * 1024 * 102
 var FIRST_PIECE = 1024 * 1024 // the first batch after the decoder ran dry
 var MAX_FRAME = require('buffer').constants.MAX_LENGTH
 
-// a batch whose frames average at most TEXT_PER_FRAME bytes has its ASCII keys cut from one
-// latin1 string of the batch (cheaper than a string per key; one string per written chunk would
-// put 64 KiB strings in V8's young generation, whose scavenges copy them); larger frames keep one
-// string per key
-var TEXT_PER_FRAME = 512
-var TEXT_MAX = 256 * 1024 * 1024 // (below V8's string length limit)
 var TYPE_MASK = 0x3f
 var CONT = 0x40
 var PARTIAL = 0x80
@@ -275,7 +269,7 @@ Decoder.prototype._form = function () {
       i++
     }
     if (p.filled < p.buf.length) { // nothing to decode yet: these writes only fill the frame
-      this._queueBatch({ chunks: [], starts: [], size: 0, res: NOTHING, tooBig: 0, text: null, first: first }, slots)
+      this._queueBatch({ chunks: [], starts: [], size: 0, res: NOTHING, tooBig: 0, first: first }, slots)
       return this._form()
     }
     this._partial = null
@@ -297,7 +291,7 @@ Decoder.prototype._form = function () {
     }
     if (g.write) slots.push({ chunk: g.chunk, end: at })
   }
-  var batch = { chunks: chunks, starts: starts, size: at, res: null, tooBig: 0, text: null, first: first }
+  var batch = { chunks: chunks, starts: starts, size: at, res: null, tooBig: 0, first: first }
   this._queueBatch(batch, slots)
   this._inflight = batch
   var self = this
@@ -352,7 +346,6 @@ Decoder.prototype._ondecoded = function (err, res, batch) {
   }
   batch.res = res
   batch.tooBig = tooBig
-  batch.text = res.asciiKeys && res.n * TEXT_PER_FRAME >= batch.size && batch.size <= TEXT_MAX ? undefined : null
   this._form() // the next batch goes to the GPU before this one's callbacks run
   this._deliver()
 }
@@ -426,8 +419,9 @@ Decoder.prototype._retire = function () {
 // Deliver the batch's frames completed before batch offset `lim` (the end of the write being
 // consumed). false: stopped at a callback not yet acknowledged, or the stream ended.
 // Change frames are built inline (the hot loop: one object, one key string, one value slice per
-// frame); keys the GPU flagged ASCII are cut from one latin1 string of the batch (the same string
-// buf.toString('utf8', ...) would give, without a UTF-8 decode per key).
+// frame); keys the GPU flagged ASCII are substrings of the batch's key text (res.keyText: those
+// keys end to end, made by the addon; the same string buf.toString('utf8', ...) would give,
+// without a UTF-8 decode and a native call per key).
 Decoder.prototype._replay = function (batch, lim) {
   var res = batch.res
   var n = res.n
@@ -445,14 +439,10 @@ Decoder.prototype._replay = function (batch, lim) {
   var cf = res.from
   var ct = res.to
   var keyHash = res.keyHash
+  var keyText = typeof res.keyText === 'string' ? res.keyText : null
+  var kp = res.kp
   var chunks = batch.chunks
   var starts = batch.starts
-  var text = batch.text
-  if (text === undefined) { // (one latin1 string of the batch; from one buffer, so V8 makes it in
-    // large-object space at once: strings per chunk would be young objects its scavenges copy)
-    text = batch.text = (chunks.length === 1 ? chunks[0] : Buffer.concat(chunks, batch.size)).toString('latin1')
-    this.timing.hostCopied += chunks.length === 1 ? batch.size : 2 * batch.size
-  }
   var down = this._down
   var i = this._next
   var k = this._ck
@@ -461,6 +451,8 @@ Decoder.prototype._replay = function (batch, lim) {
     var o = off[i]
     if ((type[i] & TYPE_MASK) !== 1) {
       if (o > lim) break // (its header ends in a later write)
+      this._next = i
+      this._ck = k
       var r = this._deliverBlob(batch, i, lim)
       if (this._ck > k) k = this._ck
       if (r === 0) break // (the next piece is in a later write)
@@ -484,8 +476,8 @@ Decoder.prototype._replay = function (batch, lim) {
     var k1 = k0 + kl[i]
     var v0 = o + vcol[i] - base
     var key
-    if (text !== null && (f & KEY_ASCII)) {
-      key = text.substring(o + ko[i], o + ko[i] + kl[i])
+    if (keyText !== null && (f & KEY_ASCII)) {
+      key = keyText.substring(kp[i], kp[i] + kl[i])
     } else {
       key = c.toString('utf8', k0, k1)
     }
@@ -500,9 +492,7 @@ Decoder.prototype._replay = function (batch, lim) {
     if (keyHash) change.keyHash = keyHash[i]
     this.changes++
     this._pending++ // released by the handler's cb (_up, decode.js:89-93)
-    this._next = i + 1
-    this._ck = k
-    this._onchange(change, down)
+    this._onchange(change, down) // (nothing it calls re-enters this loop: _down only resumes a paused replay)
     i++
     if (this.destroyed) break
   }

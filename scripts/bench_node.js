@@ -5,7 +5,7 @@
 'use strict'
 var fs = require('fs')
 var path = require('path')
-var protocol = require(path.join(__dirname, '..', 'dat-replication-protocol_amd'))
+var protocol = require(process.env.DRP_PKG || path.join(__dirname, '..', 'dat-replication-protocol_amd'))
 
 var wire = fs.readFileSync(process.argv[2])
 var write = Number(process.argv[3])

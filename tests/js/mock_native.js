@@ -161,7 +161,20 @@ function finish (b, out, rows, nrows) {
     for (var i = 0; i < nrows; i++) a[i] = rows[i][k] || 0
     out[k] = a
   })
-  out.asciiKeys = true
+  // the key text (drp_napi.c key_text): the ASCII keys of the Change rows end to end
+  var kp = new Uint32Array(nrows)
+  var parts = []
+  var tot = 0
+  for (var r = 0; r < nrows; r++) {
+    kp[r] = tot
+    var x = rows[r]
+    if ((x.type & 0x3f) === TYPE_CHANGE && (x.flags & 0x14) === 0x10) {
+      parts.push(b.toString('latin1', x.off + x.ko, x.off + x.ko + x.kl))
+      tot += x.kl
+    }
+  }
+  out.kp = kp
+  out.keyText = parts.join('')
   out.t = { h2d: 0, gpu: 0, d2h: 0, convert: 0 }
   return out
 }
