@@ -32,8 +32,8 @@ import drp_dist  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # the speculative decode's kernels (drp_decode_spec.hip, drp_walk.hip) for batches of >= 32768 tiles
-DECODE_PATH = ("speculative decode: walk_regions + walk_sync + region walkers (ring or hop, chosen on the device) "
-               "+ spec_claims + verify_lite + tile scans + emit")
+DECODE_PATH = ("speculative decode: walk_regions + walk_sync + walk_density, then claims_fast (dense) or the hop "
+               "walkers (sparse) by a 16-byte density read-back + spec_claims + verify_lite + tile scans + emit")
 FRAME = 86
 
 

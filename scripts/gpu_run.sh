@@ -9,9 +9,12 @@
 #   bench          the default bench line (C2 + c4/c5 sub-lines + CPU legs + Node path)
 #   quick          the default bench line without CPU legs and the Node path
 #   prof           rocprofv3 --kernel-trace --stats of a quick C2 + C4 + C5 run (no CPU legs)
+#   prof:<w>       the same for workload w's line alone (c2, c4, c5: its kernels' averages are per launch)
 #   pmc:<w>        FETCH_SIZE / WRITE_SIZE / SQ passes of workload w (c2, c4, c5) (scripts/gpu_pmc.sh)
 #   ab:<variant>   quick C2 + C5 lines with exp/<variant>/libdrp.so (scripts/build_variant.sh)
 #   probe:<script> python3 scripts/<script> (a measurement script)
+#   pack           summarise this session's prof / pmc outputs (kernel_phases.txt, pmc_<w>.json) and
+#                  delete their per-dispatch CSVs (gpurun copies back at most 64 MiB)
 #   env:K=V        export K=V for the steps that follow (unenv:K unsets it)
 #   c2 / c4 / c5   that workload's line alone (no sub-lines, no CPU legs), appended to <step>.log
 set -e
@@ -51,10 +54,15 @@ for step in "$@"; do
         python3 -u $ROOT/bench.py --steps 5 --warmup 2 --no-cpu > $ROOT/$OUT/bench_prof.log 2>&1)
       echo prof done
       ;;
+    prof:*)
+      W=${step#prof:}
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/prof_$W -o run -- \
+        python3 -u $ROOT/bench.py --workload $W --steps 10 --warmup 2 --no-cpu --no-sub > $ROOT/$OUT/bench_prof_$W.log 2>&1)
+      echo "prof $W done"
+      ;;
     pmc:*)
       W=${step#pmc:}
-      F=20000000
-      [ "$W" = c2 ] || F=100000000
+      F=100000000
       timeout -k 10 700 bash scripts/gpu_pmc.sh $F $W $OUT/pmc_$W
       echo "pmc $W done"
       ;;
@@ -68,6 +76,18 @@ for step in "$@"; do
       S=${step#probe:}
       timeout -k 10 400 python3 -u scripts/$S > $OUT/probe_${S%%.*}.log 2>&1
       echo "probe $S done"
+      ;;
+    pack)
+      for d in $OUT/pmc_*/; do
+        [ -d "$d" ] || continue
+        w=$(basename $d)
+        w=${w#pmc_}
+        python3 scripts/pmc_kernels.py --dir $d --workload $w --write $OUT/pmc_$w.json > $OUT/pmc_$w.txt 2>&1 || true
+      done
+      T=($OUT/prof/*kernel_trace.csv)
+      if [ -f "${T[0]}" ]; then python3 scripts/trace_phases.py ${T[0]} 7 > $OUT/kernel_phases.txt 2>&1 || true; fi
+      find $OUT -name "*.csv" ! -name "*kernel_stats.csv" -delete
+      echo pack done
       ;;
     env:*)
       export "${step#env:}"
