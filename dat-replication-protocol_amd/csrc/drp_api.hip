@@ -824,6 +824,8 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
               hs[4 + 6 * k]);
     fprintf(stderr, " walk: synced regions=%llu deaths=%llu first death at %#llx lds=%#llx hbm=%#llx w|lane|o=%#llx", hs[31], hs[32],
             hs[36], hs[37], hs[38], hs[39]);
+    fprintf(stderr, " sync (lane sums): shape_cyc=%llu rest_cyc=%llu all_cyc=%llu shape_steps=%llu shaped_checks=%llu"
+            " merge_live=%llu merge_chains=%llu general=%llu", hs[33], hs[34], hs[35], hs[40], hs[41], hs[42], hs[43], hs[44]);
     fprintf(stderr, " repairs=%d (avg cycles per tile) link_rounds=%llu max=%llu tiles_over8=%llu restart_tiles=%llu"
             " jump_tiles=%llu seg_claims: walk_cycles=%llu frames=%llu tiles=%llu wg_cycles=%llu\n", pass, hs[56],
             hs[57], hs[58], hs[59], hs[60], hs[61], hs[62], hs[63], hs[55]);

@@ -3384,8 +3384,12 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
     if (e == hipSuccess) e = hipMemcpyAsync(d, Q.walk_dense, 16, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return e;
-    if (d[0] > (unsigned long long)spec::HOP_FRAME * d[1]) Q.walk_hop = 1u;
-    else Q.walk_rp = nullptr;
+    if (d[0] > (unsigned long long)spec::HOP_FRAME * d[1]) {
+      Q.walk_hop = 1u;
+      Q.walk_tpr = drp_walk_tiles_per_region(nt_max, 1);  // (the hop walkers' region count)
+    } else {
+      Q.walk_rp = nullptr;
+    }
   }
   if (Q.walk_rp) {
     const hipError_t e = drp_launch_claims_walk(&Q, nt_max, st);

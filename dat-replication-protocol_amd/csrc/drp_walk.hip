@@ -38,8 +38,19 @@ constexpr uint32_t WK_GW = 512 / WK_WB;          // windows per group of 8 segme
 constexpr uint32_t WK_LPR = WK_WB / 16;          // lanes of one DMA instruction per region
 constexpr uint32_t SY_NEAR = 256;                // a "near" sync chain's longest frame
 constexpr uint64_t SY_TAIL = 16384;              // a sync chain's tail counts this close to the stream end
-constexpr uint64_t SY_MERGE = 1024;              // a region's entry before its first shaped Change: this close
-constexpr uint64_t SY_SHAPE = 8192;              // how far a region's first shaped Change is looked for
+#ifndef DRP_SY_MERGE
+#define DRP_SY_MERGE 1024
+#endif
+constexpr uint64_t SY_MERGE = DRP_SY_MERGE;              // a region's entry before its first shaped Change: this close
+constexpr uint64_t SY_SHAPE = 8192;
+#ifndef DRP_SY_STEP
+#define DRP_SY_STEP 512
+#endif
+constexpr uint32_t SY_STEP = DRP_SY_STEP;  // bytes per step of the shaped scan (loaded at once)
+#ifndef DRP_SY_MSTEP
+#define DRP_SY_MSTEP 256
+#endif
+constexpr uint32_t SY_MSTEP = DRP_SY_MSTEP;  // bytes per step of the merge scan              // how far a region's first shaped Change is looked for
 constexpr uint64_t SY_GENERAL = 2048;            // how far the general scan looks (else: no entry, the
                                                  // region's tiles claim identity and verification walks them)
 #ifndef DRP_WK_SLOTS
@@ -57,7 +68,7 @@ constexpr uint32_t WK_NDMA = WK_SLOT / (WAVE * 16);  // DMA instructions per ste
 constexpr uint32_t WK_K = 8;                     // frames a sync chain must survive (no Change shape)
 constexpr uint32_t WK_REGIONS = DRP_WK_REGIONS;  // regions aimed at (one per resident lane)
 #ifndef DRP_HOP_REGIONS
-#define DRP_HOP_REGIONS 262144
+#define DRP_HOP_REGIONS 65536
 #endif
 constexpr uint32_t HOP_REGIONS = DRP_HOP_REGIONS;  // hop walkers: regions aimed at
 static_assert(WK_WB == 64 || WK_WB == 128, "windows of one or two segments");
@@ -475,7 +486,17 @@ __device__ __forceinline__ uint32_t sync_live16(const Rd &R, uint64_t p) {
   return wk_live16((uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32), (uint32_t)R.rd8(p + 16));
 }
 
-// live positions of 64 bytes [p, p + 64) (4 masks of 16; the loads issued together)
+// live positions of the 64 bytes x[0..7] (x: 72 bytes; 4 masks of 16)
+__device__ __forceinline__ uint64_t sync_live64w(const uint64_t *x) {
+  uint64_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    m |= (uint64_t)wk_live16((uint32_t)x[2 * i], (uint32_t)(x[2 * i] >> 32), (uint32_t)x[2 * i + 1],
+                             (uint32_t)(x[2 * i + 1] >> 32), (uint32_t)x[2 * i + 2]) << (16 * i);
+  return m;
+}
+
+// live positions of 64 bytes [p, p + 64) (the loads issued together)
 __device__ __forceinline__ uint64_t sync_live64(const GReader &R, uint64_t p) {
   uint64_t x[9];
 #pragma unroll
@@ -549,13 +570,31 @@ __device__ __forceinline__ uint32_t wk_shape16(uint32_t a, uint32_t b, uint32_t 
   return (m1 | m2 | m3) & 0xFFFFu;
 }
 
-// shape-candidate positions of 128 bytes [p, p + 128) (the loads issued together)
-__device__ __forceinline__ uint64_t sync_shape128(const GReader &R, uint64_t p, uint64_t &hi) {
-  uint64_t x[17];
+// Is there a byte pair 0x01, then 0x0a or 0x12, at positions q, q + 1 with q in [0, 132) of the
+// 136 bytes in x? Every shape candidate in the first 128 of them has one (its id byte, then the
+// first tag), so the exact masks are only computed for a block that passes (~1 in 240 of random
+// 128-byte blocks; once per real Change header). ~5 VALU per byte instead of ~13.
+__device__ __forceinline__ bool sync_pairs136(const uint64_t *x) {
+  auto zero8 = [](uint32_t y) { return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u; };  // (exact)
+  auto tag = [&](uint32_t w) { return zero8(w ^ 0x0a0a0a0au) | zero8(w ^ 0x12121212u); };
+  uint32_t any = 0;
+  uint32_t t = tag((uint32_t)x[0]);
 #pragma unroll
-  for (int i = 0; i < 17; i++) x[i] = R.rd8(p + 8u * i);
+  for (int j = 0; j < 33; j++) {
+    const uint32_t w = j & 1 ? (uint32_t)(x[j >> 1] >> 32) : (uint32_t)x[j >> 1];
+    const uint32_t wn = (j + 1) & 1 ? (uint32_t)(x[(j + 1) >> 1] >> 32) : (uint32_t)x[(j + 1) >> 1];
+    const uint32_t tn = tag(wn);
+    any |= zero8(w ^ 0x01010101u) & __builtin_amdgcn_alignbit(tn, t, 8);  // (tag of the byte after)
+    t = tn;
+  }
+  return any != 0;
+}
+
+// shape-candidate positions of the 128 bytes x[0..15] (x: 136 bytes)
+__device__ __forceinline__ uint64_t sync_shape128(const uint64_t *x, uint64_t &hi) {
   uint64_t lo = 0;
   hi = 0;
+  if (!sync_pairs136(x)) return 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const uint64_t m = wk_shape16((uint32_t)x[2 * i], (uint32_t)(x[2 * i] >> 32), (uint32_t)x[2 * i + 1],
@@ -579,46 +618,72 @@ __device__ __forceinline__ bool sync_merges(const GReader &R, uint64_t c, uint64
 }
 
 // The entry of region G (see above).
-__device__ __forceinline__ uint64_t sync_entry(const DecodeParams &P, const Region &G) {
+__device__ __forceinline__ uint64_t sync_entry(const DecodeParams &P, const Region &G, uint64_t &t_shape) {
   if (G.exact) return G.entry;
   const GReader R{P.bytes, P.nbytes};
   const uint64_t se = G.se, end = G.A0 + (uint64_t)(G.nw / WK_WPT) * TILE;
   // the first shaped candidate (within SY_SHAPE bytes: a stream without Changes goes on to the
   // general scan soon)
+  // (SY_STEP bytes per step, loaded at once: a lane's scan is a chain of dependent loads, and the
+  // syncs run at about one wave per SIMD, so it is their latency that counts)
   uint64_t shaped = ~0ull;
   const uint64_t aend = umin64(end, G.A0 + SY_SHAPE);
 #pragma unroll 1
-  for (uint64_t c128 = G.A0; c128 < aend && shaped == ~0ull; c128 += 128u) {
-    uint64_t hi;
-    uint64_t m = sync_shape128(R, c128, hi);
+  for (uint64_t cs = G.A0; cs < aend && shaped == ~0ull; cs += SY_STEP) {
+    uint64_t x[SY_STEP / 8 + 1];
+    if (P.stats) atomicAdd(&P.stats[40], 1ull);
+#pragma unroll
+    for (uint32_t i = 0; i < SY_STEP / 8 + 1; i++) x[i] = R.rd8(cs + 8u * i);
+#pragma unroll
+    for (uint32_t b = 0; b < SY_STEP / 128; b++) {
+      const uint64_t c128 = cs + 128u * b;
+      if (shaped != ~0ull || c128 >= aend) break;
+      uint64_t hi;
+      uint64_t m = sync_shape128(x + 16 * b, hi);
 #pragma unroll 1
-    for (uint32_t half = 0; half < 2u && shaped == ~0ull; half++, m = hi) {
+      for (uint32_t half = 0; half < 2u && shaped == ~0ull; half++, m = hi) {
 #pragma unroll 1
-      while (m) {
-        const uint64_t c = c128 + 64u * half + (uint32_t)__builtin_ctzll(m);
-        m &= m - 1u;
-        if (wk_shaped(R, c, se)) {
-          shaped = c;
-          break;
+        while (m) {
+          const uint64_t c = c128 + 64u * half + (uint32_t)__builtin_ctzll(m);
+          m &= m - 1u;
+          if (P.stats) atomicAdd(&P.stats[41], 1ull);
+          if (wk_shaped(R, c, se)) {
+            shaped = c;
+            break;
+          }
         }
       }
     }
   }
-  if (shaped == ~0ull) return sync_general(R, G.A0, umin64(end, G.A0 + SY_GENERAL), se);
+  t_shape = P.stats ? __builtin_amdgcn_s_memtime() : 0;
+  if (shaped == ~0ull) {
+    if (P.stats) atomicAdd(&P.stats[44], 1ull);
+    return sync_general(R, G.A0, umin64(end, G.A0 + SY_GENERAL), se);
+  }
   // an earlier candidate (up to SY_MERGE bytes before it) whose chain lands exactly on it: the
   // region starts in other frames (blobs, short frames)
   const uint64_t from = shaped - G.A0 > SY_MERGE ? (shaped - SY_MERGE) & ~63ull : G.A0;
 #pragma unroll 1
-  for (uint64_t c64 = from; c64 < shaped; c64 += 64u) {
-    uint64_t live = sync_live64(R, c64);
+  for (uint64_t cs = from; cs < shaped; cs += SY_MSTEP) {
+    uint64_t x[SY_MSTEP / 8 + 1];
+#pragma unroll
+    for (uint32_t i = 0; i < SY_MSTEP / 8 + 1; i++) x[i] = R.rd8(cs + 8u * i);
+#pragma unroll
+    for (uint32_t b = 0; b < SY_MSTEP / 64; b++) {
+      const uint64_t c64 = cs + 64u * b;
+      if (c64 >= shaped) break;
+      uint64_t live = sync_live64w(x + 8 * b);
 #pragma unroll 1
-    while (live) {
-      const uint64_t c = c64 + (uint32_t)__builtin_ctzll(live);
-      live &= live - 1u;
-      if (c >= shaped) break;
-      const WHdr h = wk_hdr(R.rd8(c));
-      if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0) || c + h.k + (h.id ? h.L : 1u) > shaped) continue;
-      if (sync_merges(R, c, shaped)) return c;
+      while (live) {
+        const uint64_t c = c64 + (uint32_t)__builtin_ctzll(live);
+        live &= live - 1u;
+        if (c >= shaped) break;
+        const WHdr h = wk_hdr(R.rd8(c));
+        if (P.stats) atomicAdd(&P.stats[42], 1ull);
+        if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0) || c + h.k + (h.id ? h.L : 1u) > shaped) continue;
+        if (P.stats) atomicAdd(&P.stats[43], 1ull);
+        if (sync_merges(R, c, shaped)) return c;
+      }
     }
   }
   return shaped;
@@ -628,9 +693,19 @@ __global__ __launch_bounds__(256) void walk_sync(DecodeParams P) {
   const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (r >= P.walk_rp[P.nstreams]) return;
   const Region G = region_of(P, r);
-  const uint64_t found = sync_entry(P, G), se = G.se;
+  const uint64_t t0 = P.stats ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t t_shape = 0;
+  const uint64_t found = sync_entry(P, G, t_shape);
   P.walk_entry[r] = found;
-  if (P.stats && found != ~0ull) atomicAdd(&P.stats[31], 1ull);
+  if (P.stats) {  // (DRP_STATS: per-lane cycle sums of the shaped scan, the rest, the whole sync)
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if (found != ~0ull) atomicAdd(&P.stats[31], 1ull);
+    if (t_shape) {
+      atomicAdd(&P.stats[33], (unsigned long long)(t_shape - t0));
+      atomicAdd(&P.stats[34], (unsigned long long)(t1 - t_shape));
+    }
+    atomicAdd(&P.stats[35], (unsigned long long)(t1 - t0));
+  }
 }
 
 // The batch's frame density, sampled before the claims form is chosen (drp_launch_spec_head):
