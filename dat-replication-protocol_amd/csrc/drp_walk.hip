@@ -42,15 +42,7 @@ constexpr uint64_t SY_TAIL = 16384;              // a sync chain's tail counts t
 #define DRP_SY_MERGE 1024
 #endif
 constexpr uint64_t SY_MERGE = DRP_SY_MERGE;              // a region's entry before its first shaped Change: this close
-constexpr uint64_t SY_SHAPE = 8192;
-#ifndef DRP_SY_STEP
-#define DRP_SY_STEP 512
-#endif
-constexpr uint32_t SY_STEP = DRP_SY_STEP;  // bytes per step of the shaped scan (loaded at once)
-#ifndef DRP_SY_MSTEP
-#define DRP_SY_MSTEP 256
-#endif
-constexpr uint32_t SY_MSTEP = DRP_SY_MSTEP;  // bytes per step of the merge scan              // how far a region's first shaped Change is looked for
+constexpr uint64_t SY_SHAPE = 8192;              // how far a region's first shaped Change is looked for
 constexpr uint64_t SY_GENERAL = 2048;            // how far the general scan looks (else: no entry, the
                                                  // region's tiles claim identity and verification walks them)
 #ifndef DRP_WK_SLOTS
@@ -617,62 +609,88 @@ __device__ __forceinline__ bool sync_merges(const GReader &R, uint64_t c, uint64
   return p == to;
 }
 
-// The entry of region G (see above).
-__device__ __forceinline__ uint64_t sync_entry(const DecodeParams &P, const Region &G, uint64_t &t_shape) {
+// A region's sync runs on SY_LANES consecutive lanes (a group): each step of the scans gives every
+// lane of the group its own block, in address order, and the group takes the first lane that found
+// (a ballot), so the result is the one-lane scan's. More lanes per region puts more waves on the
+// SIMDs: the scans are chains of dependent loads, and one lane per region left one wave per SIMD
+// with nothing to overlap its waits.
+#ifndef DRP_SY_LANES
+#define DRP_SY_LANES 2
+#endif
+constexpr uint32_t SY_LANES = DRP_SY_LANES;
+static_assert(SY_LANES == 1 || SY_LANES == 2 || SY_LANES == 4 || SY_LANES == 8, "lanes per region");
+
+// the group's lanes holding b (bit j: the group's lane j)
+__device__ __forceinline__ uint32_t grp_ballot(bool b, uint32_t lane) {
+  return (uint32_t)((__ballot(b) >> (lane & ~(SY_LANES - 1u))) & ((1u << SY_LANES) - 1u));
+}
+// v of the group's lane j
+__device__ __forceinline__ uint64_t grp_take(uint64_t v, uint32_t lane, uint32_t j) {
+  const int src = (int)((lane & ~(SY_LANES - 1u)) + j);
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// The entry of region G (see above), on the group's lane `sub` (every lane of the group returns it;
+// the general scan's only on sub 0).
+__device__ __forceinline__ uint64_t sync_entry(const DecodeParams &P, const Region &G, uint32_t lane, uint32_t sub,
+                                               uint64_t &t_shape) {
   if (G.exact) return G.entry;
   const GReader R{P.bytes, P.nbytes};
   const uint64_t se = G.se, end = G.A0 + (uint64_t)(G.nw / WK_WPT) * TILE;
   // the first shaped candidate (within SY_SHAPE bytes: a stream without Changes goes on to the
-  // general scan soon)
-  // (SY_STEP bytes per step, loaded at once: a lane's scan is a chain of dependent loads, and the
-  // syncs run at about one wave per SIMD, so it is their latency that counts)
+  // general scan soon), 128 bytes per lane and step
   uint64_t shaped = ~0ull;
   const uint64_t aend = umin64(end, G.A0 + SY_SHAPE);
 #pragma unroll 1
-  for (uint64_t cs = G.A0; cs < aend && shaped == ~0ull; cs += SY_STEP) {
-    uint64_t x[SY_STEP / 8 + 1];
-    if (P.stats) atomicAdd(&P.stats[40], 1ull);
+  for (uint64_t cs = G.A0; cs < aend; cs += 128u * SY_LANES) {
+    const uint64_t c128 = cs + 128u * sub;
+    uint64_t found = ~0ull;
+    if (c128 < aend) {
+      if (P.stats) atomicAdd(&P.stats[40], 1ull);
+      uint64_t x[17];
 #pragma unroll
-    for (uint32_t i = 0; i < SY_STEP / 8 + 1; i++) x[i] = R.rd8(cs + 8u * i);
-#pragma unroll
-    for (uint32_t b = 0; b < SY_STEP / 128; b++) {
-      const uint64_t c128 = cs + 128u * b;
-      if (shaped != ~0ull || c128 >= aend) break;
+      for (uint32_t i = 0; i < 17; i++) x[i] = R.rd8(c128 + 8u * i);
       uint64_t hi;
-      uint64_t m = sync_shape128(x + 16 * b, hi);
+      uint64_t m = sync_shape128(x, hi);
 #pragma unroll 1
-      for (uint32_t half = 0; half < 2u && shaped == ~0ull; half++, m = hi) {
+      for (uint32_t half = 0; half < 2u && found == ~0ull; half++, m = hi) {
 #pragma unroll 1
         while (m) {
           const uint64_t c = c128 + 64u * half + (uint32_t)__builtin_ctzll(m);
           m &= m - 1u;
           if (P.stats) atomicAdd(&P.stats[41], 1ull);
           if (wk_shaped(R, c, se)) {
-            shaped = c;
+            found = c;
             break;
           }
         }
       }
     }
+    const uint32_t fm = grp_ballot(found != ~0ull, lane);
+    if (fm) {
+      shaped = grp_take(found, lane, (uint32_t)__builtin_ctz(fm));
+      break;
+    }
   }
   t_shape = P.stats ? __builtin_amdgcn_s_memtime() : 0;
   if (shaped == ~0ull) {
+    if (sub) return ~0ull;
     if (P.stats) atomicAdd(&P.stats[44], 1ull);
     return sync_general(R, G.A0, umin64(end, G.A0 + SY_GENERAL), se);
   }
   // an earlier candidate (up to SY_MERGE bytes before it) whose chain lands exactly on it: the
-  // region starts in other frames (blobs, short frames)
+  // region starts in other frames (blobs, short frames); 64 bytes per lane and step
   const uint64_t from = shaped - G.A0 > SY_MERGE ? (shaped - SY_MERGE) & ~63ull : G.A0;
 #pragma unroll 1
-  for (uint64_t cs = from; cs < shaped; cs += SY_MSTEP) {
-    uint64_t x[SY_MSTEP / 8 + 1];
+  for (uint64_t cs = from; cs < shaped; cs += 64u * SY_LANES) {
+    const uint64_t c64 = cs + 64u * sub;
+    uint64_t found = ~0ull;
+    if (c64 < shaped) {
+      uint64_t x[9];
 #pragma unroll
-    for (uint32_t i = 0; i < SY_MSTEP / 8 + 1; i++) x[i] = R.rd8(cs + 8u * i);
-#pragma unroll
-    for (uint32_t b = 0; b < SY_MSTEP / 64; b++) {
-      const uint64_t c64 = cs + 64u * b;
-      if (c64 >= shaped) break;
-      uint64_t live = sync_live64w(x + 8 * b);
+      for (uint32_t i = 0; i < 9; i++) x[i] = R.rd8(c64 + 8u * i);
+      uint64_t live = sync_live64w(x);
 #pragma unroll 1
       while (live) {
         const uint64_t c = c64 + (uint32_t)__builtin_ctzll(live);
@@ -682,22 +700,29 @@ __device__ __forceinline__ uint64_t sync_entry(const DecodeParams &P, const Regi
         if (P.stats) atomicAdd(&P.stats[42], 1ull);
         if (h.k == 0 || h.id > 2u || (h.id != 0 && h.L == 0) || c + h.k + (h.id ? h.L : 1u) > shaped) continue;
         if (P.stats) atomicAdd(&P.stats[43], 1ull);
-        if (sync_merges(R, c, shaped)) return c;
+        if (sync_merges(R, c, shaped)) {
+          found = c;
+          break;
+        }
       }
     }
+    const uint32_t fm = grp_ballot(found != ~0ull, lane);
+    if (fm) return grp_take(found, lane, (uint32_t)__builtin_ctz(fm));
   }
   return shaped;
 }
 
 __global__ __launch_bounds__(256) void walk_sync(DecodeParams P) {
-  const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (r >= P.walk_rp[P.nstreams]) return;
+  const uint32_t lane = threadIdx.x & (WAVE - 1u), sub = threadIdx.x & (SY_LANES - 1u);
+  const uint64_t r = ((uint64_t)blockIdx.x * 256u + threadIdx.x) / SY_LANES;
+  if (r >= P.walk_rp[P.nstreams]) return;  // (whole groups)
   const Region G = region_of(P, r);
   const uint64_t t0 = P.stats ? __builtin_amdgcn_s_memtime() : 0;
   uint64_t t_shape = 0;
-  const uint64_t found = sync_entry(P, G, t_shape);
+  const uint64_t found = sync_entry(P, G, lane, sub, t_shape);
+  if (sub) return;
   P.walk_entry[r] = found;
-  if (P.stats) {  // (DRP_STATS: per-lane cycle sums of the shaped scan, the rest, the whole sync)
+  if (P.stats) {  // (DRP_STATS: cycle sums over the regions of the shaped scan, the rest, the whole sync)
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     if (found != ~0ull) atomicAdd(&P.stats[31], 1ull);
     if (t_shape) {
@@ -1128,7 +1153,7 @@ extern "C" hipError_t drp_launch_claims_walk(const DecodeParams *P, uint64_t nt_
   if (nt_max == 0) return hipSuccess;
   hipLaunchKernelGGL(spec::walk_regions, dim3(1), dim3(1024), 0, st, *P);
   const uint64_t maxr = nt_max / P->walk_tpr + P->nstreams + 1;
-  hipLaunchKernelGGL(spec::walk_sync, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
+  hipLaunchKernelGGL(spec::walk_sync, dim3((uint32_t)((maxr * spec::SY_LANES + 255) / 256)), dim3(256), 0, st, *P);
   if (P->walk_hop) hipLaunchKernelGGL(spec::claims_hop, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
   if (P->walk_hop) return hipGetLastError();  // (2: dense batches take claims_fast, launched by the caller)
   if (P->rec) hipLaunchKernelGGL(spec::claims_walk<true>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
