@@ -60,7 +60,7 @@ constexpr uint32_t WK_NDMA = WK_SLOT / (WAVE * 16);  // DMA instructions per ste
 constexpr uint32_t WK_K = 8;                     // frames a sync chain must survive (no Change shape)
 constexpr uint32_t WK_REGIONS = DRP_WK_REGIONS;  // regions aimed at (one per resident lane)
 #ifndef DRP_HOP_REGIONS
-#define DRP_HOP_REGIONS 65536
+#define DRP_HOP_REGIONS 24576
 #endif
 constexpr uint32_t HOP_REGIONS = DRP_HOP_REGIONS;  // hop walkers: regions aimed at
 static_assert(WK_WB == 64 || WK_WB == 128, "windows of one or two segments");
@@ -615,7 +615,7 @@ __device__ __forceinline__ bool sync_merges(const GReader &R, uint64_t c, uint64
 // SIMDs: the scans are chains of dependent loads, and one lane per region left one wave per SIMD
 // with nothing to overlap its waits.
 #ifndef DRP_SY_LANES
-#define DRP_SY_LANES 2
+#define DRP_SY_LANES 8
 #endif
 constexpr uint32_t SY_LANES = DRP_SY_LANES;
 static_assert(SY_LANES == 1 || SY_LANES == 2 || SY_LANES == 4 || SY_LANES == 8, "lanes per region");
