@@ -165,6 +165,7 @@ struct drp_ctx {
   int device = 0;
   hipStream_t st = nullptr;
   hipEvent_t ev[4] = {};
+  hipEvent_t hev[2] = {};  // a staged piece's H2D
   uint32_t B = 128;
   int strict = 0;
   int exact = 0;  // 1: always the exact kernel (decode_tiles), never the speculative one
@@ -261,6 +262,7 @@ int drp_open(int device, drp_ctx **out) {
     return DRP_E_HIP;
   }
   for (auto &e : c->ev) (void)hipEventCreate(&e);
+  for (auto &e : c->hev) (void)hipEventCreate(&e);
   if (const char *t = getenv("DRP_TILE")) {
     uint32_t tb = (uint32_t)atoi(t);
     if (tb == 4096 || tb == 8192) c->B = tb / 64;
@@ -298,6 +300,7 @@ void drp_close(drp_ctx *c) {
   if (c->dstats) (void)hipFree(c->dstats);
   if (c->ctile) (void)hipFree(c->ctile);
   for (auto &e : c->ev) (void)hipEventDestroy(e);
+  for (auto &e : c->hev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->st);
   delete c;
 }
@@ -1051,6 +1054,18 @@ static int h2d_range(drp_ctx *c, const HostSrc &H, uint64_t a, uint64_t len, voi
 // resumed at that frame. The rows of all pieces are consecutive, as a whole-batch decode
 // writes them (a blob the batch holds whole loses the PARTIAL mark its piece gave it).
 // DRP_E_RETRY: the capacity guess was short; the caller stages the batch whole.
+// a piece's stream bounds and entry (no host buffer to keep alive: the values travel as arguments)
+__global__ void piece_meta_kernel(uint64_t *soff, uint64_t *ent, uint64_t n, uint64_t e) {
+  soff[0] = 0;
+  soff[1] = n;
+  ent[0] = e;
+}
+
+// the payload offset of a piece's last row (a cut blob's), next to its stream result
+__global__ void piece_tail_kernel(const drp_stream_result *r, const uint64_t *payload_off, uint64_t *boff) {
+  *boff = r->frames ? payload_off[r->frames - 1] : 0;
+}
+
 static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *carry,
                         uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail) {
   hipStream_t st = c->st;
@@ -1060,6 +1075,7 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
   uint64_t *soff = c->aux.at<uint64_t>(0);
   uint64_t *ent = c->aux.at<uint64_t>(16);
   drp_stream_result *dres = c->aux.at<drp_stream_result>(stage_meta);
+  uint64_t *dboff = c->aux.at<uint64_t>(stage_meta + sizeof(drp_stream_result));
   const uint64_t n = H.n;
   uint64_t copied = 0;
   const uint64_t cap = stage_cap(c, n - pos);
@@ -1074,17 +1090,21 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
   uint64_t want = std::max(kPieceMin, c->blob_run + kPieceMargin);
   float h2d_ms = 0;
   drp_timing sum = {};
-  drp_stream_result r;
+  // (per piece, one wait for the decode's verification and one for its result: the H2D, the
+  // piece's bounds and the blob row's type are queued on the stream)
+  struct {
+    drp_stream_result r;
+    uint64_t boff;  // the cut blob's payload offset in the piece (tail BLOB)
+  } hr;
+  drp_stream_result &r = hr.r;
   for (;;) {
     const uint64_t pe = std::min(n, pos + want), ps = pos & ~15ull, mp = pe - ps;
     if (!c->in_stage.ensure(mp + 64)) return DRP_E_NOMEM;
-    const double t0 = now_ms();
+    CHK(hipEventRecord(c->hev[0], st));
     if (const int rc = h2d_range(c, H, ps, mp, c->in_stage.p, st, &copied)) return rc;
-    uint64_t hv[3] = {0, mp, pos - ps};
-    CHK(hipMemcpyAsync(soff, hv, 16, hipMemcpyHostToDevice, st));
-    CHK(hipMemcpyAsync(ent, hv + 2, 8, hipMemcpyHostToDevice, st));
-    CHK(hipStreamSynchronize(st));
-    h2d_ms += (float)(now_ms() - t0);
+    hipLaunchKernelGGL(piece_meta_kernel, dim3(1), dim3(1), 0, st, soff, ent, mp, pos - ps);
+    CHK(hipGetLastError());
+    CHK(hipEventRecord(c->hev[1], st));
     staged += mp;
     drp_frames fr;
     drp_changes co;
@@ -1113,12 +1133,14 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
     sum.exact_retries += c->timing.exact_retries;
     sum.verify_relisted += c->timing.verify_relisted;
     sum.seg_repairs += c->timing.seg_repairs;
-    CHK(hipMemcpyAsync(&r, dres, sizeof(r), hipMemcpyDeviceToHost, st));
-    uint64_t boff = 0;  // the cut blob's payload offset in the piece (tail BLOB)
+    hipLaunchKernelGGL(piece_tail_kernel, dim3(1), dim3(1), 0, st, dres, fr.payload_off, dboff);
+    CHK(hipGetLastError());
+    CHK(hipMemcpyAsync(&hr, dres, sizeof(hr), hipMemcpyDeviceToHost, st));
     CHK(hipStreamSynchronize(st));
-    if (r.tail_kind == DRP_TAIL_BLOB && r.frames) {
-      CHK(hipMemcpyAsync(&boff, fr.payload_off + r.frames - 1, 8, hipMemcpyDeviceToHost, st));
-      CHK(hipStreamSynchronize(st));
+    const uint64_t boff = hr.boff;
+    {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, c->hev[0], c->hev[1]) == hipSuccess) h2d_ms += ms;
     }
     S.pieces.emplace_back(rows, ps);
     const uint64_t bad = (r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0;
@@ -1141,9 +1163,7 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
       c->blob_run = ps + boff - pos;                // (where this piece's blob payload began)
       want = std::max(kPieceMin, c->blob_run + kPieceMargin);
       if (bend <= n) {  // the batch holds the whole blob: its row is not partial
-        const uint8_t ty = DRP_TYPE_BLOB;
-        CHK(hipMemcpyAsync(S.fr.type + rows - 1, &ty, 1, hipMemcpyHostToDevice, st));
-        CHK(hipStreamSynchronize(st));
+        CHK(hipMemsetAsync(S.fr.type + rows - 1, DRP_TYPE_BLOB, 1, st));
         skipped += bend - pe;
         pos = bend;
         if (pos == n) {
