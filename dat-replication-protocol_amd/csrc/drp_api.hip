@@ -196,6 +196,7 @@ struct drp_ctx {
   DevBuf scratch, in_stage, out_stage, aux;
   PinBuf gather;  // chunked host batches: the staged ranges, gathered (drp_decode_stage_v)
   DevBuf dec_cols;  // device columns of the staged host-batch decode (drp_decode_stage)
+  DevBuf fetch_tmp; // drp_decode_fetch_block: the caller's block layout, packed on the device
   double frames_per_byte = 0;  // density of the last staged batch (sizes the next one's columns)
   int blob_skip = DRP_BLOB_SKIP_AUTO;
   bool blob_heavy = false;     // the last host batch was mostly blob payload (AUTO: stage in pieces)
@@ -1375,6 +1376,80 @@ static int fetch_staged(drp_ctx *c, const drp_frames *frames, const drp_changes 
       if (sh)
         for (uint64_t g = lo; g < hi; g++) frames->payload_off[dst + (g - g0)] += sh;
     }
+  }
+  c->timing.d2h_ms = (float)(now_ms() - t0);
+  return DRP_OK;
+}
+
+// drp_decode_fetch_block: the staged columns' rows packed into the caller's block layout on the
+// device (one launch), then one D2H of the block
+struct PackSegs {
+  const uint8_t *src[DRP_FETCH_COLS];
+  uint64_t dst[DRP_FETCH_COLS];
+  uint64_t bytes[DRP_FETCH_COLS];
+  uint32_t n;
+};
+__global__ __launch_bounds__(256) void pack_cols_kernel(PackSegs S, uint8_t *out) {
+  // bytes [i, i + 16) of the segments' concatenation (they may span several short segments)
+  const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 16u, e = i + 16u;
+  uint64_t base = 0;
+  for (uint32_t k = 0; k < S.n && base < e; k++) {
+    const uint64_t end = base + S.bytes[k], lo = i > base ? i : base, hi = e < end ? e : end;
+    for (uint64_t x = lo; x < hi; x++) out[S.dst[k] + (x - base)] = S.src[k][x - base];
+    base = end;
+  }
+}
+
+int drp_decode_fetch_block(drp_ctx *c, void *block, uint64_t block_bytes, const uint64_t *col_off, uint64_t first,
+                           uint64_t rows) {
+  if (!c || (!block && block_bytes) || !col_off) return DRP_E_INVAL;
+  static const uint32_t W[DRP_FETCH_COLS] = {8, 4, 1, 4, 4, 4, 4, 4, 4, 8, 8, 8, 1, 8};
+  const bool kh = col_off[13] != ~0ull;
+  for (int k = 0; k < DRP_FETCH_COLS - (kh ? 0 : 1); k++)
+    if (col_off[k] > block_bytes || rows * W[k] > block_bytes - col_off[k]) return DRP_E_INVAL;
+  if (rows && is_device_ptr(block)) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  auto &S = c->staged;
+  if (first > S.rows || rows > S.rows - first) return DRP_E_INVAL;
+  if (kh && !S.co.key_hash) return DRP_E_INVAL;  // not computed: drp_set_key_post(ctx, 1) first
+  if (!rows) return DRP_OK;
+  uint8_t *B = static_cast<uint8_t *>(block);
+  const double t0 = now_ms();
+  const uint64_t dst = first == 0 && S.nf0 ? 1 : 0;  // (a carried blob row: set on the host below)
+  const uint64_t g0 = first + dst - S.nf0, ng = rows - dst;
+  if (ng) {
+    if (!c->fetch_tmp.ensure(block_bytes)) return DRP_E_NOMEM;
+    const void *src[DRP_FETCH_COLS] = {S.fr.payload_off, S.fr.payload_len, S.fr.type, S.co.key_off, S.co.key_len,
+                                       S.co.subset_off, S.co.subset_len, S.co.value_off, S.co.value_len,
+                                       S.co.change, S.co.from, S.co.to, S.co.flags, S.co.key_hash};
+    PackSegs P = {};
+    uint64_t total = 0;
+    for (int k = 0; k < DRP_FETCH_COLS - (kh ? 0 : 1); k++) {
+      P.src[P.n] = static_cast<const uint8_t *>(src[k]) + g0 * W[k];
+      P.dst[P.n] = col_off[k] + dst * W[k];
+      P.bytes[P.n] = ng * W[k];
+      total += ng * W[k];
+      P.n++;
+    }
+    const uint64_t threads = (total + 15) / 16;
+    hipLaunchKernelGGL(pack_cols_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, c->st, P,
+                       static_cast<uint8_t *>(c->fetch_tmp.p));
+    CHK(hipGetLastError());
+    CHK(hipMemcpyAsync(B, c->fetch_tmp.p, block_bytes, hipMemcpyDeviceToHost, c->st));
+    CHK(hipStreamSynchronize(c->st));
+    uint64_t *poff = reinterpret_cast<uint64_t *>(B + col_off[0]);
+    for (size_t k = 0; k < S.pieces.size(); k++) {  // (as fetch_staged: piece offsets -> batch offsets)
+      const uint64_t r0 = S.pieces[k].first, r1 = k + 1 < S.pieces.size() ? S.pieces[k + 1].first : ~0ull;
+      const uint64_t sh = S.pieces[k].second, lo = std::max(r0, g0), hi = std::min(r1, g0 + ng);
+      if (sh)
+        for (uint64_t g = lo; g < hi; g++) poff[dst + (g - g0)] += sh;
+    }
+  }
+  if (dst) {  // (the other columns of that row are zero)
+    for (int k = 3; k < DRP_FETCH_COLS - (kh ? 0 : 1); k++) memset(B + col_off[k], 0, W[k]);
+    reinterpret_cast<uint64_t *>(B + col_off[0])[0] = S.off0;
+    reinterpret_cast<uint32_t *>(B + col_off[1])[0] = S.len0;
+    B[col_off[2]] = S.ty0;
   }
   c->timing.d2h_ms = (float)(now_ms() - t0);
   return DRP_OK;

@@ -369,11 +369,12 @@ static void dec_run(dec_job *j) {
     /* rows to expose: delivered frames plus a malformed Change (its flags say why) */
     j->rows = j->nf + ((j->ec == DRP_ERR_CHANGE || j->ec == DRP_ERR_REQUIRED) ? 1 : 0);
     j->rc = alloc_cols(j);
-    if (j->rc == DRP_OK) {
-      drp_frames fr = {j->col[C_OFF], j->col[C_LEN], j->col[C_TYPE]};
-      drp_changes co = {j->col[C_KO], j->col[C_KL], j->col[C_SO], j->col[C_SL], j->col[C_VO],
-                        j->col[C_VL], j->col[C_CH], j->col[C_FR], j->col[C_TO], j->col[C_FL], j->khash};
-      j->rc = drp_decode_fetch(j->box->c, &fr, &co, 0, j->rows);
+    if (j->rc == DRP_OK) {  /* the columns' block in one transfer (its layout: alloc_cols) */
+      char *base = j->blk ? (char *)j->blk->p : (char *)j->mem;
+      uint64_t off[DRP_FETCH_COLS];
+      for (int i = 0; i < NCOL; i++) off[i] = (uint64_t)((char *)j->col[i] - base);
+      off[13] = j->khash ? (uint64_t)((char *)j->khash - base) : ~(uint64_t)0;
+      j->rc = drp_decode_fetch_block(j->box->c, base, j->bytes, off, 0, j->rows);
     }
   }
   drp_timing tm;

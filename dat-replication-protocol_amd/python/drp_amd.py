@@ -23,7 +23,7 @@ EXPORTS = [
     "drp_abi_version", "drp_open", "drp_close", "drp_stream", "drp_synchronize",
     "drp_last_timing", "drp_set_tile", "drp_set_strict", "drp_set_exact", "drp_set_key_post",
     "drp_set_blob_skip", "drp_decode_scratch_bytes",
-    "drp_decode_device", "drp_decode_batch", "drp_decode_stage", "drp_decode_stage_v", "drp_decode_fetch",
+    "drp_decode_device", "drp_decode_batch", "drp_decode_stage", "drp_decode_stage_v", "drp_decode_fetch", "drp_decode_fetch_block",
     "drp_encode_size", "drp_encode_device",
     "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results", "drp_device",
     "drp_comm_id", "drp_comm_init_rank", "drp_comm_init_all", "drp_comm_destroy",

@@ -253,6 +253,16 @@ int drp_decode_stage(drp_ctx *ctx, const uint8_t *bytes, uint64_t n, drp_carry *
                      uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail);
 int drp_decode_fetch(drp_ctx *ctx, const drp_frames *frames, const drp_changes *cols, uint64_t first,
                      uint64_t rows);
+/* drp_decode_fetch into one caller-owned HOST block [block, block + block_bytes) that libdrp may
+ * write anywhere in (padding between the columns included): column k at block + col_off[k], in
+ * the order payload_off, payload_len, type, key_off, key_len, subset_off, subset_len, value_off,
+ * value_len, change, from, to, flags, key_hash (col_off[13] = UINT64_MAX: no key hash column).
+ * The columns are packed on the device in that layout and copied in one transfer (page-locked
+ * blocks: one DMA instead of one per column). Replaces the same per-frame loop as
+ * drp_decode_fetch (decode.js:144-169 with messages.Change.decode). */
+#define DRP_FETCH_COLS 14
+int drp_decode_fetch_block(drp_ctx *ctx, void *block, uint64_t block_bytes, const uint64_t *col_off, uint64_t first,
+                           uint64_t rows);
 /* drp_decode_stage over a batch the caller holds as chunks (its queued writes), laid end to end:
  * the caller never concatenates them. The ranges the decode stages into HBM (all of the batch,
  * or with blob skipping everything but the blob payloads) are gathered from the chunks into
