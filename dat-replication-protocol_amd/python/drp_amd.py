@@ -114,6 +114,7 @@ def lib():
         L.drp_decode_stage_v.argtypes = [P, C.POINTER(Chunk), U64, C.POINTER(Carry), C.POINTER(U64), C.POINTER(U64),
                                          C.POINTER(U32), C.POINTER(U32)]
         L.drp_decode_fetch.argtypes = [P, C.POINTER(Frames), C.POINTER(Changes), U64, U64]
+        L.drp_decode_fetch_block.argtypes = [P, P, U64, C.POINTER(U64), U64, U64]
         L.drp_encode_size.argtypes = [P, C.POINTER(ChangeSrc), U64, C.POINTER(U64)]
         L.drp_encode_device.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, P, U64]
         L.drp_encode_batch.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, U64,
@@ -282,10 +283,12 @@ class Ctx:
                    frame_bytes=int(carry.frame_bytes))
         return res
 
-    def decode_staged(self, wire, blob_remaining=0, pieces=1, key_hash=False):
+    def decode_staged(self, wire, blob_remaining=0, pieces=1, key_hash=False, block=False):
         """drp_decode_stage, then drp_decode_fetch of the rows in `pieces` consecutive
         fetches into host columns sized from the frame count (the N-API addon's path). `wire`
-        as a list of byte strings: the batch is those chunks end to end (drp_decode_stage_v)."""
+        as a list of byte strings: the batch is those chunks end to end (drp_decode_stage_v).
+        block=True: one drp_decode_fetch_block of every row into one host block instead (the
+        columns at 64-byte aligned offsets, as the addon lays them out)."""
         carry = Carry(blob_remaining, 0, 0, 0, 0)
         nf, ef, ec, ed = U64(), U64(), U32(), U32()
         _chk("drp_set_key_post", self.L.drp_set_key_post(self.h, KEY_POST_HASH if key_hash else KEY_POST_OFF))
@@ -301,7 +304,21 @@ class Ctx:
             _chk("drp_decode_stage", self.L.drp_decode_stage(self.h, _p(buf), n, C.byref(carry), C.byref(nf),
                                                              C.byref(ef), C.byref(ec), C.byref(ed)))
         rows = int(nf.value) + (1 if ec.value in (ERR_CHANGE, ERR_REQUIRED) else 0)
-        o = alloc_host_outputs(rows, key_hash)
+        if block:
+            names = ["payload_off", "payload_len", "type"] + COLS32 + COLS64 + ["flags"] + (["key_hash"] if key_hash else [])
+            dt = {"payload_off": np.uint64, "payload_len": np.uint32, "type": np.uint8, "flags": np.uint8,
+                  "key_hash": np.uint64, **{k: np.uint32 for k in COLS32}, **{k: np.uint64 for k in COLS64}}
+            offs, at = [], 0
+            for k in names:
+                offs.append(at)
+                at += (rows * np.dtype(dt[k]).itemsize + 8 + 63) & ~63
+            blk = np.full(at + 64, 0xAB, np.uint8)
+            col_off = (U64 * 14)(*(offs + [~0 & 0xFFFFFFFFFFFFFFFF] * (14 - len(offs))))
+            _chk("drp_decode_fetch_block", self.L.drp_decode_fetch_block(self.h, _p(blk), at, col_off, 0, rows))
+            o = {k: blk[a:a + rows * np.dtype(dt[k]).itemsize].view(dt[k]) for k, a in zip(names, offs)}
+            pieces = 0
+        else:
+            o = alloc_host_outputs(rows, key_hash)
         bounds = np.linspace(0, rows, pieces + 1).astype(np.int64)
         for a, b in zip(bounds[:-1], bounds[1:]):
             part = {k: v[a:] for k, v in o.items()}
