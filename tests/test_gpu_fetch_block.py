@@ -54,7 +54,7 @@ def test_blob_pieces_and_carried_blob(ctx):
     from _gpu import drp_amd
     ctx.set_blob_skip(drp_amd.BLOB_SKIP_ALWAYS)
     try:
-        w = S.c3_stream(random.Random(5), 3, frames_per_unit=300, blob_len=200000)
+        w = S.c3_stream(random.Random(5), 3, frames_per_unit=300, blob_len=1 << 20)
         a = _same(ctx, w)
         assert ctx.timing().h2d_skipped > 0  # (pieces: payload offsets shifted per piece)
         # a batch that starts inside a blob: its continuation is row 0, set on the host
