@@ -1006,9 +1006,10 @@ __global__ __launch_bounds__(256) void claims_hop(DecodeParams P) {
   uint64_t ent = ~0ull, fn = 0, fc = 0;  // records of the current group of 8 segments (512 bytes)
   uint32_t gcur = 0, tcur = 0;           // current group and tile of the region
   // groups [gcur, gto) to memory (the registers, then empty groups)
+  // (the records were preset to "no frame starts here" (drp_launch_claims_walk): only groups
+  // where a frame starts are written, one or two per frame however long it is)
   auto flush_to = [&](uint32_t gto) {
-#pragma unroll 1
-    for (; gcur < gto; gcur++) {
+    if (gcur < gto && (ent != ~0ull || fn || fc)) {
       const uint64_t ix = (G.t0 + gcur / 16u) * NT + (gcur % 16u) * 8u;
       *reinterpret_cast<uint64_t *>(P.ent + ix) = ent;
       *reinterpret_cast<uint64_t *>(P.ent_n + ix) = fn;
@@ -1017,6 +1018,7 @@ __global__ __launch_bounds__(256) void claims_hop(DecodeParams P) {
       fn = 0;
       fc = 0;
     }
+    if (gcur < gto) gcur = gto;
   };
   // tiles [tcur, tto) end before pos: their claims (a dead tile's records mix two chains: identity,
   // so verification re-walks it from its exact entry; the region is not walked further)
@@ -1154,7 +1156,14 @@ extern "C" hipError_t drp_launch_claims_walk(const DecodeParams *P, uint64_t nt_
   hipLaunchKernelGGL(spec::walk_regions, dim3(1), dim3(1024), 0, st, *P);
   const uint64_t maxr = nt_max / P->walk_tpr + P->nstreams + 1;
   hipLaunchKernelGGL(spec::walk_sync, dim3((uint32_t)((maxr * spec::SY_LANES + 255) / 256)), dim3(256), 0, st, *P);
-  if (P->walk_hop) hipLaunchKernelGGL(spec::claims_hop, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
+  if (P->walk_hop) {
+    const size_t nrec = (size_t)nt_max * spec::NT;  // (one record byte per 64-byte segment)
+    hipError_t e = hipMemsetAsync(P->ent, 0xFF, nrec, st);
+    if (e == hipSuccess) e = hipMemsetAsync(P->ent_n, 0, nrec, st);
+    if (e == hipSuccess) e = hipMemsetAsync(P->ent_c, 0, nrec, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(spec::claims_hop, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
+  }
   if (P->walk_hop) return hipGetLastError();  // (2: dense batches take claims_fast, launched by the caller)
   if (P->rec) hipLaunchKernelGGL(spec::claims_walk<true>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
   else hipLaunchKernelGGL(spec::claims_walk<false>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
