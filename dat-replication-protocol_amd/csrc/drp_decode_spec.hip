@@ -1994,6 +1994,8 @@ __global__ __launch_bounds__(SCAN_BLK) void scan_top(uint64_t *bsum, uint64_t nb
   }
 }
 
+// ONE: a single block covers every tile (no reduce / top passes: its offset is 0)
+template <bool ONE>
 __global__ __launch_bounds__(SCAN_BLK) void scan_down(const uint64_t *cnt, const uint64_t *tile_prefix,
                                                        uint64_t nstreams, const uint64_t *bsum, uint64_t *base,
                                                        uint64_t cap, uint32_t *overflow) {
@@ -2006,7 +2008,7 @@ __global__ __launch_bounds__(SCAN_BLK) void scan_down(const uint64_t *cnt, const
     v += c[k];
   }
   uint64_t total;
-  uint64_t o = bsum[blockIdx.x] + block_excl_scan64(v, sw, total);
+  uint64_t o = (ONE ? 0ull : bsum[blockIdx.x]) + block_excl_scan64(v, sw, total);
   for (uint32_t k = 0; k < SCAN_PER; k++) {
     if (i0 + k < nt) {
       base[i0 + k] = o;
@@ -3335,9 +3337,14 @@ extern "C" hipError_t drp_launch_tile_scan(const uint64_t *in, const uint64_t *t
                                            uint32_t *overflow, hipStream_t st) {
   if (nt_max == 0) return hipSuccess;
   const uint32_t nb = (uint32_t)((nt_max + spec::SCAN_SPAN - 1) / spec::SCAN_SPAN);
+  if (nb == 1) {  // (small batches: one launch; a staged piece pays each launch's host cost)
+    hipLaunchKernelGGL(spec::scan_down<true>, dim3(1), dim3(spec::SCAN_BLK), 0, st, in, tile_prefix, nstreams,
+                       (const uint64_t *)tmp, out, cap, overflow);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(spec::scan_reduce, dim3(nb), dim3(spec::SCAN_BLK), 0, st, in, tile_prefix, nstreams, tmp);
   hipLaunchKernelGGL(spec::scan_top, dim3(1), dim3(spec::SCAN_BLK), 0, st, tmp, (uint64_t)nb);
-  hipLaunchKernelGGL(spec::scan_down, dim3(nb), dim3(spec::SCAN_BLK), 0, st, in, tile_prefix, nstreams,
+  hipLaunchKernelGGL(spec::scan_down<false>, dim3(nb), dim3(spec::SCAN_BLK), 0, st, in, tile_prefix, nstreams,
                      (const uint64_t *)tmp, out, cap, overflow);
   return hipGetLastError();
 }
