@@ -396,6 +396,7 @@ static void dec_run(dec_job *j) {
     free_cols(j);
     return;
   }
+  if (j->keys) j->host_copied += (double)j->nkeys; /* (the key text is a host copy too) */
   /* u64 -> JS Number, in place (varint.decode yields Numbers) */
   const int conv[] = {C_OFF, C_CH, C_FR, C_TO};
   for (size_t k = 0; k < sizeof conv / sizeof conv[0]; k++) {
