@@ -441,7 +441,7 @@ def run_c5(args, dev, rank=0, world=1, steps=None, warmup=None, cpu=True):
     # the same context right after a dense C2 batch: the claims form is chosen per launch on the
     # device (walk_sync's density sample), not from the context's previous decode
     after_c2 = None
-    if rank == 0:
+    if rank == 0 and not args.no_after_c2:
         nf2 = 10_000_000
         w2 = c2_on_device(nf2, seed=99, dev=dev)
         so2 = torch.tensor([0, w2.numel()], dtype=torch.int64, device=dev)
@@ -465,6 +465,9 @@ def run_c5(args, dev, rank=0, world=1, steps=None, warmup=None, cpu=True):
     H = int(heap.numel())
     e, d = float(np.mean(enc_ms)) / 1e3, float(np.mean(dec_ms)) / 1e3
     b_enc, b_dec = 49 * n + H + W, W + 13 * n + 49 * n
+    # the counters' HBM bytes of the encode kernels and of the decode kernels (profiles/pmc_c5.json)
+    enc_actual = kernel_traffic_from_profile("c5", n, lambda k: k.startswith("enc_"))
+    dec_actual = kernel_traffic_from_profile("c5", n, lambda k: not k.startswith("enc_"))
     gather = ("drp_index_allgather (RCCL) of the 32 B stream stats + index scan" if args.backend == "nccl" else
               "gloo all-gather of the 32 B stream stats + index scan") if dist else "no collective (1 GPU)"
     out_line = {
@@ -484,8 +487,17 @@ def run_c5(args, dev, rank=0, world=1, steps=None, warmup=None, cpu=True):
                      "bytes_model": "encode 49*C + H + W, decode W + 13*F + 49*C (rank 0)"},
         "encode": {"ms": e * 1e3, "GBps": b_enc / e / 1e9, "frac": b_enc / e / 1e9 / HBM_PEAK_GBPS},
         "decode": {"ms": d * 1e3, "GBps": b_dec / d / 1e9, "frac": b_dec / d / 1e9 / HBM_PEAK_GBPS,
+                   "frac_kind": "model: the algorithmic bytes W + 13F + 49C over the decode time; the "
+                                "claims walk one header per frame and never read the 4 KB values, so "
+                                "this is not an HBM fraction (actual_* is)",
+                   "actual_GBps": dec_actual / d / 1e9 if dec_actual else None,
+                   "actual_frac": dec_actual / d / 1e9 / HBM_PEAK_GBPS if dec_actual else None,
+                   "actual_traffic": dec_actual,
                    "exact_fallbacks": t.strict_reruns, "repair_passes": t.spec_repairs,
                    "segmented_repairs": t.seg_repairs, "after_c2": after_c2},
+        "encode_actual": {"traffic": enc_actual,
+                          "GBps": enc_actual / e / 1e9 if enc_actual else None,
+                          "frac": enc_actual / e / 1e9 / HBM_PEAK_GBPS if enc_actual else None},
     }
     if rank == 0 and world == 1 and cpu and not args.no_cpu:
         out_line["cpu_baseline"] = cpu_baseline_c5()
@@ -744,6 +756,8 @@ def main():
     ap.add_argument("--c3-units", type=int, default=947, help="C3 units (1000 C2 frames + 1 MiB blob) per step")
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-after-c2", action="store_true",
+                    help="C5: no decode-after-C2 leg (PMC passes: its C2 kernels would join C5's counters)")
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL) for runs; gloo only to rehearse "
                     "several ranks on one GPU")
     args = ap.parse_args()
@@ -849,6 +863,22 @@ def traffic_from_profile(workload, nframes):
     if d.get("code_hash") != decode_code_hash():
         return None
     return d["hbm_bytes_per_frame"] * nframes if d.get("hbm_bytes_per_frame") else None
+
+
+def kernel_traffic_from_profile(workload, nframes, select):
+    """HBM bytes per launch of the kernels `select` picks from profiles/pmc_<workload>.json's
+    per-kernel FETCH_SIZE x2 + WRITE_SIZE figures (same staleness rule as traffic_from_profile)."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("code_hash") != decode_code_hash() or not d.get("per_kernel"):
+        return None
+    b = sum(v.get("fetch_B_per_frame", 0) + v.get("write_B_per_frame", 0) for k, v in d["per_kernel"].items()
+            if select(k))
+    return b * nframes if b else None
 
 
 if __name__ == "__main__":

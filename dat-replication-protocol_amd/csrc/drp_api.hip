@@ -185,7 +185,7 @@ struct drp_ctx {
   // claims_fast below; DRP_CLAIMS=walk / fast forces one (A/B, tests)
   uint64_t walk_min = 32768;
   int claims_mode = 0;  // 0 auto, 1 walk (ring), 2 fast, 3 hop
-  int walk_rec = 1;     // the walkers' per-frame records and the record emission (DRP_WALK_REC)
+  int crec = 0;         // claims_fast's per-frame records and the record emission (DRP_CREC)
   DevBuf recbuf;
   uint64_t dirty_cap = ~0ull;
   bool stats = false;
@@ -201,6 +201,7 @@ struct drp_ctx {
   int blob_skip = DRP_BLOB_SKIP_AUTO;
   bool blob_heavy = false;     // the last host batch was mostly blob payload (AUTO: stage in pieces)
   uint64_t blob_run = 0;       // bytes from a piece's start to its blob's payload, last seen
+  uint64_t piece_span = 0;     // batch bytes one blob-skipping piece covered on average, last seen
   drp_timing timing = {};
   std::vector<uint64_t> host_tmp;
   // the staged host-batch decode: row 0 is a host-built blob continuation when nf0 == 1; GPU
@@ -278,7 +279,7 @@ int drp_open(int device, drp_ctx **out) {
   if (const char *e = getenv("DRP_CASCADE_MIN")) c->cascade_min = (uint32_t)strtoul(e, nullptr, 10);
   if (const char *e = getenv("DRP_JUMP_MIN")) c->jump_min = strtoll(e, nullptr, 10);
   if (const char *e = getenv("DRP_WALK_MIN")) c->walk_min = strtoull(e, nullptr, 10);
-  if (const char *e = getenv("DRP_WALK_REC")) c->walk_rec = atoi(e);
+  if (const char *e = getenv("DRP_CREC")) c->crec = atoi(e);
   if (const char *e = getenv("DRP_CLAIMS")) c->claims_mode = strcmp(e, "walk") == 0 ? 1 : strcmp(e, "fast") == 0 ? 2 : strcmp(e, "hop") == 0 ? 3 : 0;
   if (const char *e = getenv("DRP_DIRTY_CAP")) c->dirty_cap = strtoull(e, nullptr, 10);
   c->trace_file = getenv("DRP_TRACE_FILE");
@@ -661,15 +662,13 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     P.walk_dense = c->scratch.at<unsigned long long>(L.wdense);
     P.walk_hop = c->claims_mode == 3 ? 1u : c->claims_mode == 1 ? 0u : 2u;  // 2: by the density sample
     P.walk_tpr = drp_walk_tiles_per_region(NT, (int)P.walk_hop);
-    // per-frame records: the record emission instead of reading the wire again (DRP_WALK_REC=0:
-    // off; a record buffer that cannot be had: off)
-    const uint64_t rcap = drp_walk_rec_cap(P.walk_tpr), nreg = NT / P.walk_tpr + ns + 1;
-    if (c->walk_rec && !P.walk_hop && c->recbuf.ensure(nreg * rcap * 32)) {
-      P.rec = c->recbuf.at<uint32_t>(0);
-      P.rec_cap = rcap;
-      P.tile_rec = c->scratch.at<uint32_t>(L.trec);
-      P.tile_recok = c->scratch.at<uint8_t>(L.trok);
-    }
+  }
+  // claims_fast's per-frame records (fast_records, 24 B per frame slot): emit_lean expands them into
+  // columns without reading the wire again (DRP_CREC=0: off; a buffer that cannot be had: off)
+  if (c->crec && c->recbuf.ensure(NT * drp_spec_rec_words() * 4ull)) {
+    P.rec = c->recbuf.at<uint32_t>(0);
+    P.tile_rec = c->scratch.at<uint32_t>(L.trec);
+    P.tile_recok = c->scratch.at<uint8_t>(L.trok);
   }
   unsigned long long *dstats = c->stats ? c->dstats : nullptr;
   if (dstats) P.stats = dstats;
@@ -1015,6 +1014,14 @@ static int decode_batch_device_out(drp_ctx *c, const uint8_t *bytes, uint64_t n,
 constexpr uint64_t kPieceMin = 64 << 10;     // bytes of a blob-skipping piece, at least
 constexpr uint64_t kPieceMargin = 64 << 10;  // past the predicted next blob header
 constexpr uint64_t kPiecesMin = 1 << 20;     // batches below this are staged whole
+// A piece costs ~150 us of host time (its launch sequence and two waits) however small it is, and
+// a flat batch (one buffer the DMA engine reads directly) stages at the full PCIe rate, so when the
+// blobs are dense (C3: a 1 MiB blob per 86 KB of Changes, ~950 pieces per GiB: 132 ms) the rest of
+// a flat batch goes in one more piece as soon as more than kPieceBudget pieces are still expected
+// (~20 ms per GiB by DMA). Chunked batches keep their pieces: staging them whole would copy every
+// blob payload on the host into the pinned gather buffer.
+constexpr uint64_t kPieceBudget = 8;
+constexpr uint64_t kPieceProbe = 4;  // pieces of a batch before its own span is trusted
 
 // The staged rows' capacity for m bytes: from the density of the ctx's previous batch (a
 // stream's batches are alike), 1/32 per byte at first.
@@ -1089,6 +1096,8 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
   // the next piece: kPieceMargin past where the last blob seen suggests the next blob header is;
   // doubled within this batch after each piece that met no blob
   uint64_t want = std::max(kPieceMin, c->blob_run + kPieceMargin);
+  const uint64_t pos0 = pos;
+  uint64_t npieces = 0, span_now = 0;  // (span_now: batch bytes per piece so far)
   float h2d_ms = 0;
   drp_timing sum = {};
   // (per piece, one wait for the decode's verification and one for its result: the H2D, the
@@ -1099,7 +1108,12 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
   } hr;
   drp_stream_result &r = hr.r;
   for (;;) {
+    if (H.flat && c->blob_skip == DRP_BLOB_SKIP_AUTO) {  // dense blobs in a flat batch: the rest in one piece
+      const uint64_t span = npieces >= kPieceProbe ? span_now : c->piece_span;
+      if (span && (n - pos) / span > kPieceBudget) want = n - pos;
+    }
     const uint64_t pe = std::min(n, pos + want), ps = pos & ~15ull, mp = pe - ps;
+    npieces++;
     if (!c->in_stage.ensure(mp + 64)) return DRP_E_NOMEM;
     CHK(hipEventRecord(c->hev[0], st));
     if (const int rc = h2d_range(c, H, ps, mp, c->in_stage.p, st, &copied)) return rc;
@@ -1167,6 +1181,7 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
         CHK(hipMemsetAsync(S.fr.type + rows - 1, DRP_TYPE_BLOB, 1, st));
         skipped += bend - pe;
         pos = bend;
+        span_now = (pos - pos0) / npieces;
         if (pos == n) {
           carry->blob_remaining = 0;
           carry->consumed = n;
@@ -1185,9 +1200,11 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
       const uint64_t np = r.tail_kind == DRP_TAIL_NONE ? pe : ps + r.consumed;
       want *= 2;
       if (np > pos) pos = np;
+      span_now = (pos - pos0) / npieces;
     }
   }
   c->timing = sum;
+  if (span_now) c->piece_span = span_now;
   c->timing.h2d_ms = h2d_ms;
   c->timing.h2d_bytes = staged;
   c->timing.h2d_skipped = skipped;

@@ -1186,6 +1186,183 @@ __device__ __forceinline__ uint32_t fast_claims_jump(const DecodeParams &P, uint
   return FC_OK;
 }
 
+// ---- per-frame records: the wire is read once (C2) ------------------------------------------------
+// claims_fast already holds each thread's chain, so after the claim it decodes the Change fields of
+// every frame its threads deliver (the exact frames of the tile from verification's entry thread on,
+// plus the shadow frames of the threads before it) into CR_WORDS words per frame, and emit_lean
+// expands the records of the tiles verification lets it (tile_recok) into columns without staging
+// the tile again (decode.js:144-169 / 205-214 deliver the same frames in the same order). Per tile,
+// CR_CAP slots in slot order = chain order (the threads' frame counts, prefix-summed), word-major so
+// each word of a wave's frames is one coalesced store:
+//   w0  payload offset from the tile's first byte (14 bits) | id << 14 | partial (a blob cut by the
+//       stream end) << 16 | has value << 17 | key length varint bytes << 18
+//   w1  payload length (the header's, as the column)
+//   w2  key length | value offset << 16 (payload-relative)
+//   w3..w5 change, from, to
+// Recorded: blob frames, and Change payloads in protocol-buffers' own shape without a subset: key
+// (length varint of <= 2 bytes) change from to [value], one-byte tags, numbers < 2^32, the last field
+// ending the payload. Anything else (a subset, longer varints, a field header near the stream end,
+// more than CR_CAP frames) leaves the tile without records (tile_rec REC_NONE): emit_lean then decodes
+// it from the wire as before, and errors are reported there. The record of a frame is only a
+// restatement of its header and fields; verification proves which frames are real.
+#ifndef DRP_CREC_STAGE
+#define DRP_CREC_STAGE 2  // (A/B builds: 0 stops after the frame list, 1 after the field decode)
+#endif
+constexpr uint32_t CR_CAP = NT, CR_WORDS = 6, CR_TILE_WORDS = CR_CAP * CR_WORDS;
+static_assert(CR_CAP == NT, "one frame per thread in the record decode");
+
+// one frame's fields from the 28 bytes at payload-relative ke (numbers of any width up to 5 bytes,
+// value length up to 4 bytes): false when the payload is in another shape
+__device__ __forceinline__ bool crec_general(const uint32_t *w32, uint32_t qa, uint32_t ke, uint32_t pl,
+                                             uint32_t &num0, uint32_t &num1, uint32_t &num2, uint32_t &vo, bool &hv) {
+  const uint32_t d = qa >> 2, sh = (qa & 3u) * 8u;
+  uint32_t a[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) a[i] = w32[d + i];
+  uint64_t x[4];  // bytes qa .. qa + 27 (x[3]: 4 bytes)
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+    x[i] = (uint64_t)__builtin_amdgcn_alignbit(a[2 * i + 1], a[2 * i], sh) |
+           ((uint64_t)__builtin_amdgcn_alignbit(a[2 * i + 2], a[2 * i + 1], sh) << 32);
+  x[3] = __builtin_amdgcn_alignbit(a[7], a[6], sh);
+  uint32_t used = 0, nums[3];
+#pragma unroll
+  for (int f = 0; f < 3; f++) {
+    const uint32_t b0 = (uint32_t)x[0] & 0xFFu;
+    const uint64_t y = x[0] >> 8;
+    const uint64_t tm = ~y & 0x8080808080ull;
+    if (b0 != 0x18u + 8u * (uint32_t)f || !tm) return false;
+    const uint32_t k2 = ((uint32_t)__builtin_ctzll(tm) >> 3) + 1u;
+    const uint64_t v = ((y & 0x7Full) | ((y >> 1) & 0x3F80ull) | ((y >> 2) & 0x1FC000ull) | ((y >> 3) & 0xFE00000ull) |
+                        ((y >> 4) & 0x7F0000000ull)) & ((1ull << (7u * k2)) - 1ull);
+    if (v >> 32) return false;
+    nums[f] = (uint32_t)v;
+    const uint32_t s = 1u + k2, b = 8u * s;  // (2..6 bytes)
+    used += s;
+    x[0] = (x[0] >> b) | (x[1] << (64u - b));
+    x[1] = (x[1] >> b) | (x[2] << (64u - b));
+    x[2] = (x[2] >> b) | (x[3] << (64u - b));
+    x[3] >>= b;
+  }
+  num0 = nums[0];
+  num1 = nums[1];
+  num2 = nums[2];
+  if (ke + used > pl) return false;
+  hv = ke + used != pl;
+  vo = 0;
+  if (!hv) return true;
+  const uint32_t b0 = (uint32_t)x[0] & 0xFFu;
+  const uint64_t y = x[0] >> 8;
+  const uint64_t tm = ~y & 0x80808080ull;
+  if (b0 != 0x32u || !tm) return false;
+  const uint32_t k2 = ((uint32_t)__builtin_ctzll(tm) >> 3) + 1u;
+  const uint64_t v = ((y & 0x7Full) | ((y >> 1) & 0x3F80ull) | ((y >> 2) & 0x1FC000ull) | ((y >> 3) & 0xFE00000ull)) &
+                     ((1ull << (7u * k2)) - 1ull);
+  vo = ke + used + 1u + k2;
+  return vo <= pl && v == (uint64_t)(pl - vo) && vo < 0x10000u;
+}
+
+// Records of the tile's delivered frames (after the claim; whole workgroup). E / nf: this thread's
+// settled entry and frame count (0 for a non-carrier), exactly as its per-thread record has them.
+__device__ __forceinline__ void fast_records(const DecodeParams &P, uint64_t t, FastLds &S, uint32_t E, uint32_t nf,
+                                             uint32_t s1r, uint32_t se_rel, const uint32_t *w32) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  uint16_t *fls = reinterpret_cast<uint16_t *>(S.lal);  // (free after the survival rounds)
+  const uint32_t ip = wave_scan_dpp(nf);
+  if (lane == 63) S.xw[4 + wid] = ip;
+  bsync();
+  const uint32_t tot = NT == 2 * WAVE ? S.xw[4] + S.xw[5] : S.xw[4];
+  if (tot > CR_CAP) return;  // (uniform: tile_rec stays REC_NONE)
+  uint32_t bad = 0;
+  if (nf) {  // this thread's frames in chain order, as fwalk counts them
+    uint32_t slot = ip - nf + (wid ? S.xw[4] : 0u), cnt = 0, i = E & 0xFFFFu;
+#pragma unroll 1
+    for (uint32_t g = 0; g < 64u; g++) {
+      const uint32_t nd = S.lnd[i], id = nd >> 30, c = nd & 0xFFFFu, q = (nd >> 16) & 0x3FFFu;
+      if (id == 3u || c == NX_TAILC) break;
+      if (id != 0u) {
+        if (cnt < nf) fls[slot + cnt] = (uint16_t)i;
+        cnt++;
+      }
+      if (c >= NX_TAILB || q >= s1r) break;  // (NX_TAILB, NX_TAILC, NX_NEAR, NX_FAR, NX_DEAD)
+      i = c;
+    }
+    bad = cnt != nf;
+  }
+  bsync();
+  if (DRP_CREC_STAGE == 0) return;
+  if (tid < tot && !bad) {
+    uint32_t *rr = P.rec + t * CR_TILE_WORDS + tid;
+    const uint32_t i = fls[tid];
+    const uint32_t nd = S.lnd[i], c = nd & 0xFFFFu, id = nd >> 30;
+    const uint32_t o = S.lpos[i];
+    const uint32_t d = o >> 2, sh = (o & 3u) * 8u;
+    const uint32_t a0 = w32[d], a1 = w32[d + 1], a2 = w32[d + 2];
+    const uint32_t w = __builtin_amdgcn_alignbit(a1, a0, sh), wn = __builtin_amdgcn_alignbit(a2, a1, sh);
+    const uint32_t k = ((uint32_t)__builtin_ctz((~w & 0x808080u) | 0x80000000u) >> 3) + 1u;
+    const uint32_t L = ((w & 0x7Fu) | ((w >> 1) & 0x3F80u) | ((w >> 2) & 0x1FC000u)) & ((1u << (7u * k)) - 1u);
+    const uint32_t po = o + k + 1u, pl = L - 1u;
+    uint32_t w0 = po | (id << 14) | ((c == NX_TAILB ? 1u : 0u) << 16);
+    if (id == 1u) {
+      const uint64_t x = (((uint64_t)wn << 32) | w) >> (8u * (k + 1u));  // payload bytes 0 .. 6 - k
+      const uint32_t b1 = (uint32_t)(x >> 8) & 0xFFu, b2 = (uint32_t)(x >> 16) & 0xFFu;
+      const uint32_t kb = b1 < 0x80u ? 1u : (b2 < 0x80u ? 2u : 0u);
+      const uint32_t klen = kb == 1u ? b1 : (b1 & 0x7Fu) | (b2 << 7);
+      const uint32_t ke = 1u + kb + klen;  // the key's end, payload-relative
+      uint32_t n0 = 0, n1 = 0, n2 = 0, vo = 0;
+      bool hv = false, ok = ((uint32_t)x & 0xFFu) == 0x12u && kb && ke + 6u <= pl;
+      const uint32_t qa = po + ke;
+      ok = ok && qa + 36u <= se_rel;  // (the general form's 8 dwords from qa & ~3)
+      if (ok) {
+        const uint32_t e = qa >> 2, s2 = (qa & 3u) * 8u;
+        const uint32_t c0 = w32[e], c1 = w32[e + 1], c2 = w32[e + 2], c3 = w32[e + 3];
+        const uint64_t y = (uint64_t)__builtin_amdgcn_alignbit(c1, c0, s2) |
+                           ((uint64_t)__builtin_amdgcn_alignbit(c2, c1, s2) << 32);
+        const uint32_t y8 = __builtin_amdgcn_alignbit(c3, c2, s2) & 0xFFu;
+        // one-byte change / from / to: 18 a 20 b 28 c, then [32 d (d1)] or the payload's end
+        const bool one = (y & 0xFFull) == 0x18u && ((y >> 16) & 0xFFull) == 0x20u && ((y >> 32) & 0xFFull) == 0x28u &&
+                         (y & 0x0000800080008000ull) == 0;
+        if (one) {
+          n0 = (uint32_t)(y >> 8) & 0xFFu;
+          n1 = (uint32_t)(y >> 24) & 0xFFu;
+          n2 = (uint32_t)(y >> 40) & 0xFFu;
+          if (ke + 6u == pl) {
+            hv = false;
+          } else {
+            const uint32_t d0 = (uint32_t)(y >> 56), vh = d0 < 0x80u ? 2u : (y8 < 0x80u ? 3u : 0u);
+            const uint32_t vl = vh == 2u ? d0 : (d0 & 0x7Fu) | (y8 << 7);
+            vo = ke + 6u + vh;
+            hv = true;
+            ok = ((uint32_t)(y >> 48) & 0xFFu) == 0x32u && vh && vo <= pl && vl == pl - vo && vo < 0x10000u;
+          }
+        } else {
+          ok = crec_general(w32, qa, ke, pl, n0, n1, n2, vo, hv);
+        }
+      }
+      if (DRP_CREC_STAGE == 1) {  // (A/B: keep the decode, store nothing)
+        if ((n0 ^ n1 ^ n2 ^ vo ^ klen) == 0x7FFFFFFFu && ok) rr[0] = w0;
+        ok = false;
+      }
+      if (ok) {
+        w0 |= ((hv ? 1u : 0u) << 17) | (kb << 18);
+        rr[2 * CR_CAP] = klen | (vo << 16);
+        rr[3 * CR_CAP] = n0;
+        rr[4 * CR_CAP] = n1;
+        rr[5 * CR_CAP] = n2;
+      }
+      bad = !ok;
+    }
+    if (DRP_CREC_STAGE >= 2) {
+      rr[0] = w0;
+      rr[CR_CAP] = pl;
+    }
+  }
+  const uint64_t bm = __ballot(bad);
+  if (lane == 0) S.xw[6 + wid] = bm != 0;
+  bsync();
+  if (tid == 0) P.tile_rec[t] = (NT == 2 * WAVE ? S.xw[6] | S.xw[7] : S.xw[6]) ? REC_NONE : 0u;
+}
+
 // bits of the 64 positions from base (tile-relative) that lie in [lo, hi)
 __device__ __forceinline__ uint64_t range_bits(uint32_t base, uint32_t lo, uint32_t hi) {
   const uint32_t a = lo > base ? min(lo - base, 64u) : 0u, z = hi > base ? min(hi - base, 64u) : 0u;
@@ -1591,6 +1768,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     P.claim[t] = cl;
     cl_o = cl;
   }
+  if (!EDGE && P.rec) fast_records(P, t, S, E, en_o, s1r, se_rel, w32);
   return FC_OK;
 }
 
@@ -1709,10 +1887,11 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
     if (lst) P.vlist[base + (uint32_t)__builtin_popcountll(lm & ((1ull << lane) - 1ull))] = (uint32_t)t;
   }
   if (r != 0 || lst) return;
-  // the record emission takes the tile when the claims kernel recorded every frame of it and its
-  // first record is the frame at e_t (no recorded frame in the threads before e_t's)
-  const bool recok = P.tile_recok && inside && sb == 0 && P.tile_rec[t] != REC_NONE;
-  if (P.tile_recok) P.tile_recok[t] = recok ? 1 : 0;
+  // the record emission takes the tile when the claims kernel recorded every frame its threads
+  // deliver: the tile's rows are its records from slot sb on (sb = the frames of the threads before
+  // e_t's), kept here as sb + 1
+  const bool recok = P.tile_recok && inside && sb < 255u && P.tile_rec[t] != REC_NONE;
+  if (P.tile_recok) P.tile_recok[t] = recok ? (uint8_t)(sb + 1u) : 0;
   P.tile_exit[t] = inside ? claim : et;
   P.tile_count[t] = sf;
   P.tile_nch[t] = sc;
@@ -2495,6 +2674,67 @@ __device__ __forceinline__ void st_col(T *base, uint32_t i, T v) {
   *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (uint32_t)(i * (uint32_t)sizeof(T))) = v;
 }
 
+// ---- record emission: columns from claims_fast's per-frame records (fast_records) -------------
+// The tiles verification lets it take (tile_recok = 1 + the slot of the tile's first row): rows
+// [tile_base, + tile_count) from slot tile_recok - 1 on. Reads 24 B per row and writes the columns;
+// the wire is not read again. Four tiles per workgroup in XCD-contiguous order (neighbouring
+// tiles' column lines meet in one L2); a small kernel (no LDS, few registers) so that many tiles'
+// loads are in flight per CU.
+constexpr uint32_t ER_WAVES = 4, ER_RPL = CR_CAP / WAVE;  // tiles (waves) per workgroup, rows per lane
+static_assert(CR_CAP % WAVE == 0, "a lane's rows are slots lane, lane + 64, ...");
+__device__ __forceinline__ void emit_rec_row(const RowCols &C, uint64_t A, uint32_t s, uint32_t w0, uint32_t pl,
+                                             uint32_t w2, uint32_t n0, uint32_t n1, uint32_t n2) {
+  const uint32_t id = (w0 >> 14) & 3u;
+  st_col(C.poff, s, A + (w0 & 0x3FFFu));
+  st_col(C.plen, s, pl);
+  st_col(C.type, s, (uint8_t)(id | (((w0 >> 16) & 1u) ? DRP_FRAME_PARTIAL : 0u)));
+  if (id != 1u) return;
+  const uint32_t hv = (w0 >> 17) & 1u, vo = hv ? w2 >> 16 : 0u;
+  st_col(C.ko, s, 1u + ((w0 >> 18) & 3u));
+  st_col(C.kl, s, w2 & 0xFFFFu);
+  st_col(C.so, s, 0u);
+  st_col(C.sl, s, 0u);
+  st_col(C.vo, s, vo);
+  st_col(C.vl, s, hv ? pl - vo : 0u);
+  st_col(C.ch, s, (uint64_t)n0);
+  st_col(C.fr, s, (uint64_t)n1);
+  st_col(C.to, s, (uint64_t)n2);
+  st_col(C.fl, s, (uint8_t)(hv ? DRP_F_VALUE : 0u));
+}
+// A wave per tile (its meta by scalar loads), every record word of the lane's rows loaded before
+// any column is stored.
+__global__ __launch_bounds__(ER_WAVES * WAVE) void emit_recs(DecodeParams P) {
+  if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
+  uint64_t b;
+  {
+    const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = blockIdx.x % 8u;
+    b = (uint64_t)x * q + min(x, r) + blockIdx.x / 8u;
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t t = b * ER_WAVES + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (t >= ldc(P.tile_prefix + P.nstreams)) return;  // (whole wave)
+  const uint32_t rk = ldc(P.tile_recok + t);
+  if (!rk) return;
+  const uint32_t n = (uint32_t)ldc(P.tile_count + t);
+  const uint64_t base = ldc(P.tile_base + t);
+  const RowCols C = row_cols(P, base);
+  const uint32_t lim = min(n, C.lim);
+  const uint32_t *rr = P.rec + t * CR_TILE_WORDS + (rk - 1u);
+  uint32_t w[ER_RPL][CR_WORDS];
+#pragma unroll
+  for (uint32_t j = 0; j < ER_RPL; j++) {
+    const uint32_t s = lane + j * WAVE;
+#pragma unroll
+    for (uint32_t k = 0; k < CR_WORDS; k++) w[j][k] = s < lim ? rr[k * CR_CAP + s] : 0u;
+  }
+  const uint64_t A = tile_geo(P, t).A;
+#pragma unroll
+  for (uint32_t j = 0; j < ER_RPL; j++) {
+    const uint32_t s = lane + j * WAVE;
+    if (s < lim) emit_rec_row(C, A, s, w[j][0], w[j][1], w[j][2], w[j][3], w[j][4], w[j][5]);
+  }
+}
+
 struct LeanLds {
   __attribute__((aligned(16))) uint8_t buf[IMG + 32];
   uint32_t wsum[NT / WAVE];
@@ -2504,7 +2744,8 @@ struct LeanLds {
 __device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t, LeanLds &L);
 
 // Long-frame streams (the context's change_checks form: >= 512 B per frame) leave nearly every
-// tile to emit_sparse, so a workgroup per tile would mostly be dispatched to exit: there each
+// tile to emit_sparse, and with per-frame records nearly every tile goes to emit_recs, so a
+// workgroup per tile would mostly be dispatched to exit: there each
 // workgroup takes EMIT_LONG_TPW tiles, strided by the grid (drp_launch_spec_tail sizes it), reads
 // their sparse marks in one load (a lane each) and runs only the others (8 tiles with a load each
 // in turn: C5's emit_lean took 0.116 ms of dependent mark loads).
@@ -2513,12 +2754,13 @@ static_assert(EMIT_LONG_TPW <= WAVE, "one lane per tile's mark");
 __global__ __launch_bounds__(NT, DRP_EMIT_LEAN_WAVES) void emit_lean(DecodeParams P) {
   __shared__ LeanLds L;
   if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
-  if (P.change_checks) {
+  if (P.change_checks || P.rec) {
     const uint64_t ntiles = P.tile_prefix[P.nstreams];
     const uint32_t tid = threadIdx.x;
     if (tid < WAVE) {
       const uint64_t t = blockIdx.x + (uint64_t)tid * gridDim.x;
-      const bool run = tid < EMIT_LONG_TPW && t < ntiles && !(P.tile_sparse && P.tile_sparse[t]);
+      const bool run = tid < EMIT_LONG_TPW && t < ntiles && !(P.tile_sparse && P.tile_sparse[t]) &&
+                       !(P.tile_recok && P.tile_recok[t]);
       const uint64_t m = __ballot(run);
       if (tid == 0) L.todo = m;
     }
@@ -2551,14 +2793,14 @@ __device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t
   // array covers the grid, and a stale mark past the tile count only ends a tile that ends anyway),
   // or the record emission writes it
   if (P.tile_sparse && P.tile_sparse[t]) return;
-  if (P.tile_recok && t < P.tile_prefix[P.nstreams] && P.tile_recok[t]) return;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   const TileGeo G = tile_geo(P, t);
   if (t >= ntiles) return;  // (whole workgroup)
   const uint64_t A = G.A;
+  const uint64_t base = ldc(P.tile_base + t);
+  const RowCols C = row_cols(P, base);
   const uint32_t se_rel = (uint32_t)umin64(G.se - A, 0x7FFFFFFFull);
   const uint32_t lim = se_rel < IMG ? se_rel : IMG;  // image bytes of the stream
-  const uint64_t base = ldc(P.tile_base + t);
   const uint32_t k0 = P.tile_k ? P.tile_k[t] : 0u;
   const uint8_t eb = tid < k0 ? (uint8_t)0xFF : P.ent[t * NT + tid];  // exact entry of this thread's bytes
   const uint8_t en = P.ent_n[t * NT + tid];                            // frames from it
@@ -2572,7 +2814,6 @@ __device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t
 #pragma unroll
   for (uint32_t w = 0; w < NT / WAVE; w++)
     if (w < wid) i += wsum[w];
-  const RowCols C = row_cols(P, base);
   bool ok = true;
   if (n) {
     uint32_t o = tid * SEGB + (eb & 63u);
@@ -3360,6 +3601,7 @@ extern "C" hipError_t drp_launch_stream_counts(const uint64_t *tile_prefix, uint
 }
 
 extern "C" uint32_t drp_spec_tile_bytes(void) { return spec::TILE; }
+extern "C" uint32_t drp_spec_rec_words(void) { return spec::CR_TILE_WORDS; }  // (per tile: fast_records)
 extern "C" uint32_t drp_spec_retry_mask(void) { return spec::F_MISS | spec::F_WAIT; }
 
 extern "C" uint32_t drp_spec_miss_bit(void) { return spec::F_MISS; }
@@ -3494,12 +3736,13 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
     } else {
       Q.tile_sparse = nullptr;
     }
+    if (Q.rec)  // (the tiles with records; emit_lean skips them)
+      hipLaunchKernelGGL(spec::emit_recs, dim3((uint32_t)((nt_max + spec::ER_WAVES - 1) / spec::ER_WAVES)),
+                         dim3(spec::ER_WAVES * WAVE), 0, st, Q);
     hipLaunchKernelGGL(spec::emit_lean,
-                       dim3((uint32_t)(Q.change_checks ? (nt_max + spec::EMIT_LONG_TPW - 1) / spec::EMIT_LONG_TPW
-                                                       : nt_max)),
+                       dim3((uint32_t)(Q.change_checks || Q.rec ? (nt_max + spec::EMIT_LONG_TPW - 1) / spec::EMIT_LONG_TPW
+                                                                : nt_max)),
                        dim3(spec::NT), 0, st, Q);
-    e = drp_launch_emit_rec(&Q, nt_max, st);  // (the tiles with records; emit_lean skipped them)
-    if (e != hipSuccess) return e;
     drp_dbg_mark("emit_fast", st);
     hipLaunchKernelGGL(spec::emit_tiles, dim3((uint32_t)(nt_max < 16384 ? nt_max : 16384)), dim3(spec::NT), 0,
                        st, Q);

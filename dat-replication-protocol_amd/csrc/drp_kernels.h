@@ -126,6 +126,7 @@ hipError_t drp_launch_tile_prefix(uint32_t B, const uint64_t *stream_off, uint64
 hipError_t drp_launch_decode(uint32_t B, const drp::DecodeParams *P, uint32_t grid, hipStream_t st);
 uint32_t drp_decode_waves_per_group(void);  // tiles (waves) per workgroup; grid counts groups
 uint32_t drp_spec_tile_bytes(void);
+uint32_t drp_spec_rec_words(void);  // u32 record words per tile (claims_fast's per-frame records)
 uint32_t drp_spec_retry_mask(void);
 uint32_t drp_spec_miss_bit(void);
 uint32_t drp_spec_cascade_bit(void);

@@ -286,6 +286,7 @@ static void free_cols(dec_job *j) {
 static void free_job(dec_job *j) {
   free_cols(j);
   if (j->chunks != &j->one) free(j->chunks);
+  if (j->st) env_unref(j->st); /* (the job's reference: dec_args) */
   free(j);
 }
 
@@ -570,6 +571,12 @@ static dec_job *dec_args(napi_env env, napi_callback_info info, size_t want, nap
     return NULL;
   }
   j->st = env_get(env);
+  if (j->st) { /* the worker thread uses it (col_get): held until free_job, so a torn-down
+                  environment (a terminated worker_thread) cannot free it under the job */
+    pthread_mutex_lock(&j->st->mu);
+    j->st->refs++;
+    pthread_mutex_unlock(&j->st->mu);
+  }
   j->carry.blob_remaining = (uint64_t)brem;
   if (argc > want) {
     bool kp = false;

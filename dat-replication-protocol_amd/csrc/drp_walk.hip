@@ -1165,8 +1165,7 @@ extern "C" hipError_t drp_launch_claims_walk(const DecodeParams *P, uint64_t nt_
     hipLaunchKernelGGL(spec::claims_hop, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
   }
   if (P->walk_hop) return hipGetLastError();  // (2: dense batches take claims_fast, launched by the caller)
-  if (P->rec) hipLaunchKernelGGL(spec::claims_walk<true>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
-  else hipLaunchKernelGGL(spec::claims_walk<false>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
+  hipLaunchKernelGGL(spec::claims_walk<false>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
   return hipGetLastError();
 }
 

@@ -2,7 +2,7 @@
 // mafintosh/dat-replication-protocol v4.1.2) over the gfx950 batch codec.
 //
 // Writes reach _write one at a time, as in the reference; the ones buffered behind the write
-// being consumed (the stream's highWaterMark is MAX_BATCH) are read ahead: up to PIECE bytes of
+// being consumed (the stream's highWaterMark is MAX_BATCH unless opts.highWaterMark says otherwise) are read ahead: up to PIECE bytes of
 // them form a batch, decoded on the GPU in one call on a worker thread (frame split + Change
 // decode, libdrp via lib/drp.node, the written chunks handed over as they are: libdrp gathers
 // the ranges it stages, so nothing is concatenated here). While one batch is replayed the next
@@ -10,7 +10,7 @@
 // the write holding its last byte is consumed, a change/blob callback increments _pending and
 // delivery stops while _pending > 0 (decode.js:89-99, 144-169), and a write's callback fires
 // once every frame it completes has been delivered and acknowledged (decode.js:167-168), so
-// producers see the reference's backpressure and the callbacks interleave as they do there.
+// the callbacks interleave as they do there (write()'s return value: opts.highWaterMark below).
 //
 // Carry across batches (decode.js:75-81): an incomplete header (<= 10 bytes) is prepended to
 // the next batch; an incomplete Change frame is collected once into a buffer of its declared
@@ -92,9 +92,16 @@ var NOTHING = { n: 0, errCode: 0, tailKind: 0, consumed: 0, blobRemaining: 0, fr
 //                    a BigInt, computed on the GPU (drp_keys.hip)
 //   device: k      - the GPU this stream decodes on (default: DRP_DEVICE or 0); independent
 //                    streams are spread over a node's GPUs this way (index.js: shard)
+//   highWaterMark  - the Writable's highWaterMark. Default MAX_BATCH (64 MiB), a deliberate
+//                    divergence from the reference (Node's default, 16 KiB): a producer that
+//                    honours write()'s return value stops at the highWaterMark, and the writes
+//                    buffered behind the one being consumed are all a GPU batch can read ahead.
+//                    16384 restores the reference's write()/'drain' signal (batches then hold
+//                    ~one write each; INTEGRATION.md)
 function Decoder (opts) {
   if (!(this instanceof Decoder)) return new Decoder(opts)
-  stream.Writable.call(this, { highWaterMark: MAX_BATCH })
+  var hwm = opts && opts.highWaterMark !== undefined ? opts.highWaterMark : MAX_BATCH
+  stream.Writable.call(this, { highWaterMark: hwm })
   this._keyPost = !!(opts && opts.keyHash)
 
   this.destroyed = false
@@ -166,9 +173,10 @@ Decoder.prototype.finalize = function (fn) { this._onfinalize = fn }
 
 Decoder.prototype._write = function (data, enc, cb) {
   var q = this._q
-  while (this._qh < q.length && q[this._qh] !== data) this._qh++ // (chunks the stream refused)
-  if (this._qh < q.length) this._qh++
-  if (this._qh > 4096 && this._qh * 2 > q.length) {
+  // (taken slots are cleared at once: the queue must not keep consumed writes alive)
+  while (this._qh < q.length && q[this._qh] !== data) q[this._qh++] = undefined // (chunks the stream refused)
+  if (this._qh < q.length) q[this._qh++] = undefined
+  if (this._qh >= 64 && this._qh * 2 > q.length) {
     this._q = q.slice(this._qh)
     this._qh = 0
   }

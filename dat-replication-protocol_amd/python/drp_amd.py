@@ -12,6 +12,8 @@ import numpy as np
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("DRP_LIB") or os.path.join(PKG, "lib", "libdrp.so")
+if not os.path.isabs(LIB_PATH):  # (an A/B build named relative to the repo root: exp/<name>/libdrp.so)
+    LIB_PATH = os.path.join(os.path.dirname(PKG), LIB_PATH)
 
 DRP_OK, DRP_E_INVAL, DRP_E_HIP, DRP_E_NOMEM, DRP_E_CAPACITY, DRP_E_NODEV = 0, -1, -2, -3, -4, -5
 TYPE_CHANGE, TYPE_BLOB, FRAME_CONT, FRAME_PARTIAL = 1, 2, 0x40, 0x80

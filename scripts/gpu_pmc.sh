@@ -11,7 +11,7 @@ mkdir -p $D
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d $D/$name -o run -- \
-    python3 -u bench.py --frames $F --workload $W --steps 1 --warmup 1 --no-cpu --no-sub > $D/$name.log 2>&1
+    python3 -u bench.py --frames $F --workload $W --steps 1 --warmup 1 --no-cpu --no-sub --no-after-c2 > $D/$name.log 2>&1
 }
 run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH
 run sq2 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_FLAT

@@ -9,10 +9,11 @@
 #   bench          the default bench line (C2 + c4/c5 sub-lines + CPU legs + Node path)
 #   quick          the default bench line without CPU legs and the Node path
 #   prof           rocprofv3 --kernel-trace --stats of a quick C2 + C4 + C5 run (no CPU legs)
-#   prof:<w>       the same for workload w's line alone (c2, c4, c5: its kernels' averages are per launch)
+#   prof:<w>[:tag] the same for workload w's line alone (c2, c4, c5: its kernels' averages are per launch)
 #   pmc:<w>        FETCH_SIZE / WRITE_SIZE / SQ passes of workload w (c2, c4, c5) (scripts/gpu_pmc.sh)
 #   ab:<variant>   quick C2 + C5 lines with exp/<variant>/libdrp.so (scripts/build_variant.sh)
 #   probe:<script> python3 scripts/<script> (a measurement script)
+#   bin:<path>     a prebuilt measurement binary (e.g. exp/probe_bw from scripts/probe_bw.hip)
 #   pack           summarise this session's prof / pmc outputs (kernel_phases.txt, pmc_<w>.json) and
 #                  delete their per-dispatch CSVs (gpurun copies back at most 64 MiB)
 #   env:K=V        export K=V for the steps that follow (unenv:K unsets it)
@@ -56,9 +57,11 @@ for step in "$@"; do
       ;;
     prof:*)
       W=${step#prof:}
-      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/prof_$W -o run -- \
-        python3 -u $ROOT/bench.py --workload $W --steps 10 --warmup 2 --no-cpu --no-sub > $ROOT/$OUT/bench_prof_$W.log 2>&1)
-      echo "prof $W done"
+      T=${W#*:}
+      [ "$T" = "$W" ] && T="" || W=${W%%:*}
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/prof_$W$T -o run -- \
+        python3 -u $ROOT/bench.py --workload $W --steps 10 --warmup 2 --no-cpu --no-sub > $ROOT/$OUT/bench_prof_$W$T.log 2>&1)
+      echo "prof $W$T done: $(python3 scripts/kstats.py $OUT/prof_$W$T/run_kernel_stats.csv 3 | tr -s ' ' | tr '\n' ';')"
       ;;
     pmc:*)
       W=${step#pmc:}
@@ -76,6 +79,11 @@ for step in "$@"; do
       S=${step#probe:}
       timeout -k 10 400 python3 -u scripts/$S > $OUT/probe_${S%%.*}.log 2>&1
       echo "probe $S done"
+      ;;
+    bin:*)
+      B=${step#bin:}
+      timeout -k 10 300 ./$B > $OUT/bin_$(basename $B).log 2>&1
+      echo "bin $B: $(tr '\n' ';' < $OUT/bin_$(basename $B).log | cut -c1-600)"
       ;;
     pack)
       for d in $OUT/pmc_*/; do

@@ -47,10 +47,27 @@ CASES = [("burst_100", 1, 300, [100], "burst"), ("burst_mixed", 2, 400, [100, 17
          ("paced_big", 5, 300, [2048, 700], "paced")]
 
 
+def error_cases():
+    """Protocol errors whose header straddles two writes: the reference raises
+    'unknown type' in the write that holds the type byte (decode.js:144-169, 251-262), after the
+    write before it has been acknowledged. A 2-byte length varint split after its first byte, and
+    the type byte alone at the start of the next write; plus the same header inside one write."""
+    prefix = wire_for(6, 30)
+    bad = bytes([0xC8, 0x01, 0x07]) + b"junk" * 5
+    wire = prefix + bad
+    P = len(prefix)
+    out = []
+    for name, sizes in [("err_split_varint", [P + 1, 100]), ("err_split_type", [P + 2, 100]),
+                        ("err_one_write", [P + 3, 100]), ("err_small_writes", [97, 13])]:
+        for pattern in ("burst", "paced"):
+            out.append((name + "_" + pattern, wire, sizes, pattern))
+    return out
+
+
 def main():
     cases = []
-    for name, seed, n, sizes, pattern in CASES:
-        wire = wire_for(seed, n)
+    todo = [(name, wire_for(seed, n), sizes, pattern) for name, seed, n, sizes, pattern in CASES] + error_cases()
+    for name, wire, sizes, pattern in todo:
         with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
             f.write(wire)
             path = f.name

@@ -33,6 +33,14 @@ def test_library_exports_every_declared_symbol():
     assert set(declared()) <= exported
 
 
+def test_library_exports_nothing_else():
+    """The dynamic symbol table is the header's ABI and nothing more (csrc/libdrp.map): no kernel
+    host stubs, no C++ internals."""
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB], text=True)
+    exported = {l.split()[-1] for l in out.splitlines() if l.strip()}
+    assert exported == set(declared()), sorted(exported ^ set(declared()))
+
+
 def test_binding_matches_header():
     import sys
     sys.path.insert(0, os.path.join(ROOT, "dat-replication-protocol_amd", "python"))

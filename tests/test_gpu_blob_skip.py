@@ -61,8 +61,10 @@ def _check(got, ref):
 @pytest.mark.parametrize("mode", ["always", "auto"])
 def test_c3_blob_payloads_skip_hbm(ctx, mode):
     """C3-shaped stream (1000 C2 frames + one 1 MiB blob per unit, ~113 MB) in ragged host
-    batches of 4-17 MiB: every frame equals the oracle's, and at most 25% of the wire is staged
-    into HBM (the blobs' payloads stay in host memory)."""
+    batches of 4-17 MiB: every frame equals the oracle's. ALWAYS: at most 25% of the wire is
+    staged into HBM (the blobs' payloads stay in host memory). AUTO on flat batches: the blobs
+    are too dense for pieces (~150 us of host time each against ~20 us to DMA a 1 MiB blob), so
+    after a few probe pieces the rest of each batch is staged whole (drp_api.hip kPieceBudget)."""
     from _gpu import drp_amd
     wire = S.c3_stream(random.Random(5), 100, frames_per_unit=1000)
     ref = O.decode_batch(wire, chunk=65536, cap=100 * 1001 + 16)
@@ -74,8 +76,8 @@ def test_c3_blob_payloads_skip_hbm(ctx, mode):
     print(f"{mode}: staged {staged} B ({staged / len(wire):.1%} of the wire), skipped {skipped} B")
     if mode == "always":
         assert staged <= len(wire) // 4, (staged, len(wire))
-    else:  # the first batch is staged whole; the ctx then sees blobs dominate
-        assert staged <= len(wire) // 3, (staged, len(wire))
+    else:
+        assert staged >= len(wire) // 2, (staged, len(wire))
     assert staged + skipped >= len(wire) * 9 // 10
 
 

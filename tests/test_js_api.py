@@ -560,3 +560,19 @@ def test_write_acks_follow_the_reference():
     """As test_write_acks_follow_the_reference_cpu, through the addon and the GPU."""
     for case in _ack_cases():
         assert run_acks(case, mock=False) == case["log"], case["name"]
+
+
+@needs_node
+def test_high_water_mark_option():
+    """decode() keeps MAX_BATCH (64 MiB) as its highWaterMark so a producer that honours write()
+    runs far enough ahead to fill GPU batches (a documented divergence, INTEGRATION.md);
+    decode({highWaterMark: 16384}) restores the reference's Writable default (decode.js:65), so
+    write() returns false once 16 KiB are buffered. And the write queue never keeps a consumed
+    write alive (300 distinct 64 KiB writes, each issued after the previous callback)."""
+    out = json.loads(subprocess.check_output([NODE, os.path.join(JS, "hwm_queue.js"), "300", "65536"],
+                                             text=True, timeout=120))
+    assert out["defaultHwm"] == 64 * 1024 * 1024 and out["optionHwm"] == 16384
+    assert out["writeReturns"][-1] is False, out["writeReturns"]  # (Node's Writable, as the reference's)
+    assert out["retained"] == 0, out
+    assert out["queueLength"] < 130, out
+    assert out["changes"] > 300 * 1000, out
