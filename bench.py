@@ -605,7 +605,8 @@ def run_c3(args, dev, steps, warmup, cpu):
                 "ms": float(np.mean(t_h2d))},
         "d2h_ms": float(np.mean(t_d2h)),
         "roofline": {"bound": "hbm", "achieved": b_dev / dec_s / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": b_dev / dec_s / 1e9 / HBM_PEAK_GBPS, "traffic": None,
+                     "frac": b_dev / dec_s / 1e9 / HBM_PEAK_GBPS, "traffic": traffic_from_profile("c3", nf),
+                     "traffic_source": TRAFFIC_SOURCE % "c3",
                      "kernel": "the staged pieces' device decode (claims + verify + emit), summed", "kernel_ms": dec_s * 1e3,
                      "bytes_model": "staged + 13*frames + 49*changes"},
     }

@@ -184,7 +184,7 @@ struct drp_ctx {
   // claims kernel: the region walkers (drp_walk.hip) for batches of at least walk_min tiles,
   // claims_fast below; DRP_CLAIMS=walk / fast forces one (A/B, tests)
   uint64_t walk_min = 32768;
-  int claims_mode = 0;  // 0 auto, 1 walk (ring), 2 fast, 3 hop
+  int claims_mode = 0;  // 0 auto, 2 fast, 3 hop
   int crec = 0;         // claims_fast's per-frame records and the record emission (DRP_CREC)
   DevBuf recbuf;
   uint64_t dirty_cap = ~0ull;
@@ -280,7 +280,7 @@ int drp_open(int device, drp_ctx **out) {
   if (const char *e = getenv("DRP_JUMP_MIN")) c->jump_min = strtoll(e, nullptr, 10);
   if (const char *e = getenv("DRP_WALK_MIN")) c->walk_min = strtoull(e, nullptr, 10);
   if (const char *e = getenv("DRP_CREC")) c->crec = atoi(e);
-  if (const char *e = getenv("DRP_CLAIMS")) c->claims_mode = strcmp(e, "walk") == 0 ? 1 : strcmp(e, "fast") == 0 ? 2 : strcmp(e, "hop") == 0 ? 3 : 0;
+  if (const char *e = getenv("DRP_CLAIMS")) c->claims_mode = strcmp(e, "fast") == 0 ? 2 : strcmp(e, "hop") == 0 ? 3 : 0;
   if (const char *e = getenv("DRP_DIRTY_CAP")) c->dirty_cap = strtoull(e, nullptr, 10);
   c->trace_file = getenv("DRP_TRACE_FILE");
   if (getenv("DRP_STATS") && hipMalloc((void **)&c->dstats, 64 * 8) == hipSuccess) c->stats = true;
@@ -656,11 +656,11 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   P.cascade_min = c->cascade_min;
   P.jump_min = c->jump_min >= 0 ? (uint32_t)c->jump_min : (uint32_t)std::max<uint64_t>(64, NT / 512);
   P.dlist_cap = std::min<uint64_t>(NT, c->dirty_cap);  // (tests: DRP_DIRTY_CAP)
-  if (c->claims_mode == 1 || c->claims_mode == 3 || (c->claims_mode == 0 && NT >= c->walk_min)) {
+  if (c->claims_mode == 3 || (c->claims_mode == 0 && NT >= c->walk_min)) {
     P.walk_rp = c->scratch.at<uint64_t>(L.walk);
     P.walk_entry = c->scratch.at<uint64_t>(L.went);
     P.walk_dense = c->scratch.at<unsigned long long>(L.wdense);
-    P.walk_hop = c->claims_mode == 3 ? 1u : c->claims_mode == 1 ? 0u : 2u;  // 2: by the density sample
+    P.walk_hop = c->claims_mode == 3 ? 1u : 2u;  // 2: by the density sample
     P.walk_tpr = drp_walk_tiles_per_region(NT, (int)P.walk_hop);
   }
   // claims_fast's per-frame records (fast_records, 24 B per frame slot): emit_lean expands them into
@@ -726,9 +726,14 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     uint32_t k = 0;
     bool full = h[10] != 0 || h[8] > P.dlist_cap;
     for (; pass < kSpecRepairPasses && (h[1] & miss); pass++) {
-      // a dirty list this long after a pass is a cascade already (C5's first list is ~300 tiles)
+      // a dirty list this long after a repair pass is a cascade already (C5's first list is ~300
+      // tiles). Not after the head's pass: independent misses (C3: a blob tile whose random bytes
+      // held a far candidate that landed on the next unit's chain, ~1.5% of the blob tiles) each
+      // list the identity tiles behind them, and one repair pass fixes them all; taken for a
+      // cascade, they cost a segmented repair (~100 ms per 0.34 GB)
       const uint64_t seg_early = std::max<uint64_t>(1024, NT / 256);
-      if ((pass >= kSegRepairAfter || h[8 + k] > seg_early || (h[1] & drp_spec_cascade_bit())) && !seg_done) {
+      if ((pass >= kSegRepairAfter || (pass > 0 && h[8 + k] > seg_early) || (h[1] & drp_spec_cascade_bit())) &&
+          !seg_done) {
         // the misses keep coming one tile per pass (wrong predictions that agree with each
         // other): recompute the claims of each stream from its first missed tile by exact
         // chain walks (drp_decode_spec.hip, segmented repair), then verify them
@@ -1417,9 +1422,21 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(PackSegs S, uint8_t *out
   }
 }
 
+// u64 -> double in place of a column copy (DRP_FETCH_F64): dst[i] = (double)src[i]
+__global__ __launch_bounds__(256) void u64_f64_kernel(const uint64_t *src, double *dst, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u)
+    dst[i] = (double)src[i];
+}
+
 int drp_decode_fetch_block(drp_ctx *c, void *block, uint64_t block_bytes, const uint64_t *col_off, uint64_t first,
                            uint64_t rows) {
-  if (!c || (!block && block_bytes) || !col_off) return DRP_E_INVAL;
+  return drp_decode_fetch_block_ex(c, block, block_bytes, col_off, first, rows, 0);
+}
+
+int drp_decode_fetch_block_ex(drp_ctx *c, void *block, uint64_t block_bytes, const uint64_t *col_off, uint64_t first,
+                              uint64_t rows, uint32_t flags) {
+  if (!c || (!block && block_bytes) || !col_off || (flags & ~DRP_FETCH_F64)) return DRP_E_INVAL;
+  const bool f64 = flags & DRP_FETCH_F64;
   static const uint32_t W[DRP_FETCH_COLS] = {8, 4, 1, 4, 4, 4, 4, 4, 4, 8, 8, 8, 1, 8};
   const bool kh = col_off[13] != ~0ull;
   for (int k = 0; k < DRP_FETCH_COLS - (kh ? 0 : 1); k++)
@@ -1439,6 +1456,17 @@ int drp_decode_fetch_block(drp_ctx *c, void *block, uint64_t block_bytes, const 
     const void *src[DRP_FETCH_COLS] = {S.fr.payload_off, S.fr.payload_len, S.fr.type, S.co.key_off, S.co.key_len,
                                        S.co.subset_off, S.co.subset_len, S.co.value_off, S.co.value_len,
                                        S.co.change, S.co.from, S.co.to, S.co.flags, S.co.key_hash};
+    if (f64) {  // the four u64 columns as doubles, converted into the space after the packed block
+      if (!c->fetch_tmp.ensure(block_bytes + 4 * ng * 8 + 256)) return DRP_E_NOMEM;
+      double *cv = reinterpret_cast<double *>(static_cast<uint8_t *>(c->fetch_tmp.p) + ((block_bytes + 255) & ~255ull));
+      const int ks[4] = {0, 9, 10, 11};
+      const uint32_t grid = (uint32_t)std::min<uint64_t>((ng + 255) / 256, 4096);
+      for (int q = 0; q < 4; q++) {
+        hipLaunchKernelGGL(u64_f64_kernel, dim3(grid), dim3(256), 0, c->st,
+                           static_cast<const uint64_t *>(src[ks[q]]) + g0, cv + q * ng, ng);
+        src[ks[q]] = cv + q * ng - g0;  // (the packing below adds g0 rows)
+      }
+    }
     PackSegs P = {};
     uint64_t total = 0;
     for (int k = 0; k < DRP_FETCH_COLS - (kh ? 0 : 1); k++) {
@@ -1455,16 +1483,20 @@ int drp_decode_fetch_block(drp_ctx *c, void *block, uint64_t block_bytes, const 
     CHK(hipMemcpyAsync(B, c->fetch_tmp.p, block_bytes, hipMemcpyDeviceToHost, c->st));
     CHK(hipStreamSynchronize(c->st));
     uint64_t *poff = reinterpret_cast<uint64_t *>(B + col_off[0]);
+    double *poffd = reinterpret_cast<double *>(B + col_off[0]);
     for (size_t k = 0; k < S.pieces.size(); k++) {  // (as fetch_staged: piece offsets -> batch offsets)
       const uint64_t r0 = S.pieces[k].first, r1 = k + 1 < S.pieces.size() ? S.pieces[k + 1].first : ~0ull;
       const uint64_t sh = S.pieces[k].second, lo = std::max(r0, g0), hi = std::min(r1, g0 + ng);
-      if (sh)
+      if (sh && f64)
+        for (uint64_t g = lo; g < hi; g++) poffd[dst + (g - g0)] += (double)sh;  // (exact below 2^53)
+      else if (sh)
         for (uint64_t g = lo; g < hi; g++) poff[dst + (g - g0)] += sh;
     }
   }
   if (dst) {  // (the other columns of that row are zero)
     for (int k = 3; k < DRP_FETCH_COLS - (kh ? 0 : 1); k++) memset(B + col_off[k], 0, W[k]);
-    reinterpret_cast<uint64_t *>(B + col_off[0])[0] = S.off0;
+    if (f64) reinterpret_cast<double *>(B + col_off[0])[0] = (double)S.off0;
+    else reinterpret_cast<uint64_t *>(B + col_off[0])[0] = S.off0;
     reinterpret_cast<uint32_t *>(B + col_off[1])[0] = S.len0;
     B[col_off[2]] = S.ty0;
   }

@@ -197,9 +197,6 @@ constexpr int64_t SG = 64;  // tiles per super-group (second look-back level)
 #ifndef DRP_NAP
 #define DRP_NAP 2  // s_sleep units (64 cycles) between polls of a global look-back word
 #endif
-#ifndef DRP_MEASURE_NO_EMIT
-#define DRP_MEASURE_NO_EMIT 0  // 1: skip the column writes (timing attribution only)
-#endif
 #ifndef DRP_EAGER_Y
 #define DRP_EAGER_Y 1  // group-first waves wait for Y_{t-1} before looking back (else lazy)
 #endif
@@ -1389,7 +1386,7 @@ __global__ __launch_bounds__(64 * WPG, DRP_MIN_WAVES) void decode_tiles(DecodePa
     uint64_t badf = ~0ull;
 #pragma unroll
     for (int w = 0; w < NW; w++) {
-      uint64_t bits = DRP_MEASURE_NO_EMIT ? 0ull : dmask[w];  // measurement builds only
+      uint64_t bits = dmask[w];
       while (bits) {
         const uint32_t o = 64u * w + (uint32_t)__builtin_ctzll(bits);
         bits &= bits - 1;

@@ -149,7 +149,7 @@ __device__ __forceinline__ uint32_t strong(const Img &m, uint64_t c, uint64_t s1
     const Hdr h = m.at(p);
     if (h.kind == H_VALID) {
       if (k == 0) far = h.succ >= m.A + TILE;
-      if (!plausible(m, p, h, 0 && k == 0)) return S_DEAD;
+      if (!plausible(m, p, h, false)) return S_DEAD;
       if (p < s1) n += (h.id != 0) + ((h.id == 1) << 16);
       p = h.succ;
       if (R == NONE && p >= s1) R = p;
@@ -1262,6 +1262,61 @@ __device__ __forceinline__ bool crec_general(const uint32_t *w32, uint32_t qa, u
   return vo <= pl && v == (uint64_t)(pl - vo) && vo < 0x10000u;
 }
 
+// The record of the delivered frame whose header is at tile-relative offset o (id from its node;
+// tailb: a blob cut by the stream end). w32: the tile's first byte; bytes up to se_rel are readable.
+// false: the frame is not in the record's shape (the tile takes the wire-reading emission).
+__device__ __forceinline__ bool crec_frame(const uint32_t *w32, uint32_t o, uint32_t se_rel, uint32_t id, bool tailb,
+                                           uint32_t (&w)[CR_WORDS]) {
+  const uint32_t d = o >> 2, sh = (o & 3u) * 8u;
+  const uint32_t a0 = w32[d], a1 = w32[d + 1], a2 = w32[d + 2];
+  const uint32_t h = __builtin_amdgcn_alignbit(a1, a0, sh), hn = __builtin_amdgcn_alignbit(a2, a1, sh);
+  const uint32_t k = ((uint32_t)__builtin_ctz((~h & 0x808080u) | 0x80000000u) >> 3) + 1u;
+  const uint32_t L = ((h & 0x7Fu) | ((h >> 1) & 0x3F80u) | ((h >> 2) & 0x1FC000u)) & ((1u << (7u * k)) - 1u);
+  const uint32_t po = o + k + 1u, pl = L - 1u;
+  w[0] = po | (id << 14) | ((tailb ? 1u : 0u) << 16);
+  w[1] = pl;
+  w[2] = w[3] = w[4] = w[5] = 0;
+  if (id != 1u) return true;
+  const uint64_t x = (((uint64_t)hn << 32) | h) >> (8u * (k + 1u));  // payload bytes 0 .. 6 - k
+  const uint32_t b1 = (uint32_t)(x >> 8) & 0xFFu, b2 = (uint32_t)(x >> 16) & 0xFFu;
+  const uint32_t kb = b1 < 0x80u ? 1u : (b2 < 0x80u ? 2u : 0u);
+  const uint32_t klen = kb == 1u ? b1 : (b1 & 0x7Fu) | (b2 << 7);
+  const uint32_t ke = 1u + kb + klen;  // the key's end, payload-relative
+  uint32_t n0 = 0, n1 = 0, n2 = 0, vo = 0;
+  bool hv = false, ok = ((uint32_t)x & 0xFFu) == 0x12u && kb && ke + 6u <= pl;
+  const uint32_t qa = po + ke;
+  ok = ok && qa + 36u <= se_rel;  // (the general form's 8 dwords from qa & ~3)
+  if (ok) {
+    const uint32_t e = qa >> 2, s2 = (qa & 3u) * 8u;
+    const uint32_t c0 = w32[e], c1 = w32[e + 1], c2 = w32[e + 2], c3 = w32[e + 3];
+    const uint64_t y = (uint64_t)__builtin_amdgcn_alignbit(c1, c0, s2) | ((uint64_t)__builtin_amdgcn_alignbit(c2, c1, s2) << 32);
+    const uint32_t y8 = __builtin_amdgcn_alignbit(c3, c2, s2) & 0xFFu;
+    // one-byte change / from / to: 18 a 20 b 28 c, then [32 d (d1)] or the payload's end
+    const bool one = (y & 0xFFull) == 0x18u && ((y >> 16) & 0xFFull) == 0x20u && ((y >> 32) & 0xFFull) == 0x28u &&
+                     (y & 0x0000800080008000ull) == 0;
+    if (one) {
+      n0 = (uint32_t)(y >> 8) & 0xFFu;
+      n1 = (uint32_t)(y >> 24) & 0xFFu;
+      n2 = (uint32_t)(y >> 40) & 0xFFu;
+      if (ke + 6u != pl) {
+        const uint32_t d0 = (uint32_t)(y >> 56), vh = d0 < 0x80u ? 2u : (y8 < 0x80u ? 3u : 0u);
+        const uint32_t vl = vh == 2u ? d0 : (d0 & 0x7Fu) | (y8 << 7);
+        vo = ke + 6u + vh;
+        hv = true;
+        ok = ((uint32_t)(y >> 48) & 0xFFu) == 0x32u && vh && vo <= pl && vl == pl - vo && vo < 0x10000u;
+      }
+    } else {
+      ok = crec_general(w32, qa, ke, pl, n0, n1, n2, vo, hv);
+    }
+  }
+  w[0] |= ((hv ? 1u : 0u) << 17) | (kb << 18);
+  w[2] = klen | (vo << 16);
+  w[3] = n0;
+  w[4] = n1;
+  w[5] = n2;
+  return ok;
+}
+
 // Records of the tile's delivered frames (after the claim; whole workgroup). E / nf: this thread's
 // settled entry and frame count (0 for a non-carrier), exactly as its per-thread record has them.
 __device__ __forceinline__ void fast_records(const DecodeParams &P, uint64_t t, FastLds &S, uint32_t E, uint32_t nf,
@@ -1292,69 +1347,22 @@ __device__ __forceinline__ void fast_records(const DecodeParams &P, uint64_t t, 
   bsync();
   if (DRP_CREC_STAGE == 0) return;
   if (tid < tot && !bad) {
-    uint32_t *rr = P.rec + t * CR_TILE_WORDS + tid;
     const uint32_t i = fls[tid];
-    const uint32_t nd = S.lnd[i], c = nd & 0xFFFFu, id = nd >> 30;
-    const uint32_t o = S.lpos[i];
-    const uint32_t d = o >> 2, sh = (o & 3u) * 8u;
-    const uint32_t a0 = w32[d], a1 = w32[d + 1], a2 = w32[d + 2];
-    const uint32_t w = __builtin_amdgcn_alignbit(a1, a0, sh), wn = __builtin_amdgcn_alignbit(a2, a1, sh);
-    const uint32_t k = ((uint32_t)__builtin_ctz((~w & 0x808080u) | 0x80000000u) >> 3) + 1u;
-    const uint32_t L = ((w & 0x7Fu) | ((w >> 1) & 0x3F80u) | ((w >> 2) & 0x1FC000u)) & ((1u << (7u * k)) - 1u);
-    const uint32_t po = o + k + 1u, pl = L - 1u;
-    uint32_t w0 = po | (id << 14) | ((c == NX_TAILB ? 1u : 0u) << 16);
-    if (id == 1u) {
-      const uint64_t x = (((uint64_t)wn << 32) | w) >> (8u * (k + 1u));  // payload bytes 0 .. 6 - k
-      const uint32_t b1 = (uint32_t)(x >> 8) & 0xFFu, b2 = (uint32_t)(x >> 16) & 0xFFu;
-      const uint32_t kb = b1 < 0x80u ? 1u : (b2 < 0x80u ? 2u : 0u);
-      const uint32_t klen = kb == 1u ? b1 : (b1 & 0x7Fu) | (b2 << 7);
-      const uint32_t ke = 1u + kb + klen;  // the key's end, payload-relative
-      uint32_t n0 = 0, n1 = 0, n2 = 0, vo = 0;
-      bool hv = false, ok = ((uint32_t)x & 0xFFu) == 0x12u && kb && ke + 6u <= pl;
-      const uint32_t qa = po + ke;
-      ok = ok && qa + 36u <= se_rel;  // (the general form's 8 dwords from qa & ~3)
-      if (ok) {
-        const uint32_t e = qa >> 2, s2 = (qa & 3u) * 8u;
-        const uint32_t c0 = w32[e], c1 = w32[e + 1], c2 = w32[e + 2], c3 = w32[e + 3];
-        const uint64_t y = (uint64_t)__builtin_amdgcn_alignbit(c1, c0, s2) |
-                           ((uint64_t)__builtin_amdgcn_alignbit(c2, c1, s2) << 32);
-        const uint32_t y8 = __builtin_amdgcn_alignbit(c3, c2, s2) & 0xFFu;
-        // one-byte change / from / to: 18 a 20 b 28 c, then [32 d (d1)] or the payload's end
-        const bool one = (y & 0xFFull) == 0x18u && ((y >> 16) & 0xFFull) == 0x20u && ((y >> 32) & 0xFFull) == 0x28u &&
-                         (y & 0x0000800080008000ull) == 0;
-        if (one) {
-          n0 = (uint32_t)(y >> 8) & 0xFFu;
-          n1 = (uint32_t)(y >> 24) & 0xFFu;
-          n2 = (uint32_t)(y >> 40) & 0xFFu;
-          if (ke + 6u == pl) {
-            hv = false;
-          } else {
-            const uint32_t d0 = (uint32_t)(y >> 56), vh = d0 < 0x80u ? 2u : (y8 < 0x80u ? 3u : 0u);
-            const uint32_t vl = vh == 2u ? d0 : (d0 & 0x7Fu) | (y8 << 7);
-            vo = ke + 6u + vh;
-            hv = true;
-            ok = ((uint32_t)(y >> 48) & 0xFFu) == 0x32u && vh && vo <= pl && vl == pl - vo && vo < 0x10000u;
-          }
-        } else {
-          ok = crec_general(w32, qa, ke, pl, n0, n1, n2, vo, hv);
-        }
-      }
-      if (DRP_CREC_STAGE == 1) {  // (A/B: keep the decode, store nothing)
-        if ((n0 ^ n1 ^ n2 ^ vo ^ klen) == 0x7FFFFFFFu && ok) rr[0] = w0;
-        ok = false;
-      }
-      if (ok) {
-        w0 |= ((hv ? 1u : 0u) << 17) | (kb << 18);
-        rr[2 * CR_CAP] = klen | (vo << 16);
-        rr[3 * CR_CAP] = n0;
-        rr[4 * CR_CAP] = n1;
-        rr[5 * CR_CAP] = n2;
-      }
-      bad = !ok;
+    const uint32_t nd = S.lnd[i];
+    uint32_t w[CR_WORDS];
+    bad = !crec_frame(w32, S.lpos[i], se_rel, nd >> 30, (nd & 0xFFFFu) == NX_TAILB, w);
+    uint32_t *rr = P.rec + t * CR_TILE_WORDS + tid;
+    if (DRP_CREC_STAGE == 1) {  // (A/B: keep the decode, store nothing)
+      if ((w[0] ^ w[2] ^ w[3] ^ w[4] ^ w[5]) == 0x7FFFFFFFu && !bad) rr[0] = w[1];
+      bad = true;
     }
-    if (DRP_CREC_STAGE >= 2) {
-      rr[0] = w0;
-      rr[CR_CAP] = pl;
+    if (!bad) {
+      rr[0] = w[0];
+      rr[CR_CAP] = w[1];
+      if ((w[0] >> 14 & 3u) == 1u) {
+#pragma unroll
+        for (uint32_t k = 2; k < CR_WORDS; k++) rr[k * CR_CAP] = w[k];
+      }
     }
   }
   const uint64_t bm = __ballot(bad);
@@ -1387,7 +1395,6 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   uint32_t *hmx = S.hmx, *lnd = S.lnd, *xw = S.xw, *xf = S.xf, *wl = S.wl, *fl = S.fl;
   uint8_t *lal = S.lal;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-  static_assert(!EDGE || 1, "the edge form has no LDS image");
   // ---- stage, masks, live positions (varints of 1..3 bytes) --------------------------------
   uint4 v[SEGB / 16], hv;
   if (EDGE) {
@@ -1772,14 +1779,32 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   return FC_OK;
 }
 
-// CF: with the structural check of frames that leave the image (long frames, C5). The host picks
-// the form from the frame density of the ctx's previous decode: dense streams (C2) are predicted
-// as well without it, and its code costs them ~4% (DESIGN.md "Long frames").
+// CF: with the structural check of frames that leave the image (long frames, C5). Picked per
+// launch: the host takes it for a context whose last decode averaged >= 512 bytes per frame (and
+// for its first), and large batches take the hop walkers instead when walk_density's sample says
+// the stream is sparse; dense streams (C2) are predicted as well without it, and its code costs
+// them ~4% (DESIGN.md "Long frames").
+#ifndef DRP_K1_PERSIST
+#define DRP_K1_PERSIST 0  // (A/B: workgroups per CU of a persistent claims grid; 0: a workgroup per tile)
+#endif
 template <bool CF>
 __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) {
   __shared__ FastLds S;
-  const uint64_t t = blockIdx.x;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
+#if DRP_K1_PERSIST  // (A/B: a persistent grid; measured slower, its loop spills registers)
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    bsync();  // (the previous tile's LDS reads are done)
+    const TileGeo G = tile_geo(P, t);
+    if (G.A < G.so || G.A + IMG > G.se) {  // edge tile: the general kernel
+      push_work(P, t);
+      continue;
+    }
+    uint32_t eb, en, ecn;
+    uint64_t cl;
+    (void)fast_claims<CF>(P, G, t, S, eb, en, ecn, cl);
+  }
+#else
+  const uint64_t t = blockIdx.x;
   const TileGeo G = tile_geo(P, t);
   if (t >= ntiles) return;  // (whole workgroup)
   if (G.A < G.so || G.A + IMG > G.se) {  // edge tile: the general kernel
@@ -1789,6 +1814,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   uint32_t eb, en, ecn;
   uint64_t cl;
   (void)fast_claims<CF>(P, G, t, S, eb, en, ecn, cl);
+#endif
 }
 
 // ==== kernel 2: exact entries, verification, frame counts =====================================
@@ -1802,6 +1828,10 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
 // that does not pass (a re-walk is needed, a miss, a longer identity run) goes to a list that
 // verify_counts then takes, so results are verify_counts' in every case. Threads before k are
 // left to emit_tiles through tile_k (the records stay as kernel 1 wrote them).
+#ifndef DRP_CASCADE_HARD
+#define DRP_CASCADE_HARD 1  // (A/B: 0 counts every listed tile toward a cascade, as round 5 did)
+#endif
+constexpr uint32_t VL_HARD = 1u << 31;  // verify_lite's list entry: the tile's prediction failed
 #ifndef DRP_CASCADE_DIV
 #define DRP_CASCADE_DIV 8  // verify_counts hands the listed tiles to the segmented repair when more
 #endif                     // than 1/8 of the tiles (and P.cascade_min) are listed (0: never)
@@ -1878,13 +1908,19 @@ __global__ __launch_bounds__(VL_BLK) void verify_lite(DecodeParams P) {
   // verify_counts decides the tiles listed here; one atomic per wave (a cascade lists every tile,
   // and one counter word takes ~88 atomics per us: 207K single appends cost 0.3 ms)
   const bool lst = r == 0 && (!found || bad || bogus || miss || (inside && claim == C_ID));
+  // a listed tile a prediction failed on (every reason but !found: a tile deep inside a long
+  // payload, more than 32 identity claims after the last frame start, only needs a longer
+  // look-back) carries VL_HARD in its list entry; verify_counts decides a cascade from a sample of
+  // the entries (no counter: one atomic per listing wave cost 0.2 ms on C2)
+  // (!found: et is only the stream entry, so bogus and miss mean nothing there)
+  const bool hard = DRP_CASCADE_HARD && found && (bad || bogus || miss || (inside && claim == C_ID));
   const uint64_t lm = __ballot(lst);
   if (lm) {
     const uint32_t lane = threadIdx.x & 63u, ld = (uint32_t)__builtin_ctzll(lm);
     uint32_t base = 0;
     if (lane == ld) base = atomicAdd(P.vlist_n, (uint32_t)__builtin_popcountll(lm));
     base = (uint32_t)__shfl((int)base, (int)ld, WAVE);
-    if (lst) P.vlist[base + (uint32_t)__builtin_popcountll(lm & ((1ull << lane) - 1ull))] = (uint32_t)t;
+    if (lst) P.vlist[base + (uint32_t)__builtin_popcountll(lm & ((1ull << lane) - 1ull))] = (uint32_t)t | (hard ? VL_HARD : 0u);
   }
   if (r != 0 || lst) return;
   // the record emission takes the tile when the claims kernel recorded every frame its threads
@@ -1919,19 +1955,33 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     }
     return;
   }
-  // A cascade: verify_lite listed more than 1 / DRP_CASCADE_DIV of the tiles (and at least
-  // P.cascade_min, 4096 unless DRP_CASCADE_MIN says otherwise), i.e. the prediction followed a
+  // A cascade: verify_lite listed more than 1 / DRP_CASCADE_DIV of the tiles as failed predictions
+  // (and at least P.cascade_min, 4096 unless DRP_CASCADE_MIN says otherwise; tiles listed only for
+  // a longer look-back do not count: C3's 1 MiB blobs list ~90% of the tiles that way, and taking
+  // them for a cascade cost a segmented repair, 110 ms per 0.34 GB), i.e. the prediction followed a
   // second framing through the stream (tests/_streams.shadow_stream). Re-walking every listed tile only to find them missed costs
   // as much as the segmented repair that follows (1.7 GB dense cascade: 2.4 of 11.7 ms), so the
   // list goes to that repair directly: each stream's first listed tile in first_miss (every tile
   // before it passed the records-only proof, so its entry is exact) and F_CASCADE for the host.
   // Only in the head's pass (pass_id 1).
-  if (DRP_CASCADE_DIV && P.pass_id == 1 && P.vlist && !P.vlist_ovf && nwork >= P.cascade_min &&
-      (uint64_t)nwork * DRP_CASCADE_DIV > ntiles) {
+  // (the share of failed predictions among the listed tiles, from 64 entries spread over the list:
+  // every workgroup reads the same sample and takes the same decision)
+  bool cascade = DRP_CASCADE_DIV && P.pass_id == 1 && P.vlist && !P.vlist_ovf && nwork >= P.cascade_min &&
+                 (uint64_t)nwork * DRP_CASCADE_DIV > ntiles;
+  if (cascade && DRP_CASCADE_HARD) {
+    const uint32_t e = P.vlist[(uint64_t)nwork * lane / WAVE];
+    const uint32_t nh = (uint32_t)__builtin_popcountll(__ballot(wid == 0 && (e & VL_HARD)));
+    if (wid == 0 && lane == 0) xs[0] = nh;
+    bsync();
+    // the hard entries extrapolated: a cascade when they alone are over the threshold
+    cascade = (uint64_t)nwork * xs[0] / WAVE >= P.cascade_min && (uint64_t)nwork * xs[0] / WAVE * DRP_CASCADE_DIV > ntiles;
+    bsync();
+  }
+  if (cascade) {
     // one stream: a wave minimum, one atomic per wave; several: one atomic per listed tile
     uint32_t tmin = ~0u;
     for (uint32_t wi = blockIdx.x * NT + tid; wi < nwork; wi += gridDim.x * NT) {
-      const uint32_t t = P.vlist[wi];
+      const uint32_t t = P.vlist[wi] & ~VL_HARD;
       if (P.nstreams == 1) tmin = min(tmin, t);
       else atomicMin((unsigned long long *)&P.first_miss[P.tile_stream[t]], (unsigned long long)t);
     }
@@ -1943,7 +1993,7 @@ __global__ __launch_bounds__(NT) void verify_counts(DecodeParams P) {
     return;
   }
   for (uint32_t wi = blockIdx.x; P.vlist ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
-  const uint64_t t = P.vlist ? P.vlist[wi] : wi;
+  const uint64_t t = P.vlist ? P.vlist[wi] & ~VL_HARD : wi;
   bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
   if (t >= ntiles) continue;  // (whole workgroup)
@@ -2510,7 +2560,7 @@ __global__ __launch_bounds__(NT, DRP_EMIT_WAVES) void emit_tiles(DecodeParams P)
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
   const uint32_t nwork = P.vlist ? *P.vlist_n : 0u;
   for (uint32_t wi = blockIdx.x; P.vlist ? wi < nwork : wi == blockIdx.x; wi += gridDim.x) {
-  const uint64_t t = P.vlist ? P.vlist[wi] : wi;
+  const uint64_t t = P.vlist ? P.vlist[wi] & ~VL_HARD : wi;
   bsync();  // the previous tile's LDS reads are done
   const TileGeo G = tile_geo(P, t);  // (its loads go out with the tile count's)
   if (t >= ntiles) continue;  // (whole workgroup)
@@ -2701,8 +2751,13 @@ __device__ __forceinline__ void emit_rec_row(const RowCols &C, uint64_t A, uint3
   st_col(C.to, s, (uint64_t)n2);
   st_col(C.fl, s, (uint8_t)(hv ? DRP_F_VALUE : 0u));
 }
-// A wave per tile (its meta by scalar loads), every record word of the lane's rows loaded before
-// any column is stored.
+// ER_TPW tiles per wave (their meta by scalar loads, issued together), every record word of the
+// lane's rows of all of them loaded before any column is stored: a wave has two round trips to
+// memory in all, and its bytes in flight cover them.
+#ifndef DRP_ER_TPW
+#define DRP_ER_TPW 2
+#endif
+constexpr uint32_t ER_TPW = DRP_ER_TPW;
 __global__ __launch_bounds__(ER_WAVES * WAVE) void emit_recs(DecodeParams P) {
   if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
   uint64_t b;
@@ -2711,27 +2766,39 @@ __global__ __launch_bounds__(ER_WAVES * WAVE) void emit_recs(DecodeParams P) {
     b = (uint64_t)x * q + min(x, r) + blockIdx.x / 8u;
   }
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t t = b * ER_WAVES + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (t >= ldc(P.tile_prefix + P.nstreams)) return;  // (whole wave)
-  const uint32_t rk = ldc(P.tile_recok + t);
-  if (!rk) return;
-  const uint32_t n = (uint32_t)ldc(P.tile_count + t);
-  const uint64_t base = ldc(P.tile_base + t);
-  const RowCols C = row_cols(P, base);
-  const uint32_t lim = min(n, C.lim);
-  const uint32_t *rr = P.rec + t * CR_TILE_WORDS + (rk - 1u);
-  uint32_t w[ER_RPL][CR_WORDS];
+  const uint64_t t0 = (b * ER_WAVES + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * ER_TPW;
+  const uint64_t ntiles = ldc(P.tile_prefix + P.nstreams);
+  uint32_t rk[ER_TPW], lim[ER_TPW];
+  uint64_t base[ER_TPW];
 #pragma unroll
-  for (uint32_t j = 0; j < ER_RPL; j++) {
-    const uint32_t s = lane + j * WAVE;
-#pragma unroll
-    for (uint32_t k = 0; k < CR_WORDS; k++) w[j][k] = s < lim ? rr[k * CR_CAP + s] : 0u;
+  for (uint32_t i = 0; i < ER_TPW; i++) {
+    const uint64_t t = t0 + i;
+    rk[i] = t < ntiles ? ldc(P.tile_recok + t) : 0u;
+    const uint32_t n = t < ntiles ? (uint32_t)ldc(P.tile_count + t) : 0u;
+    base[i] = t < ntiles ? ldc(P.tile_base + t) : 0ull;
+    lim[i] = rk[i] ? min(n, base[i] >= P.cap ? 0u : (uint32_t)umin64(P.cap - base[i], 0xFFFFFFFFull)) : 0u;
   }
-  const uint64_t A = tile_geo(P, t).A;
+  uint32_t w[ER_TPW][ER_RPL][CR_WORDS];
 #pragma unroll
-  for (uint32_t j = 0; j < ER_RPL; j++) {
-    const uint32_t s = lane + j * WAVE;
-    if (s < lim) emit_rec_row(C, A, s, w[j][0], w[j][1], w[j][2], w[j][3], w[j][4], w[j][5]);
+  for (uint32_t i = 0; i < ER_TPW; i++) {
+    const uint32_t *rr = P.rec + (t0 + i) * CR_TILE_WORDS + (rk[i] - 1u);
+#pragma unroll
+    for (uint32_t j = 0; j < ER_RPL; j++) {
+      const uint32_t s = lane + j * WAVE;
+#pragma unroll
+      for (uint32_t k = 0; k < CR_WORDS; k++) w[i][j][k] = s < lim[i] ? rr[k * CR_CAP + s] : 0u;
+    }
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < ER_TPW; i++) {
+    if (!lim[i]) continue;
+    const uint64_t A = tile_geo(P, t0 + i).A;
+    const RowCols C = row_cols(P, base[i]);
+#pragma unroll
+    for (uint32_t j = 0; j < ER_RPL; j++) {
+      const uint32_t s = lane + j * WAVE;
+      if (s < lim[i]) emit_rec_row(C, A, s, w[i][j][0], w[i][j][1], w[i][j][2], w[i][j][3], w[i][j][4], w[i][j][5]);
+    }
   }
 }
 
@@ -2746,9 +2813,11 @@ __device__ __forceinline__ void emit_lean_tile(const DecodeParams &P, uint64_t t
 // Long-frame streams (the context's change_checks form: >= 512 B per frame) leave nearly every
 // tile to emit_sparse, and with per-frame records nearly every tile goes to emit_recs, so a
 // workgroup per tile would mostly be dispatched to exit: there each
-// workgroup takes EMIT_LONG_TPW tiles, strided by the grid (drp_launch_spec_tail sizes it), reads
-// their sparse marks in one load (a lane each) and runs only the others (8 tiles with a load each
-// in turn: C5's emit_lean took 0.116 ms of dependent mark loads).
+// workgroup takes EMIT_LONG_TPW consecutive tiles (drp_launch_spec_tail sizes the grid), reads
+// their marks in one load (a lane each) and runs only the others (8 tiles with a load each in
+// turn: C5's emit_lean took 0.116 ms of dependent mark loads). Consecutive, not strided by the
+// grid: a tile's halo is its successor's head, and their column lines meet, in one L2 (with every
+// tile left to it, the strided order took 4.5 ms on C2 against 2.8 for a workgroup per tile).
 constexpr uint32_t EMIT_LONG_TPW = 32;
 static_assert(EMIT_LONG_TPW <= WAVE, "one lane per tile's mark");
 __global__ __launch_bounds__(NT, DRP_EMIT_LEAN_WAVES) void emit_lean(DecodeParams P) {
@@ -2758,7 +2827,7 @@ __global__ __launch_bounds__(NT, DRP_EMIT_LEAN_WAVES) void emit_lean(DecodeParam
     const uint64_t ntiles = P.tile_prefix[P.nstreams];
     const uint32_t tid = threadIdx.x;
     if (tid < WAVE) {
-      const uint64_t t = blockIdx.x + (uint64_t)tid * gridDim.x;
+      const uint64_t t = (uint64_t)blockIdx.x * EMIT_LONG_TPW + tid;
       const bool run = tid < EMIT_LONG_TPW && t < ntiles && !(P.tile_sparse && P.tile_sparse[t]) &&
                        !(P.tile_recok && P.tile_recok[t]);
       const uint64_t m = __ballot(run);
@@ -2772,7 +2841,7 @@ __global__ __launch_bounds__(NT, DRP_EMIT_LEAN_WAVES) void emit_lean(DecodeParam
       todo &= todo - 1;
       if (!first) bsync();  // (the last tile's LDS reads are done)
       first = false;
-      emit_lean_tile(P, blockIdx.x + (uint64_t)j * gridDim.x, L);
+      emit_lean_tile(P, (uint64_t)blockIdx.x * EMIT_LONG_TPW + j, L);
     }
     return;
   }
@@ -3644,10 +3713,13 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
     const hipError_t e = drp_launch_claims_walk(&Q, nt_max, st);
     if (e != hipSuccess) return e;
     drp_dbg_mark("claims_walk", st);
-  } else if (Q.change_checks && !P->walk_rp)
-    hipLaunchKernelGGL(spec::claims_fast<true>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
-  else
-    hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)nt_max), dim3(spec::NT), 0, st, Q);
+  } else {
+    const uint64_t g = DRP_K1_PERSIST ? std::min<uint64_t>(nt_max, 256ull * DRP_K1_PERSIST) : nt_max;
+    if (Q.change_checks && !P->walk_rp)
+      hipLaunchKernelGGL(spec::claims_fast<true>, dim3((uint32_t)g), dim3(spec::NT), 0, st, Q);
+    else
+      hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)g), dim3(spec::NT), 0, st, Q);
+  }
   drp_dbg_mark("claims_fast", st);
   const uint32_t gw = (uint32_t)(nt_max < 16384 ? nt_max : 16384);
   hipLaunchKernelGGL(spec::spec_claims, dim3(gw), dim3(spec::NT), 0, st, Q);
@@ -3737,7 +3809,8 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
       Q.tile_sparse = nullptr;
     }
     if (Q.rec)  // (the tiles with records; emit_lean skips them)
-      hipLaunchKernelGGL(spec::emit_recs, dim3((uint32_t)((nt_max + spec::ER_WAVES - 1) / spec::ER_WAVES)),
+      hipLaunchKernelGGL(spec::emit_recs,
+                         dim3((uint32_t)((nt_max + spec::ER_WAVES * spec::ER_TPW - 1) / (spec::ER_WAVES * spec::ER_TPW))),
                          dim3(spec::ER_WAVES * WAVE), 0, st, Q);
     hipLaunchKernelGGL(spec::emit_lean,
                        dim3((uint32_t)(Q.change_checks || Q.rec ? (nt_max + spec::EMIT_LONG_TPW - 1) / spec::EMIT_LONG_TPW
@@ -3790,17 +3863,17 @@ extern "C" hipError_t drp_launch_seg_repair(const DecodeParams *P, uint64_t s, u
   R.nseg = (n + R.G - 1) / R.G;
   R.cand = scratch;
   R.seg_entry = scratch + 2 * spec::SEG_CAND * spec::SEG_NMAX;
-  R.nidx = 1 ? reinterpret_cast<uint8_t *>(R.seg_entry + spec::SEG_NMAX + 2) : nullptr;  // (SEG_NMAX x 64 B, 16-B aligned)
+  R.nidx = reinterpret_cast<uint8_t *>(R.seg_entry + spec::SEG_NMAX + 2);  // (SEG_NMAX x 64 B, 16-B aligned)
   R.seg_lane = reinterpret_cast<uint8_t *>(R.seg_entry + spec::SEG_NMAX + 2) + spec::SEG_NMAX * spec::SEG_CAND;
   // (the parallel seg_claims needs the stitch's tables and a position per candidate per tile)
-  R.ctile = 1 && R.nidx && ctile && ctile_cap >= n * spec::SEG_CAND ? ctile : nullptr;
+  R.ctile = ctile && ctile_cap >= n * spec::SEG_CAND ? ctile : nullptr;
   DecodeParams Q = *P;
   if (Q.tile_rec) {  // (the repair rewrites these tiles' records: the region walkers' no longer apply)
     const hipError_t e = hipMemsetAsync(Q.tile_rec + t0, 0xFF, (tl - t0) * 4, st);
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(spec::seg_walk, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);
-  if (R.nidx) hipLaunchKernelGGL(spec::seg_link, dim3((uint32_t)R.nseg), dim3(WAVE), 0, st, Q, R);
+  hipLaunchKernelGGL(spec::seg_link, dim3((uint32_t)R.nseg), dim3(WAVE), 0, st, Q, R);
   hipLaunchKernelGGL(spec::seg_stitch, dim3(1), dim3(spec::SEG_STB), 0, st, Q, R);
   if (R.ctile) hipLaunchKernelGGL(spec::seg_claims_par, dim3((uint32_t)((n + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, Q, R);
   hipLaunchKernelGGL(spec::seg_claims, dim3((uint32_t)R.nseg), dim3(spec::NT), 0, st, Q, R);

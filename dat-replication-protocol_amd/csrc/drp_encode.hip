@@ -112,28 +112,12 @@ __device__ __forceinline__ uint64_t enc_funnel(uint64_t lo, uint64_t hi, uint32_
   return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
 }
 
-#ifndef DRP_ENC_UNROLL
-#define DRP_ENC_UNROLL 1  // 16-byte blocks per lane in flight in the bulk copy
-#endif
-#ifndef DRP_ENC_NT
-#define DRP_ENC_NT 0  // 1: non-temporal heap loads and wire stores in the bulk copy (A/B)
-#endif
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 enc_ld(const uint4 *p) {
-#if DRP_ENC_NT
-  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-  return make_uint4(v.x, v.y, v.z, v.w);
-#else
   return *p;
-#endif
 }
 __device__ __forceinline__ void enc_st(uint4 *p, uint4 v) {
-#if DRP_ENC_NT
-  u32x4 w = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p));
-#else
   *p = v;
-#endif
 }
 // 16 bytes starting `sh` bytes into lo (the next bytes from hi)
 __device__ __forceinline__ uint4 enc_shift(uint4 lo, uint4 hi, uint32_t sh) {
@@ -156,9 +140,6 @@ __device__ __forceinline__ uint4 enc_shift(uint4 lo, uint4 hi, uint32_t sh) {
 // cover them (funnel shift by the wave-uniform source misalignment), then a byte tail. The
 // second block of the last step lies in the aligned 16 bytes that hold the last source byte,
 // so no load leaves the source's pages.
-#ifndef DRP_ENC_PIPE
-#define DRP_ENC_PIPE 0  // 1: the next step's loads issued before this step's store (A/B)
-#endif
 __device__ __forceinline__ void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint64_t n,
                                           uint32_t lane) {
   if (n < 128) {
@@ -175,105 +156,16 @@ __device__ __forceinline__ void wave_copy(uint8_t *__restrict__ dst, const uint8
   const uint4 *sa = reinterpret_cast<const uint4 *>(src - sh);
   uint4 *da = reinterpret_cast<uint4 *>(dst);
   uint64_t b = lane;
-#if DRP_ENC_UNROLL > 1
-  // DRP_ENC_UNROLL blocks per lane in flight: every load of a step is issued before its stores
-  for (; b + 64 * (DRP_ENC_UNROLL - 1) < nb; b += 64 * DRP_ENC_UNROLL) {
-    uint4 lo[DRP_ENC_UNROLL], hi[DRP_ENC_UNROLL];
-#pragma unroll
-    for (int u = 0; u < DRP_ENC_UNROLL; u++) {
-      lo[u] = enc_ld(sa + b + 64 * u);
-      hi[u] = sh ? enc_ld(sa + b + 64 * u + 1) : lo[u];
-    }
-#pragma unroll
-    for (int u = 0; u < DRP_ENC_UNROLL; u++) enc_st(da + b + 64 * u, enc_shift(lo[u], hi[u], sh));
-  }
-#endif
-#if DRP_ENC_PIPE
-  // software-pipelined: step b + 64's two blocks are loaded before step b's store
-  if (b < nb) {
-    uint4 lo = enc_ld(sa + b), hi = sh ? enc_ld(sa + b + 1) : lo;
-    for (; b + 64 < nb; b += 64) {
-      const uint4 lo2 = enc_ld(sa + b + 64), hi2 = sh ? enc_ld(sa + b + 65) : lo2;
-      enc_st(da + b, enc_shift(lo, hi, sh));
-      lo = lo2;
-      hi = hi2;
-    }
-    enc_st(da + b, enc_shift(lo, hi, sh));
-    b += 64;
-  }
-#else
   for (; b < nb; b += 64) {
     const uint4 lo = enc_ld(sa + b);
     enc_st(da + b, sh == 0 ? lo : enc_shift(lo, enc_ld(sa + b + 1), sh));
   }
-#endif
   const uint32_t tail = (uint32_t)(n & 15);
-  if (lane < tail) dst[(nb << 4) + lane] = src[(nb << 4) + lane];
-}
-
-#ifndef DRP_ENC_COPY2
-#define DRP_ENC_COPY2 0  // 1: wave_copy2 (measured slower on C5: 4.23 vs 2.92 ms)
-#endif
-#ifndef DRP_ENC_BATCH
-#define DRP_ENC_BATCH 8  // 16-byte blocks per lane loaded before any is stored (wave_copy2)
-#endif
-// wave_copy2: the same aligned-store copy with up to DRP_ENC_BATCH blocks per lane loaded before
-// any is stored (a 4 KB value is one batch: every load of the copy is in flight at once), and
-// each source block loaded once: the second block a lane's funnel shift needs is the next lane's
-// first (a lane permute), lane 63 taking the first block of the next column. Copies under 64
-// bytes are one byte per lane.
-__device__ __forceinline__ void wave_copy2(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint64_t n,
-                                           uint32_t lane) {
-  if (n < 64) {
-    if (lane < n) dst[lane] = src[lane];
-    return;
-  }
-  const uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15);
-  if (lane < head) dst[lane] = src[lane];
-  dst += head;
-  src += head;
-  n -= head;
-  const uint64_t nb = n >> 4;
-  const uint32_t tail = (uint32_t)(n & 15);
-  const uint32_t sh = (uint32_t)((uintptr_t)src & 15);
-  const uint4 *sa = reinterpret_cast<const uint4 *>(src - sh);
-  uint4 *da = reinterpret_cast<uint4 *>(dst);
-  // source blocks needed: [0, nb) and, when shifted, block nb (it holds source bytes: the last
-  // byte is past 16 nb - sh + 15 whenever sh > 0 and the copy is not empty)
-  const uint64_t ns = nb + (sh ? 1 : 0);
-  const int nxt = (int)(((lane + 1) & 63u) << 2);
-  for (uint64_t b0 = 0; b0 < nb; b0 += 64 * DRP_ENC_BATCH) {
-    uint4 v[DRP_ENC_BATCH + 1];
-#pragma unroll
-    for (int u = 0; u <= DRP_ENC_BATCH; u++) {
-      const uint64_t b = b0 + 64u * u + lane;
-      v[u] = (u < DRP_ENC_BATCH || lane == 0) && b < ns ? enc_ld(sa + b) : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < DRP_ENC_BATCH; u++) {
-      const uint64_t b = b0 + 64u * u + lane;
-      if (b0 + 64u * u >= nb) break;
-      uint4 w = v[u];
-      if (sh) {
-        const uint4 src_hi = lane == 0 ? v[u + 1] : v[u];  // (lane 63 reads lane 0: the next column)
-        uint4 hi;
-        hi.x = (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)src_hi.x);
-        hi.y = (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)src_hi.y);
-        hi.z = (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)src_hi.z);
-        hi.w = (uint32_t)__builtin_amdgcn_ds_bpermute(nxt, (int)src_hi.w);
-        w = enc_shift(w, hi, sh);
-      }
-      if (b < nb) enc_st(da + b, w);
-    }
-  }
   if (lane < tail) dst[(nb << 4) + lane] = src[(nb << 4) + lane];
 }
 
 #ifndef DRP_ENC_WAVES
 #define DRP_ENC_WAVES 65536  // waves of the write kernel (grid-stride over frames)
-#endif
-#ifndef DRP_ENC_LANEPREFIX
-#define DRP_ENC_LANEPREFIX 1  // 0: lane 0 writes the prefixes byte by byte from private arrays
 #endif
 
 // A varint (or one byte) packed into registers: bytes 0..7 in lo, 8..9 in hi.
@@ -309,15 +201,8 @@ __device__ __forceinline__ uint32_t put_segs(uint8_t *o, uint32_t lane, const VS
   return tot;
 }
 
-#if DRP_ENC_COPY2
-#define WAVE_COPY wave_copy2
-#else
 #define WAVE_COPY wave_copy
-#endif
 // one wave per frame (grid-stride over frames)
-#ifndef DRP_ENC_MINW
-#define DRP_ENC_MINW 0  // > 0: min waves per SIMD for the write kernel (8: 64 VGPRs, a 28-byte spill)
-#endif
 // The bytes of frame i written by one wave (the header and field prefixes lane-parallel, the key /
 // subset / value bytes by WAVE_COPY).
 __device__ __forceinline__ void write_frame(const EncodeParams &P, uint64_t i, uint32_t lane) {
@@ -351,11 +236,7 @@ __device__ __forceinline__ void write_frame(const EncodeParams &P, uint64_t i, u
 }
 
 // one wave per frame (grid-stride over frames): every frame (DRP_ENC_OS=0, A/B)
-#if DRP_ENC_MINW
-__global__ __launch_bounds__(256, DRP_ENC_MINW) void enc_write_kernel(EncodeParams P) {
-#else
 __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
-#endif
   const uint32_t lane = lane_id();
   const uint64_t wid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;

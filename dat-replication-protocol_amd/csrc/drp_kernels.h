@@ -77,14 +77,13 @@ struct DecodeParams {
   // region walkers (drp_walk.hip): per-stream region prefix [nstreams + 1], tiles per region
   uint64_t *walk_rp;
   uint64_t *walk_entry;  // region walkers: each region's entry (walk_sync)
-  uint32_t walk_hop;      // 1: the hop walkers (claims_hop), 0: the ring walkers (claims_walk), 2: by walk_dense
+  uint32_t walk_hop;      // 1: the hop walkers (claims_hop), 2: by walk_dense (hop walkers or claims_fast)
   unsigned long long *walk_dense;  // walk_density's sample: bytes, frames after stream entries
   uint32_t walk_tpr;
-  // per-frame records (null: none): rec_cap 32-byte slots per region; per tile its first record
-  // (REC_NONE: none, the tile takes the wire-reading emission) and whether verification lets the
-  // record emission take it
+  // claims_fast's per-frame records (null: none): CR_TILE_WORDS words per tile; per tile REC_NONE
+  // (no records: the tile takes the wire-reading emission) or 0, and verification's verdict for the
+  // record emission (0: not, else 1 + the slot of the tile's first row)
   uint32_t *rec;
-  uint64_t rec_cap;
   uint32_t *tile_rec;
   uint8_t *tile_recok;
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
@@ -133,8 +132,6 @@ uint32_t drp_spec_cascade_bit(void);
 hipError_t drp_launch_claims_walk(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t st);
 uint32_t drp_walk_tiles_per_region(uint64_t nt_max, int hop);
 hipError_t drp_launch_walk_density(const drp::DecodeParams *P, hipStream_t st);
-hipError_t drp_launch_emit_rec(const drp::DecodeParams *P, uint64_t nt_max, hipStream_t st);
-uint64_t drp_walk_rec_cap(uint32_t tpr);
 hipError_t drp_launch_spec_head(const drp::DecodeParams *P, uint64_t nt_max, uint64_t nstreams,
                                 uint32_t *tile_stream, hipStream_t st);
 // out[0] = payload bytes of the blob rows among rows [0, n) (out zeroed by the caller)

@@ -326,7 +326,7 @@ static int alloc_cols(dec_job *j) {
 #define KEYS_MAX ((uint64_t)256 << 20) /* (well below V8's string length limit) */
 
 static int key_text(dec_job *j) {
-  const uint64_t *off = (const uint64_t *)j->col[C_OFF];
+  const double *off = (const double *)j->col[C_OFF]; /* (converted: DRP_FETCH_F64) */
   const uint32_t *ko = (const uint32_t *)j->col[C_KO], *kl = (const uint32_t *)j->col[C_KL];
   const uint8_t *ty = (const uint8_t *)j->col[C_TYPE], *fl = (const uint8_t *)j->col[C_FL];
   uint32_t *kp = j->kp;
@@ -346,7 +346,7 @@ static int key_text(dec_job *j) {
   uint64_t k = 0, s0 = 0; /* the chunk holding batch offset a, and its start */
   for (uint64_t r = 0; r < j->rows; r++) {
     if (!((ty[r] & 0x3f) == DRP_TYPE_CHANGE && (fl[r] & (DRP_F_KEY_ASCII | DRP_F_BAD)) == DRP_F_KEY_ASCII)) continue;
-    uint64_t a = off[r] + ko[r], n = kl[r];
+    uint64_t a = (uint64_t)off[r] + ko[r], n = kl[r];
     char *d = j->keys + kp[r];
     while (n) {
       while (k + 1 < j->nchunks && s0 + j->chunks[k].n <= a) s0 += j->chunks[k++].n;
@@ -375,7 +375,8 @@ static void dec_run(dec_job *j) {
       uint64_t off[DRP_FETCH_COLS];
       for (int i = 0; i < NCOL; i++) off[i] = (uint64_t)((char *)j->col[i] - base);
       off[13] = j->khash ? (uint64_t)((char *)j->khash - base) : ~(uint64_t)0;
-      j->rc = drp_decode_fetch_block(j->box->c, base, j->bytes, off, 0, j->rows);
+      /* payload_off, change, from, to as doubles (JS Numbers), converted on the device */
+      j->rc = drp_decode_fetch_block_ex(j->box->c, base, j->bytes, off, 0, j->rows, DRP_FETCH_F64);
     }
   }
   drp_timing tm;
@@ -398,14 +399,7 @@ static void dec_run(dec_job *j) {
     return;
   }
   if (j->keys) j->host_copied += (double)j->nkeys; /* (the key text is a host copy too) */
-  /* u64 -> JS Number, in place (varint.decode yields Numbers) */
-  const int conv[] = {C_OFF, C_CH, C_FR, C_TO};
-  for (size_t k = 0; k < sizeof conv / sizeof conv[0]; k++) {
-    uint64_t *u = (uint64_t *)j->col[conv[k]];
-    double *d = (double *)j->col[conv[k]];
-    for (uint64_t r = 0; r < j->rows; r++) d[r] = (double)u[r];
-  }
-  j->t_convert = now_ms() - t0;
+  j->t_convert = now_ms() - t0; /* (the key text; the u64 -> Number columns come converted) */
 }
 
 static void free_finalizer(napi_env env, void *data, void *hint) {

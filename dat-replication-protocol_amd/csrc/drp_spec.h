@@ -28,7 +28,7 @@ constexpr uint64_t RDY = 1ull << 63;          // published word: value | RDY
 constexpr uint64_t C_ID = 1ull << 62;         // claim: identity (no chain survives the tile)
 constexpr uint64_t M_ERR = 1ull << 60;        // with MARK_TERM: the chain ended at an error header
 constexpr uint64_t NONE = ~0ull;              // internal: no chain
-constexpr uint32_t REC_NONE = 0xFFFFFFFFu;    // tile_rec: the tile has no records (drp_walk.hip)
+constexpr uint32_t REC_NONE = 0xFFFFFFFFu;    // tile_rec: the tile has no records (fast_records)
 
 constexpr uint32_t F_MISS = 1u << 12;         // overflow bit: prediction failed -> exact re-run
 constexpr uint32_t F_WAIT = 1u << 13;
@@ -136,7 +136,7 @@ __device__ __forceinline__ Hdr hdr_global(const uint8_t *g, uint64_t p, uint64_t
 // The claims form of a large batch (drp_launch_spec_head chooses it per launch from a density
 // sample, walk_density): streams averaging <= HOP_FRAME bytes per frame take claims_fast, sparser
 // ones the hop walkers (claims_hop: one header read per frame, so long frames cost nothing
-// extra). P.walk_hop: 1 the hop walkers, 0 the ring walkers (forced: DRP_CLAIMS=hop / walk).
+// extra). P.walk_hop: 1 the hop walkers (forced: DRP_CLAIMS=hop), 2 by the density sample.
 constexpr uint32_t HOP_FRAME = 512;
 __device__ __forceinline__ bool walk_hops(const DecodeParams &P) { return P.walk_hop == 1u; }
 

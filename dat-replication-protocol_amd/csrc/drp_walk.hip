@@ -8,19 +8,14 @@
 // prove claims_fast's, so every result still comes from the exact chain.
 //
 // claims_fast computes every tile from its own bytes: every live position of the tile is
-// parsed and linked (~800 VALU instructions per 4 KiB wave, VALU-issue-bound). Here one LANE
-// walks one REGION of consecutive interior tiles of a stream frame by frame, as decode.js does:
-// the entry of a region's first tile is found once (a "sync": the first position whose Change
-// payload parses exactly in the schema's shape, or whose chain survives WK_K frames), and every
-// later frame start follows from its predecessor's header. The VALU work is per frame, not per
-// byte (C2: ~1.5 frames per 128-byte window and lane).
-//
-// Data movement: the 64 regions of a wave advance together, 128 bytes (one "window") each per
-// step. A step stages the windows of all 64 regions with LDS-DMA (8 global_load_lds_dwordx4 per
-// step, each one 128-byte line of 8 regions: full lines, no VGPRs), three steps ahead into a ring
-// of 4 slots (8 KiB each), so 16 KiB per wave are in flight while two windows are walked. One
-// wave per workgroup (32 KiB of LDS: 5 per CU). The wire is read from HBM once; the kernel writes
-// 3 bytes of records per 64 bytes and one claim per tile.
+// parsed and linked (~800 VALU instructions per 4 KiB wave, VALU-issue-bound). For sparse streams
+// (frames of more than HOP_FRAME bytes on average, decided per launch from walk_density's sample)
+// one LANE instead walks one REGION of consecutive interior tiles of a stream frame by frame, as
+// decode.js does: the entry of a region's first tile is found once (walk_sync: the first position
+// whose Change payload parses exactly in the schema's shape, or whose chain survives WK_K
+// frames), and every later frame start follows from its predecessor's header, one 16-byte load
+// per frame (claims_hop): a 4 KB value is never read by the claims. The kernel writes the records
+// of the 64-byte segments where a frame starts and one claim per tile.
 //
 // Regions never cross a stream and hold only interior tiles (A >= stream start, A + IMG <= stream
 // end); the edge tiles go to spec_claims' work list, as claims_fast sends them.
@@ -29,13 +24,6 @@
 namespace drp {
 namespace spec {
 
-#ifndef DRP_WK_WB
-#define DRP_WK_WB 128
-#endif
-constexpr uint32_t WK_WB = DRP_WK_WB;            // window bytes per region and step
-constexpr uint32_t WK_WPT = TILE / WK_WB;        // windows per tile
-constexpr uint32_t WK_GW = 512 / WK_WB;          // windows per group of 8 segment records
-constexpr uint32_t WK_LPR = WK_WB / 16;          // lanes of one DMA instruction per region
 constexpr uint32_t SY_NEAR = 256;                // a "near" sync chain's longest frame
 constexpr uint64_t SY_TAIL = 16384;              // a sync chain's tail counts this close to the stream end
 #ifndef DRP_SY_MERGE
@@ -45,26 +33,15 @@ constexpr uint64_t SY_MERGE = DRP_SY_MERGE;              // a region's entry bef
 constexpr uint64_t SY_SHAPE = 8192;              // how far a region's first shaped Change is looked for
 constexpr uint64_t SY_GENERAL = 2048;            // how far the general scan looks (else: no entry, the
                                                  // region's tiles claim identity and verification walks them)
-#ifndef DRP_WK_SLOTS
-#define DRP_WK_SLOTS 4
-#define DRP_WK_AHEAD 3
-#endif
 #ifndef DRP_WK_REGIONS
 #define DRP_WK_REGIONS 65536
 #endif
-constexpr uint32_t WK_SLOTS = DRP_WK_SLOTS;      // LDS ring slots
-constexpr uint32_t WK_AHEAD = DRP_WK_AHEAD;      // windows staged ahead of the one walked
-static_assert(WK_AHEAD == 2 || WK_AHEAD == 3, "the wait accounting below covers these");
-constexpr uint32_t WK_SLOT = WAVE * WK_WB;       // bytes per slot (8 KiB)
-constexpr uint32_t WK_NDMA = WK_SLOT / (WAVE * 16);  // DMA instructions per step (8)
 constexpr uint32_t WK_K = 8;                     // frames a sync chain must survive (no Change shape)
 constexpr uint32_t WK_REGIONS = DRP_WK_REGIONS;  // regions aimed at (one per resident lane)
 #ifndef DRP_HOP_REGIONS
 #define DRP_HOP_REGIONS 24576
 #endif
 constexpr uint32_t HOP_REGIONS = DRP_HOP_REGIONS;  // hop walkers: regions aimed at
-static_assert(WK_WB == 64 || WK_WB == 128, "windows of one or two segments");
-static_assert(WK_SLOTS >= WK_AHEAD + 1, "the ring holds the walked window, the next and the in-flight ones");
 
 enum : uint32_t { WM_WALK = 1, WM_DONE = 2 };
 
@@ -145,27 +122,6 @@ __global__ __launch_bounds__(1024) void walk_regions(DecodeParams P) {
   if (tid == 0) P.walk_rp[P.nstreams] = carry;
 }
 
-// ---- the walker -------------------------------------------------------------------------------
-struct WalkLds {
-  __attribute__((aligned(16))) uint32_t ring[WK_SLOTS * WK_SLOT / 4];
-};
-
-// dword of this lane's bytes at window-relative offset o (4-aligned, o < 2 * WK_WB: the window
-// walked and the next one), from the ring
-__device__ __forceinline__ uint32_t wk_rd(const WalkLds &S, uint32_t w, uint32_t o) {
-  const uint32_t slot = (w + o / WK_WB) % WK_SLOTS;
-  return S.ring[(slot * WK_SLOT + threadIdx.x * WK_WB + (o & (WK_WB - 1))) >> 2];
-}
-
-// the 8 bytes at window-relative offset o (o + 8 <= 2 * WK_WB + 4: the ring's two windows plus
-// one dword), little endian
-__device__ __forceinline__ uint64_t wk_rd8(const WalkLds &S, uint32_t w, uint32_t o) {
-  const uint32_t d = o & ~3u, sh = (o & 3u) * 8u;
-  const uint32_t a = wk_rd(S, w, d), b = wk_rd(S, w, d + 4), c = wk_rd(S, w, d + 8);
-  const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh), hi = __builtin_amdgcn_alignbit(c, b, sh);
-  return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-
 // 8 bytes at absolute position p from the batch (two aligned 8-byte loads; p + 16 <= nbytes).
 // The value is waited for here, in the caller's branch: left to the compiler, the wait (a
 // vmcnt(0), which also drains the ring's DMAs in flight) lands where the branch merges with the
@@ -206,21 +162,6 @@ __device__ __forceinline__ WHdr wk_hdr(uint64_t x) {  // (branch-free)
   h.id = ok ? (uint32_t)(x >> (8u * k)) & 0xFFu : 0xFFu;
   return h;
 }
-
-// Byte reader for the sync checks: this lane's windows w, w + 1 from the ring, anything else
-// from the batch (rare: Change fields past the next window).
-struct WkReader {
-  const WalkLds &S;
-  const uint8_t *g;
-  uint64_t W0, nbytes;
-  uint32_t w;
-  __device__ __forceinline__ uint64_t rd8(uint64_t p) const {
-    const uint64_t o = p - W0;
-    if (o + 12 <= 2 * WK_WB) return wk_rd8(S, w, (uint32_t)o);
-    if (p + 16 > nbytes) return 0;  // (past the batch: parses as nothing valid)
-    return g_rd8(g, p);
-  }
-};
 
 // Byte reader for the region syncs (walk_sync): the batch, read through the caches.
 struct GReader {
@@ -342,99 +283,11 @@ __device__ __forceinline__ uint32_t wk_live16(uint32_t a, uint32_t b, uint32_t c
   return (X | (M & ((X >> 1) | ((M >> 1) & (X >> 2))))) & 0xFFFFu;  // through 0, 1 or 2 MSB bytes
 }
 
-// ---- per-frame records for the record emission (emit_rec) ------------------------------------
-// One delivered frame as 32 bytes: what decode_change and the frame table write for it, so that
-// the emission expands records into columns without reading the wire again.
-//   x: payload offset from the tile's first byte (14 bits) | id << 14 | partial << 16 |
-//      DRP_F_SUBSET << 17 | DRP_F_VALUE << 18        y: payload length (clamped as the column)
-//   z: key_off | subset_off << 8 | key_len << 16     w: value_off | subset_len << 16
-//   then change, from, to (low 32 bits) and their bits 32..41 (10 bits each)
-// Only Change payloads in protocol-buffers' own shape are recorded ([subset] key change from to
-// [value], one-byte tags, lengths of < 2^28 in <= 4 bytes, numbers of < 2^42, the last field
-// ending the payload, every offset and length inside its field); any other frame makes its tile
-// take the wire-reading emission (emit_lean / emit_tiles), as does a region whose records
-// overflow its share of the record buffer.
-constexpr uint32_t WK_REC_BYTES = 64;  // the record buffer holds one record per this many wire bytes
-
-// a varint of <= n bytes from y (little endian): bytes used (0: none ends within n)
-__device__ __forceinline__ uint32_t wk_varint(uint64_t y, uint32_t n, uint64_t &v) {
-  const uint64_t tm = ~y & 0x808080808080ull & ((1ull << (8u * n)) - 1ull);
-  if (!tm) return 0;
-  const uint32_t kb = ((uint32_t)__builtin_ctzll(tm) >> 3) + 1u;
-  v = ((y & 0x7Full) | ((y >> 1) & 0x3F80ull) | ((y >> 2) & 0x1FC000ull) | ((y >> 3) & 0xFE00000ull) |
-       ((y >> 4) & 0x7F0000000ull) | ((y >> 5) & 0x3F800000000ull)) &
-      ((1ull << (7u * kb)) - 1ull);
-  return kb;
-}
-
-// One field at q: its tag byte must be `tag`, then a varint of <= n bytes (into v: 0 when there is
-// none) inside [q, end); returns the field's header bytes (tag + varint), and clears ok when the
-// field is not there. Computed without early exits: the record's checks below run as one
-// straight-line sequence (divergent early returns out of this parse were miscompiled into
-// records with zeroed numbers: change / to columns of 0 on every frame).
-__device__ __forceinline__ uint32_t wk_field(const WkReader &R, uint64_t q, uint64_t end, uint32_t tag, uint32_t n,
-                                             uint64_t &v, bool &ok) {
-  const uint64_t x = R.rd8(q);
-  v = 0;
-  const uint32_t kb = wk_varint(x >> 8, n, v);
-  ok = ok && q < end && (x & 0xFFu) == tag && kb != 0 && 1u + kb <= end - q;
-  return 1u + kb;
-}
-
-__device__ __forceinline__ bool wk_record(const WkReader &R, uint64_t po, uint64_t pl, uint4 &a, uint4 &b) {
-  const uint64_t end = po + pl;
-  uint64_t q = po, slen = 0, klen = 0, nc = 0, nf = 0, nt = 0, vlen = 0;
-  bool ok = true, sub = (R.rd8(q) & 0xFFu) == 0x0Au, sok = true;
-  const uint32_t sh = wk_field(R, q, end, 0x0Au, 4, slen, sok);  // subset (when its tag is there)
-  ok = !sub || (sok && slen <= end - q - sh && slen < 0x10000u);
-  const uint32_t soff = sub ? sh : 0u;
-  slen = sub ? slen : 0u;
-  q = sub && ok ? q + sh + slen : q;
-  const uint32_t kh = wk_field(R, q, end, 0x12u, 4, klen, ok);  // key
-  ok = ok && klen <= end - q - kh && klen < 0x10000u && q - po + kh < 0x100u;
-  const uint32_t koff = (uint32_t)(q - po) + kh;
-  q = ok ? q + kh + klen : end;
-  q += wk_field(R, q, end, 0x18u, 6, nc, ok);  // change
-  q += wk_field(R, q, end, 0x20u, 6, nf, ok);  // from
-  q += wk_field(R, q, end, 0x28u, 6, nt, ok);  // to
-  const bool val = ok && q != end;  // value: the last field
-  bool vok = true;
-  const uint32_t vh = wk_field(R, q, end, 0x32u, 4, vlen, vok);
-  ok = ok && (!val || (vok && vlen == end - q - vh && q - po + vh < 0x10000u));
-  const uint32_t fl = (sub ? DRP_F_SUBSET : 0u) | (val ? DRP_F_VALUE : 0u);
-  a.x |= fl << 17;
-  a.z = koff | (soff << 8) | ((uint32_t)klen << 16);
-  a.w = (val ? (uint32_t)(q - po) + vh : 0u) | ((uint32_t)slen << 16);
-  b.x = (uint32_t)nc;
-  b.y = (uint32_t)nf;
-  b.z = (uint32_t)nt;
-  b.w = (uint32_t)(nc >> 32) | ((uint32_t)(nf >> 32) << 10) | ((uint32_t)(nt >> 32) << 20);
-  return ok;
-}
-
-// s_waitcnt vmcnt(n) for a count known only at run time (wave-uniform): the largest immediate
-// <= n of a small set (waiting for more operations than needed is always safe)
-__device__ __forceinline__ void wk_wait_vm(uint32_t n) {
-  n = __builtin_amdgcn_readfirstlane(n);  // (scalar branches)
-  if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-  else if (n >= 28) asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
-  else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else if (n >= 22) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
-  else if (n >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-  else if (n >= 19) asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
-  else if (n >= 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 // Region r of the batch: its first tile (t0, at A0), its stream end, its windows, and for a
 // stream's first tile the exact entry.
 struct Region {
   uint64_t t0, A0, se, entry;
-  uint32_t nw;
+  uint32_t nt;  // interior tiles of the region
   bool exact;
 };
 __device__ __forceinline__ Region region_of(const DecodeParams &P, uint64_t r) {
@@ -454,7 +307,7 @@ __device__ __forceinline__ Region region_of(const DecodeParams &P, uint64_t r) {
   G.t0 = P.tile_prefix[s] + i0;
   G.A0 = I.base + i0 * TILE;
   G.se = I.se;
-  G.nw = (uint32_t)umin64(P.walk_tpr, I.i_lo + I.n - i0) * WK_WPT;
+  G.nt = (uint32_t)umin64(P.walk_tpr, I.i_lo + I.n - i0);
   G.exact = G.A0 == I.so;
   G.entry = I.so + (P.entry ? P.entry[s] : 0ull);
   return G;
@@ -637,7 +490,7 @@ __device__ __forceinline__ uint64_t sync_entry(const DecodeParams &P, const Regi
                                                uint64_t &t_shape) {
   if (G.exact) return G.entry;
   const GReader R{P.bytes, P.nbytes};
-  const uint64_t se = G.se, end = G.A0 + (uint64_t)(G.nw / WK_WPT) * TILE;
+  const uint64_t se = G.se, end = G.A0 + (uint64_t)G.nt * TILE;
   // the first shaped candidate (within SY_SHAPE bytes: a stream without Changes goes on to the
   // general scan soon), 128 bytes per lane and step
   uint64_t shaped = ~0ull;
@@ -756,232 +609,6 @@ __global__ __launch_bounds__(256) void walk_density(DecodeParams P) {
   }
 }
 
-// ---- the walkers -----------------------------------------------------------------------------
-// One lane per region, from its entry (walk_sync), frame by frame through the ring. A frame that
-// breaks the grammar ends the region's walk ("death": a mispredicted entry, or a protocol error):
-// its tile and the rest of the region claim identity, and verification walks them exactly.
-template <bool REC>
-__global__ __launch_bounds__(WAVE) void claims_walk(DecodeParams P) {
-  __shared__ WalkLds S;
-  const uint32_t lane = threadIdx.x;
-  const uint64_t nreg = P.walk_rp[P.nstreams];
-  const uint64_t r = (uint64_t)blockIdx.x * WAVE + lane;
-  if ((uint64_t)blockIdx.x * WAVE >= nreg || walk_hops(P)) return;  // (whole wave)
-  // ---- this lane's region ---------------------------------------------------------------------
-  uint64_t t0 = 0, A0 = 0, se = 0, pos = ~0ull;
-  uint64_t rbase = 0;  // this region's first record slot (P.rec_cap slots per region)
-  uint32_t nw = 0;
-  if (r < nreg) {
-    const Region G = region_of(P, r);
-    t0 = G.t0;
-    A0 = G.A0;
-    se = G.se;
-    nw = G.nw;
-    rbase = r * P.rec_cap;
-    pos = P.walk_entry[r];
-  }
-  uint32_t mode = pos != ~0ull ? WM_WALK : WM_DONE;
-  bool rs = true;  // the next frame noted restarts the records' chain
-  // ---- DMA addressing: instruction i stages regions 8 i .. 8 i + 7 (16 bytes per lane) ---------
-  uint64_t dA[WK_NDMA];
-#pragma unroll
-  for (uint32_t i = 0; i < WK_NDMA; i++) {
-    const int src = (int)(i * (WAVE / WK_LPR) + lane / WK_LPR);
-    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)A0, src, WAVE), hi = (uint32_t)__shfl((int)(uint32_t)(A0 >> 32), src, WAVE);
-    dA[i] = (((uint64_t)hi << 32) | lo) + (lane % WK_LPR) * 16u;
-  }
-  uint32_t nwmax = nw;
-#pragma unroll
-  for (uint32_t d = 1; d < WAVE; d <<= 1) nwmax = max(nwmax, (uint32_t)__shfl_xor((int)nwmax, d, WAVE));
-  nwmax = __builtin_amdgcn_readfirstlane(nwmax);
-  // (the LDS-DMA is issued from inline asm: the compiler would otherwise put a vmcnt(0) wait in
-  // front of every LDS read, since it cannot tell which slot a pending DMA writes; the one wait
-  // the ring needs is the counted one below)
-  const uint32_t ring0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)S.ring;
-  // The regions' windows w into the ring slot w % WK_SLOTS; returns the DMA instructions issued.
-  // Only the windows a walk may read are staged: from the one holding the region's next frame
-  // start on (a region whose frames are long skips the windows inside them; a finished one all).
-  // When every region needs it (dense streams: nearly every step), one unmasked form.
-  const uint64_t act = __ballot(nw != 0);
-  auto issue = [&](uint32_t w) -> uint32_t {
-    const uint32_t slot = w % WK_SLOTS;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the slot's last reads, a step ago, are done)
-    const uint64_t need = __ballot(w <= nw && mode == WM_WALK && pos < A0 + (uint64_t)(w + 1u) * WK_WB);
-    if (need == act) {  // (inactive lanes load bytes of the batch's first lines, unread)
-#pragma unroll
-      for (uint32_t i = 0; i < WK_NDMA; i++) {
-        const uint8_t *g = P.bytes + dA[i] + (uint64_t)w * WK_WB;
-        const uint32_t l = __builtin_amdgcn_readfirstlane(ring0 + slot * WK_SLOT + i * 1024u);
-        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
-      }
-      return WK_NDMA;
-    }
-    uint32_t n = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < WK_NDMA; i++) {
-      constexpr uint32_t RPI = WAVE / WK_LPR;  // regions per DMA instruction
-      const uint32_t sub = (uint32_t)(need >> (i * RPI)) & (uint32_t)((1ull << RPI) - 1u);
-      if (sub) {
-        n++;
-        if ((sub >> (lane / WK_LPR)) & 1u) {
-          const uint8_t *g = P.bytes + dA[i] + (uint64_t)w * WK_WB;
-          const uint32_t l = __builtin_amdgcn_readfirstlane(ring0 + slot * WK_SLOT + i * 1024u);
-          asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
-        }
-      }
-    }
-    return n;
-  };
-  uint32_t d_pre = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < WK_AHEAD; w++) d_pre = issue(w);
-  // segment records of the current 4-window group (8 segments: byte j = segment j)
-  uint64_t ent = ~0ull, fn = 0, fc = 0;
-  bool had = false;   // a chain frame started in the current tile
-  bool dead = false;  // the chain died in the current tile
-  uint64_t term = 0;  // MARK_TERM | p: the tail that ended the chain in the current tile
-  // records (P.rec): the next slot of the region, the current tile's first one, and whether every
-  // frame of the tile so far has one
-  uint32_t rnext = 0, rtile = 0;
-  bool rok = REC && mode == WM_WALK;
-  // vector-memory operations issued after the DMA of window w + 1 (loads, stores and DMAs count
-  // together, in issue order): the stores of the steps since and the DMAs issued since (lower
-  // bounds, so the wait below is never short)
-  uint32_t st2 = 0, st1 = 0, d1 = d_pre;
-#pragma unroll 1
-  for (uint32_t w = 0; w < nwmax; w++) {
-    const uint32_t d0 = issue(w + WK_AHEAD);
-    wk_wait_vm(WK_AHEAD == 3 ? st2 + d1 + st1 + d0 : st1 + d0);  // windows w and w + 1 have landed
-    const uint32_t q = w % WK_WPT;  // window of the tile (the same for every lane)
-    uint32_t nrec = 0;              // records this lane stored in this step
-    if (w < nw) {
-      const uint64_t W0 = A0 + (uint64_t)w * WK_WB, W1 = W0 + WK_WB;
-      const uint64_t T0 = A0 + (uint64_t)(w - q) * WK_WB;  // the tile's first byte
-      const WkReader R{S, P.bytes, W0, P.nbytes, w};
-      // a frame start p (in window w, so in the current group) into the segment records
-      auto note = [&](uint64_t p, uint32_t id, bool deliver) {
-        const uint32_t rp = (uint32_t)(p - T0), sh = 8u * ((rp >> 6) & 7u);
-        const uint64_t e = (uint64_t)((rp & 63u) | (rs ? 0x40u : 0u)) << sh;
-        const uint64_t m = ((ent >> sh) & 0xFFull) == 0xFFull ? 0xFFull << sh : 0ull;  // (the segment's first)
-        ent = (ent & ~m) | (e & m);
-        rs = false;
-        had = true;
-        fn += (uint64_t)(deliver ? 1u : 0u) << sh;
-        fc += (uint64_t)(deliver && id == 1u ? 1u : 0u) << sh;
-      };
-      // this frame's record
-      auto record = [&](uint32_t k, uint64_t L, uint32_t id, bool tail) {
-        uint4 a = make_uint4((uint32_t)(pos + k + 1u - T0) | (id << 14) | ((tail ? 1u : 0u) << 16),
-                             (uint32_t)umin64(L - 1u, 0xFFFFFFFFull), 0u, 0u),
-              b = make_uint4(0u, 0u, 0u, 0u);
-        rok = rnext < P.rec_cap && (id != 1u || wk_record(R, pos + k + 1u, L - 1u, a, b));
-        if (rok) {
-          uint4 *d = reinterpret_cast<uint4 *>(P.rec + (rbase + rnext) * 8u);
-          d[0] = a;
-          d[1] = b;
-          rnext++;
-          nrec++;
-        }
-      };
-      // The straight path: complete Change and blob frames (nearly every frame). A lane stops it
-      // at any other frame (a long varint, a header-only frame, a tail, a death), which the
-      // general step below takes, one frame, before the straight path resumes.
-#pragma unroll 1
-      while (__ballot(mode == WM_WALK && pos < W1)) {
-        bool go = mode == WM_WALK && pos < W1;
-#pragma unroll 1
-        while (go) {
-          const WHdr h = wk_hdr(wk_rd8(S, w, (uint32_t)(pos - W0)));
-          const bool plain = (h.k != 0u) & (h.id - 1u < 2u) & (h.L != 0u) & (h.L <= se - pos - h.k);
-          if (plain) {
-            note(pos, h.id, true);
-            if (REC && rok) record(h.k, h.L, h.id, false);
-            pos += h.k + h.L;
-          }
-          go = plain & (pos < W1);
-        }
-        if (mode != WM_WALK || pos >= W1) continue;
-        // the general step: one frame
-        const uint32_t o = (uint32_t)(pos - W0);
-        const WHdr h = wk_hdr(wk_rd8(S, w, o));
-        uint64_t L = h.L;
-        uint32_t k = h.k, id = h.id;
-        if (k == 0) {  // a length varint of 6..10 bytes: the exact grammar
-          const Hdr e = hdr_global(P.bytes, pos, se);
-          if (e.kind == H_VALID || e.kind == H_TAIL_CHANGE || e.kind == H_TAIL_BLOB) {
-            k = e.vlen;
-            L = e.L;
-            id = e.id;
-          } else {
-            id = 0xFF;  // (an error or a cut header: the chain ends)
-          }
-        }
-        if (id > 2u || (id != 0u && L == 0)) {  // the chain dies
-          dead = true;
-          mode = WM_DONE;
-          if (P.stats) {  // (DRP_STATS: deaths; the first one's bytes from LDS and from HBM)
-            if (atomicAdd(&P.stats[32], 1ull) == 0) {
-              P.stats[36] = pos;
-              P.stats[37] = wk_rd8(S, w, o);
-              P.stats[38] = g_rd8(P.bytes, pos);
-              P.stats[39] = ((uint64_t)w << 32) | (lane << 16) | o;
-            }
-          }
-        } else if (id == 0u) {
-          note(pos, 0u, false);
-          pos += k + 1u;
-        } else {
-          const bool tail = L > se - pos - k;  // the stream ends inside this frame
-          note(pos, id, !tail || id == 2u);    // (a cut Change is carried, a cut blob delivered)
-          if (REC && rok && (!tail || id == 2u)) record(k, L, id, tail);
-          if (tail) {
-            term = MARK_TERM | pos;
-            mode = WM_DONE;
-          } else {
-            pos += k + L;
-          }
-        }
-      }
-      if (q % WK_GW == WK_GW - 1) {  // flush the group's 8 segment records
-        const uint64_t ix = (t0 + w / WK_WPT) * NT + (q / WK_GW) * 8u;
-        *reinterpret_cast<uint64_t *>(P.ent + ix) = ent;
-        *reinterpret_cast<uint64_t *>(P.ent_n + ix) = fn;
-        *reinterpret_cast<uint64_t *>(P.ent_c + ix) = fc;
-        ent = ~0ull;
-        fn = 0;
-        fc = 0;
-      }
-      if (q == WK_WPT - 1) {  // the tile's claim
-        // (a dead tile's records mix two chains, which no record marks: identity, so verification
-        // re-walks it from its exact entry; the rest of the region is not walked)
-        uint64_t cl = C_ID;
-        if (term) cl = term;
-        else if (mode == WM_WALK && had) cl = pos;
-        if (dead) cl = C_ID;
-        P.claim[t0 + w / WK_WPT] = cl;
-        if (REC) {  // its first record (or none: the tile takes the wire-reading emission)
-          P.tile_rec[t0 + w / WK_WPT] = rok && !dead ? (uint32_t)(rbase + rtile) : REC_NONE;
-          rtile = rnext;
-          rok = rnext < P.rec_cap && !dead && mode == WM_WALK;
-        }
-        had = false;
-        term = 0;
-        dead = false;
-      }
-    }
-    // this step's stores (at least one lane is active: the one with nwmax windows)
-    uint32_t st = (q % WK_GW == WK_GW - 1 ? 3u : 0u) + (q == WK_WPT - 1 ? (REC ? 2u : 1u) : 0u);
-    if (REC) {
-#pragma unroll
-      for (uint32_t d = 1; d < WAVE; d <<= 1) nrec = max(nrec, (uint32_t)__shfl_xor((int)nrec, d, WAVE));
-      st += 2u * __builtin_amdgcn_readfirstlane(nrec);
-    }
-    st2 = st1;
-    st1 = st;
-    d1 = d0;
-  }
-}
-
 // ---- the hop walkers --------------------------------------------------------------------------
 // One lane per region, from its entry (walk_sync), frame to frame with a direct read of each
 // header (two 8-byte loads through the caches; nothing staged): a frame costs one dependent load
@@ -995,7 +622,7 @@ __global__ __launch_bounds__(256) void claims_hop(DecodeParams P) {
   if (r >= P.walk_rp[P.nstreams] || !walk_hops(P)) return;
   const Region G = region_of(P, r);
   const uint64_t A0 = G.A0, se = G.se;
-  const uint32_t ntr = G.nw / WK_WPT;       // tiles
+  const uint32_t ntr = G.nt;       // tiles
   const uint64_t end = A0 + (uint64_t)ntr * TILE;
   uint64_t pos = P.walk_entry[r];
   uint32_t mode = pos != ~0ull ? WM_WALK : WM_DONE;
@@ -1091,81 +718,24 @@ __global__ __launch_bounds__(256) void claims_hop(DecodeParams P) {
   close_to(ntr);
 }
 
-// ---- record emission ---------------------------------------------------------------------------
-// The tiles verification lets it take (tile_recok: every frame of the tile has a record and its
-// first record is the frame at e_t): rows [tile_base, + tile_count) from the tile's records, a wave
-// per tile, in XCD-contiguous order (neighbouring tiles' column lines meet in one L2). Reads
-// 32 bytes per row and writes the columns; the wire is not read again.
-constexpr uint32_t ER_WAVES = 4;
-__global__ __launch_bounds__(ER_WAVES * WAVE) void emit_rec(DecodeParams P) {
-  if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
-  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  uint64_t g;
-  {
-    const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = blockIdx.x % 8u;
-    g = (uint64_t)x * q + min(x, r) + blockIdx.x / 8u;
-  }
-  const uint64_t t = g * ER_WAVES + wid;
-  if (t >= P.tile_prefix[P.nstreams] || !P.tile_recok[t]) return;  // (whole wave)
-  const uint64_t base = P.tile_base[t], n = P.tile_count[t];
-  const uint64_t r0 = P.tile_rec[t];
-  const uint64_t A = tile_geo(P, t).A;
-#pragma unroll 1
-  for (uint64_t i = lane; i < n; i += WAVE) {
-    const uint64_t f = base + i;
-    if (f >= P.cap) break;
-    const uint4 *src = reinterpret_cast<const uint4 *>(P.rec + (r0 + i) * 8u);
-    const uint4 a = src[0], b = src[1];
-    const uint32_t id = (a.x >> 14) & 3u, fl = (a.x >> 17) & 3u;
-    P.payload_off[f] = A + (a.x & 0x3FFFu);
-    P.payload_len[f] = a.y;
-    P.type[f] = (uint8_t)(id | (((a.x >> 16) & 1u) ? DRP_FRAME_PARTIAL : 0u));
-    if (id != 1u) continue;
-    P.key_off[f] = a.z & 0xFFu;
-    P.subset_off[f] = (a.z >> 8) & 0xFFu;
-    P.key_len[f] = a.z >> 16;
-    P.value_off[f] = a.w & 0xFFFFu;
-    P.subset_len[f] = a.w >> 16;
-    P.value_len[f] = (fl & DRP_F_VALUE) ? a.y - (a.w & 0xFFFFu) : 0u;
-    P.change[f] = b.x | ((uint64_t)(b.w & 0x3FFu) << 32);
-    P.from[f] = b.y | ((uint64_t)((b.w >> 10) & 0x3FFu) << 32);
-    P.to[f] = b.z | ((uint64_t)((b.w >> 20) & 0x3FFu) << 32);
-    P.flags[f] = (uint8_t)fl;
-  }
-}
-
 }  // namespace spec
 }  // namespace drp
 
 using namespace drp;
 
-extern "C" hipError_t drp_launch_emit_rec(const DecodeParams *P, uint64_t nt_max, hipStream_t st) {
-  if (nt_max == 0 || !P->rec) return hipSuccess;
-  hipLaunchKernelGGL(spec::emit_rec, dim3((uint32_t)((nt_max + spec::ER_WAVES - 1) / spec::ER_WAVES)),
-                     dim3(spec::ER_WAVES * WAVE), 0, st, *P);
-  return hipGetLastError();
-}
-
-// record slots per region (P->rec_cap) for tpr tiles per region
-extern "C" uint64_t drp_walk_rec_cap(uint32_t tpr) { return (uint64_t)tpr * spec::TILE / spec::WK_REC_BYTES; }
-
-// Region walkers in place of claims_fast: the region list (and the edge tiles onto P->work), then
-// the walkers. P->walk_rp: nstreams + 1 words; P->walk_tpr: tiles per region.
+// Hop walkers in place of claims_fast: the region list (and the edge tiles onto P->work), the region
+// syncs, then the walkers. P->walk_rp: nstreams + 1 words; P->walk_tpr: tiles per region.
 extern "C" hipError_t drp_launch_claims_walk(const DecodeParams *P, uint64_t nt_max, hipStream_t st) {
   if (nt_max == 0) return hipSuccess;
   hipLaunchKernelGGL(spec::walk_regions, dim3(1), dim3(1024), 0, st, *P);
   const uint64_t maxr = nt_max / P->walk_tpr + P->nstreams + 1;
   hipLaunchKernelGGL(spec::walk_sync, dim3((uint32_t)((maxr * spec::SY_LANES + 255) / 256)), dim3(256), 0, st, *P);
-  if (P->walk_hop) {
-    const size_t nrec = (size_t)nt_max * spec::NT;  // (one record byte per 64-byte segment)
-    hipError_t e = hipMemsetAsync(P->ent, 0xFF, nrec, st);
-    if (e == hipSuccess) e = hipMemsetAsync(P->ent_n, 0, nrec, st);
-    if (e == hipSuccess) e = hipMemsetAsync(P->ent_c, 0, nrec, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(spec::claims_hop, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
-  }
-  if (P->walk_hop) return hipGetLastError();  // (2: dense batches take claims_fast, launched by the caller)
-  hipLaunchKernelGGL(spec::claims_walk<false>, dim3((uint32_t)((maxr + WAVE - 1) / WAVE)), dim3(WAVE), 0, st, *P);
+  const size_t nrec = (size_t)nt_max * spec::NT;  // (one record byte per 64-byte segment)
+  hipError_t e = hipMemsetAsync(P->ent, 0xFF, nrec, st);
+  if (e == hipSuccess) e = hipMemsetAsync(P->ent_n, 0, nrec, st);
+  if (e == hipSuccess) e = hipMemsetAsync(P->ent_c, 0, nrec, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(spec::claims_hop, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
   return hipGetLastError();
 }
 

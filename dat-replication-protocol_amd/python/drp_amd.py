@@ -26,6 +26,7 @@ EXPORTS = [
     "drp_last_timing", "drp_set_tile", "drp_set_strict", "drp_set_exact", "drp_set_key_post",
     "drp_set_blob_skip", "drp_decode_scratch_bytes",
     "drp_decode_device", "drp_decode_batch", "drp_decode_stage", "drp_decode_stage_v", "drp_decode_fetch", "drp_decode_fetch_block",
+    "drp_decode_fetch_block_ex",
     "drp_encode_size", "drp_encode_device",
     "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results", "drp_device",
     "drp_comm_id", "drp_comm_init_rank", "drp_comm_init_all", "drp_comm_destroy",
@@ -117,6 +118,7 @@ def lib():
                                          C.POINTER(U32), C.POINTER(U32)]
         L.drp_decode_fetch.argtypes = [P, C.POINTER(Frames), C.POINTER(Changes), U64, U64]
         L.drp_decode_fetch_block.argtypes = [P, P, U64, C.POINTER(U64), U64, U64]
+        L.drp_decode_fetch_block_ex.argtypes = [P, P, U64, C.POINTER(U64), U64, U64, U32]
         L.drp_encode_size.argtypes = [P, C.POINTER(ChangeSrc), U64, C.POINTER(U64)]
         L.drp_encode_device.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, P, U64]
         L.drp_encode_batch.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, U64,
@@ -285,12 +287,13 @@ class Ctx:
                    frame_bytes=int(carry.frame_bytes))
         return res
 
-    def decode_staged(self, wire, blob_remaining=0, pieces=1, key_hash=False, block=False):
+    def decode_staged(self, wire, blob_remaining=0, pieces=1, key_hash=False, block=False, f64=False):
         """drp_decode_stage, then drp_decode_fetch of the rows in `pieces` consecutive
         fetches into host columns sized from the frame count (the N-API addon's path). `wire`
         as a list of byte strings: the batch is those chunks end to end (drp_decode_stage_v).
         block=True: one drp_decode_fetch_block of every row into one host block instead (the
-        columns at 64-byte aligned offsets, as the addon lays them out)."""
+        columns at 64-byte aligned offsets, as the addon lays them out); f64=True: with
+        drp_decode_fetch_block_ex(DRP_FETCH_F64), payload_off / change / from / to as float64."""
         carry = Carry(blob_remaining, 0, 0, 0, 0)
         nf, ef, ec, ed = U64(), U64(), U32(), U32()
         _chk("drp_set_key_post", self.L.drp_set_key_post(self.h, KEY_POST_HASH if key_hash else KEY_POST_OFF))
@@ -310,13 +313,18 @@ class Ctx:
             names = ["payload_off", "payload_len", "type"] + COLS32 + COLS64 + ["flags"] + (["key_hash"] if key_hash else [])
             dt = {"payload_off": np.uint64, "payload_len": np.uint32, "type": np.uint8, "flags": np.uint8,
                   "key_hash": np.uint64, **{k: np.uint32 for k in COLS32}, **{k: np.uint64 for k in COLS64}}
+            if f64:
+                dt.update({k: np.float64 for k in ["payload_off"] + COLS64})
             offs, at = [], 0
             for k in names:
                 offs.append(at)
                 at += (rows * np.dtype(dt[k]).itemsize + 8 + 63) & ~63
             blk = np.full(at + 64, 0xAB, np.uint8)
             col_off = (U64 * 14)(*(offs + [~0 & 0xFFFFFFFFFFFFFFFF] * (14 - len(offs))))
-            _chk("drp_decode_fetch_block", self.L.drp_decode_fetch_block(self.h, _p(blk), at, col_off, 0, rows))
+            if f64:
+                _chk("drp_decode_fetch_block_ex", self.L.drp_decode_fetch_block_ex(self.h, _p(blk), at, col_off, 0, rows, 1))
+            else:
+                _chk("drp_decode_fetch_block", self.L.drp_decode_fetch_block(self.h, _p(blk), at, col_off, 0, rows))
             o = {k: blk[a:a + rows * np.dtype(dt[k]).itemsize].view(dt[k]) for k, a in zip(names, offs)}
             pieces = 0
         else:

@@ -263,6 +263,13 @@ int drp_decode_fetch(drp_ctx *ctx, const drp_frames *frames, const drp_changes *
 #define DRP_FETCH_COLS 14
 int drp_decode_fetch_block(drp_ctx *ctx, void *block, uint64_t block_bytes, const uint64_t *col_off, uint64_t first,
                            uint64_t rows);
+/* drp_decode_fetch_block with column forms for a JavaScript host: flags DRP_FETCH_F64 writes
+ * payload_off, change, from and to as IEEE doubles (the Numbers decode.js hands out: exact below
+ * 2^53, the nearest double above, as a host (double) cast rounds), converted on the device before
+ * the transfer. flags 0: drp_decode_fetch_block. */
+#define DRP_FETCH_F64 1u
+int drp_decode_fetch_block_ex(drp_ctx *ctx, void *block, uint64_t block_bytes, const uint64_t *col_off,
+                              uint64_t first, uint64_t rows, uint32_t flags);
 /* drp_decode_stage over a batch the caller holds as chunks (its queued writes), laid end to end:
  * the caller never concatenates them. The ranges the decode stages into HBM (all of the batch,
  * or with blob skipping everything but the blob payloads) are gathered from the chunks into

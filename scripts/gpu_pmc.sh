@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC counter passes over one workload's decode (one rocprofv3 run per pass, as the pool requires).
-# Usage: gpurun --timeout 900 -- 'bash scripts/gpu_pmc.sh [frames] [c2|c4|c5] [outdir]'; summary:
+# Usage: gpurun --timeout 900 -- 'bash scripts/gpu_pmc.sh [frames] [c2|c3|c4|c5] [outdir]'; summary:
 # scripts/pmc_kernels.py (c5: the C5 round trip, 1M Changes: encode + decode kernels; c4: 8192 streams)
 set -e
 export TMPDIR=/tmp
@@ -8,6 +8,8 @@ F=${1:-20000000}
 W=${2:-c2}
 D=${3:-gpurun_out/pmc}
 mkdir -p $D
+# (c3: the host-batch decode of a ~1 GiB C3 stream, warmup 1 + 1 step = 2 whole decode calls:
+# pmc_kernels.py --calls 2 divides the kernels' totals by 2 x the stream's frames)
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d $D/$name -o run -- \

@@ -90,7 +90,8 @@ for step in "$@"; do
         [ -d "$d" ] || continue
         w=$(basename $d)
         w=${w#pmc_}
-        python3 scripts/pmc_kernels.py --dir $d --workload $w --write $OUT/pmc_$w.json > $OUT/pmc_$w.txt 2>&1 || true
+        python3 scripts/pmc_kernels.py --dir $d --workload $w $([ $w = c3 ] && echo --calls 2) --write $OUT/pmc_$w.json \
+          > $OUT/pmc_$w.txt 2>&1 || true
       done
       T=($OUT/prof/*kernel_trace.csv)
       if [ -f "${T[0]}" ]; then python3 scripts/trace_phases.py ${T[0]} 7 > $OUT/kernel_phases.txt 2>&1 || true; fi

@@ -1,6 +1,6 @@
 """Per-kernel PMC summary of scripts/gpu_pmc.sh passes (gpurun_out/pmc/<pass>/): average per dispatch
 and per frame, FETCH_SIZE doubled per the gfx950 note (MI355X_MICROARCH.md: 128-B requests
-tallied at 64 B). Usage: python scripts/pmc_kernels.py [frames (default: from the passes' bench lines)] [--dir gpurun_out/pmc] [--workload c2|c4|c5]
+tallied at 64 B). Usage: python scripts/pmc_kernels.py [frames (default: from the passes' bench lines)] [--dir gpurun_out/pmc] [--workload c2|c3|c4|c5] [--calls N]
 [--write profiles/pmc_<workload>.json] (c5: the encode kernels are counted too: its roofline prices the
 round trip)"""
 import collections
@@ -14,7 +14,11 @@ sys.path.insert(0, ROOT)
 from bench import DECODE_PATH as KNAME, decode_code_hash  # noqa: E402  (bench.py's kernel name and source hash)
 PMC_DIR = sys.argv[sys.argv.index("--dir") + 1] if "--dir" in sys.argv else "gpurun_out/pmc"
 WORKLOAD = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else "c2"
-opt_vals = {sys.argv[sys.argv.index(o) + 1] for o in ("--dir", "--write", "--workload") if o in sys.argv}
+# --calls N: the passes ran N whole decode calls of `frames` frames each, in dispatches of varying
+# sizes (C3: a host batch staged in pieces); per-frame figures are then the kernels' totals over
+# all dispatches / (frames x N), not per-dispatch averages
+CALLS = float(sys.argv[sys.argv.index("--calls") + 1]) if "--calls" in sys.argv else None
+opt_vals = {sys.argv[sys.argv.index(o) + 1] for o in ("--dir", "--write", "--workload", "--calls") if o in sys.argv}
 args = [a for a in sys.argv[1:] if not a.startswith("--") and a not in opt_vals]
 
 
@@ -33,6 +37,8 @@ def frames_from_logs():
                 m = re.match(r"C5: (\d+) Changes", cfg.get("workload", ""))
                 if m:
                     return float(m.group(1))
+                if cfg.get("workload", "").startswith("C3") and "frames" in cfg:
+                    return float(cfg["frames"])
     return None
 
 
@@ -50,7 +56,7 @@ for f in glob.glob(PMC_DIR + "/*/**/*counter_collection.csv", recursive=True):
 kern = sorted({k for k, _ in tot})
 per = {}
 for k in kern:
-    avg = {c: tot[(kk, c)] / len(disp[(kk, c)]) for kk, c in tot if kk == k}
+    avg = {c: tot[(kk, c)] / (CALLS if CALLS else len(disp[(kk, c)])) for kk, c in tot if kk == k}
     if "FETCH_SIZE" in avg:
         avg["FETCH_SIZE"] *= 2
     w = avg.get("SQ_WAVES", 0)

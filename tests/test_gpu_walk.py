@@ -1,7 +1,8 @@
-"""GPU parity of the region walkers (drp_walk.hip, the claims kernel of large batches) against the
-oracle. Every context here forces the walkers for batches of any size (DRP_CLAIMS=walk,
+"""GPU parity of the hop walkers (drp_walk.hip, the claims kernel of large sparse batches) against
+the oracle. Every context here forces the walkers for batches of any size (DRP_CLAIMS=hop,
 read by drp_open), so a test's small input runs them with one tile per region; the default
-path takes them from DRP_WALK_MIN tiles on (test_gpu_configs.py's full-size C2/C4/C5).
+path takes them from DRP_WALK_MIN tiles on when frames average more than 512 bytes
+(test_gpu_configs.py's full-size C5).
 
 The walkers only predict: verify_lite / verify_counts prove every claim on the exact chain, so a
 wrong prediction costs repair passes, never a wrong row. The parity tests below compare rows;
@@ -23,8 +24,8 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-# the walkers under test: "walk" (ring walkers) or "hop" (hop walkers); DRP_TEST_WALKERS picks
-WALKERS = os.environ.get("DRP_TEST_WALKERS", "walk")
+# the claims form under test (DRP_CLAIMS): "hop" (the hop walkers) or "fast" (claims_fast)
+WALKERS = os.environ.get("DRP_TEST_WALKERS", "hop")
 
 
 def walk_ctx(**env):

@@ -1,8 +1,6 @@
-"""CPU check of the region walkers' per-frame record parser (drp_walk.hip wk_varint / wk_field /
-wk_record, compiled here as host C++ from the kernel's own source text): every Change payload it
-accepts gets exactly the columns the oracle's Change decode (protocol-buffers@2 restated) gives,
-and every payload in its shape is accepted. The GPU tests then check the whole record emission
-(tests/test_gpu_walk.py)."""
+"""CPU checks of the region syncs' prefilters (drp_walk.hip wk_shape16 / sync_pairs136, compiled
+here as host C++ from the kernel's own source text): they mark exactly the positions their
+contracts say, so the syncs never miss a shaped Change header."""
 import os
 import random
 import re
@@ -18,40 +16,6 @@ import _streams as S
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "dat-replication-protocol_amd", "csrc", "drp_walk.hip")
 
-HARNESS = r"""
-#include <cstdint>
-#include <cstdio>
-#include <cstring>
-struct uint4 { uint32_t x, y, z, w; };
-#define __device__
-#define __forceinline__
-#define DRP_F_SUBSET 1
-#define DRP_F_VALUE 2
-static const uint8_t *G;
-struct WkReader { uint64_t rd8(uint64_t p) const { uint64_t x; memcpy(&x, G + p, 8); return x; } };
-%s
-int main(int argc, char **argv) {
-  FILE *f = fopen(argv[1], "rb");
-  fseek(f, 0, SEEK_END);
-  long n = ftell(f);
-  fseek(f, 0, SEEK_SET);
-  static uint8_t *buf = new uint8_t[n + 64]();
-  if (fread(buf, 1, n, f) != (size_t)n) return 1;
-  fclose(f);
-  G = buf;
-  WkReader R;
-  FILE *g = fopen(argv[2], "r");
-  unsigned long long po, pl;
-  while (fscanf(g, "%%llu %%llu", &po, &pl) == 2) {
-    uint4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
-    const bool ok = wk_record(R, po, pl, a, b);
-    printf("%%d %%u %%u %%u %%u %%u %%u %%u %%u\n", ok, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w);
-  }
-  return 0;
-}
-"""
-
-
 def functions(src, names):
     out = []
     for nm in names:
@@ -59,72 +23,6 @@ def functions(src, names):
         assert m, nm
         out.append(m.group(0))
     return "\n".join(out)
-
-
-@pytest.fixture(scope="module")
-def parser():
-    src = open(SRC).read()
-    code = HARNESS % functions(src, ["wk_varint", "wk_field", "wk_record"])
-    d = tempfile.mkdtemp()
-    cpp, exe = os.path.join(d, "rec.cpp"), os.path.join(d, "rec")
-    open(cpp, "w").write(code)
-    subprocess.run(["g++", "-O1", "-o", exe, cpp], check=True)
-    return exe, d
-
-
-def records(parser, wire, frames):
-    exe, d = parser
-    wp, fp = os.path.join(d, "wire.bin"), os.path.join(d, "frames.txt")
-    open(wp, "wb").write(wire)
-    with open(fp, "w") as f:
-        for po, pl in frames:
-            f.write(f"{po} {pl}\n")
-    out = subprocess.run([exe, wp, fp], capture_output=True, text=True, check=True).stdout.split("\n")
-    return [list(map(int, ln.split())) for ln in out if ln]
-
-
-@pytest.mark.parametrize("seed", range(4))
-def test_records_match_change_decode(parser, seed):
-    rng = random.Random(seed)
-    wire = S.random_stream(rng, 2500, blob_p=0.05) + S.c2_stream(300).tobytes() + S.c5_stream(rng, 20)
-    r = O.decode_batch(wire)
-    ch = np.flatnonzero((r["type"] & 0x3F) == 1)
-    recs = records(parser, wire, [(int(r["payload_off"][i]), int(r["payload_len"][i])) for i in ch])
-    recorded = 0
-    for i, (ok, ax, ay, az, aw, bx, by, bz, bw) in zip(ch, recs):
-        # in the record's shape: canonical field order (the oracle decodes no error), numbers < 2^42
-        fits = max(int(r["change"][i]), int(r["from"][i]), int(r["to"][i])) < 2 ** 42 and r["flags"][i] & 0x0C == 0
-        assert bool(ok) == fits, (i, ok, fits)
-        if not ok:
-            continue
-        recorded += 1
-        fl = (ax >> 17) & 3
-        got = {"key_off": az & 0xFF, "subset_off": (az >> 8) & 0xFF, "key_len": az >> 16,
-               "value_off": aw & 0xFFFF, "subset_len": aw >> 16,
-               "value_len": int(r["payload_len"][i]) - (aw & 0xFFFF) if fl & 2 else 0,
-               "change": bx | ((bw & 0x3FF) << 32), "from": by | (((bw >> 10) & 0x3FF) << 32),
-               "to": bz | (((bw >> 20) & 0x3FF) << 32), "flags": fl}
-        for k, v in got.items():
-            assert int(r[k][i]) == v, (i, k, int(r[k][i]), v)
-    assert recorded > 1000
-
-
-def test_records_reject_other_shapes(parser):
-    """Payloads outside the record's shape (field order, wire types, unknown fields, empty, a
-    value that does not end the payload) are not recorded: their tiles take the wire-reading
-    emission, whose general decoder handles them."""
-    bad = [b"", b"\x18\x01\x12\x01k\x20\x02\x28\x03", b"\x12\x01k\x18\x01\x20\x02",  # empty, order, no `to`
-           b"\x12\x01k\x18\x01\x20\x02\x28\x03\x38\x01",  # an unknown field
-           b"\x12\x01k\x18\x01\x20\x02\x28\x03\x32\x05ab",  # a value past the payload
-           b"\x10\x01\x18\x01\x20\x02\x28\x03",  # the key with a varint wire type
-           b"\x12\x01k\x18\x01\x20\x02\x28\x03\x32\x01a\x32\x01b"]  # a repeated value
-    wire, frames = b"", []
-    for p in bad:
-        wire += S.frame(p)
-        frames.append((len(wire) - len(p), len(p)))
-    wire += b"\0" * 32
-    for (ok, *_), p in zip(records(parser, wire, frames), bad):
-        assert ok == 0, p
 
 
 SHAPE_HARNESS = r"""
