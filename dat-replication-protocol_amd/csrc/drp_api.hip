@@ -185,7 +185,7 @@ struct drp_ctx {
   // claims_fast below; DRP_CLAIMS=walk / fast forces one (A/B, tests)
   uint64_t walk_min = 32768;
   int claims_mode = 0;  // 0 auto, 2 fast, 3 hop
-  int crec = 0;         // claims_fast's per-frame records and the record emission (DRP_CREC)
+  int crec = 1;         // claims_fast's per-frame records and the record emission (DRP_CREC=0: off)
   DevBuf recbuf;
   uint64_t dirty_cap = ~0ull;
   bool stats = false;
@@ -665,8 +665,10 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   }
   // claims_fast's per-frame records (fast_records, 24 B per frame slot): emit_lean expands them into
   // columns without reading the wire again (DRP_CREC=0: off; a buffer that cannot be had: off)
-  if (c->crec && c->recbuf.ensure(NT * drp_spec_rec_words() * 4ull)) {
+  const uint64_t rec_bytes = (NT * drp_spec_rec_words() * 4ull + 255) & ~255ull;
+  if (c->crec && c->recbuf.ensure(rec_bytes + (cap / 64 + 2) * 4)) {
     P.rec = c->recbuf.at<uint32_t>(0);
+    P.chunk_tile = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(c->recbuf.p) + rec_bytes);
     P.tile_rec = c->scratch.at<uint32_t>(L.trec);
     P.tile_recok = c->scratch.at<uint8_t>(L.trok);
   }

@@ -542,12 +542,15 @@ constexpr uint16_t NX_NEAR = 0xFFFD, NX_FAR = 0xFFFE, NX_DEAD = 0xFFFF;
 #endif
 // the fast form (below), which spec_claims also runs for the stream-edge tiles on its list
 struct FastLds;
+// spec_claims' image buffer: the tile's image, or the edge form's FastLds (whose own image for the
+// per-frame records is IMG + 32 bytes, plus its frame list and the small words)
+constexpr uint32_t SPEC_BUF = IMG + 32 + 4 * DRP_SPEC_NT + 256;
 enum : uint32_t { FC_OK = 0, FC_DENSE = 1 };
-template <bool CF, bool EDGE = false>
+template <bool CF, bool EDGE = false, bool REC = false>
 __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const TileGeo &G, uint64_t t, FastLds &S,
                                                 uint32_t &eb_o, uint32_t &en_o, uint32_t &ecn_o, uint64_t &cl_o);
 __global__ __launch_bounds__(NT, DRP_K1G_WAVES) void spec_claims(DecodeParams P) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[IMG + 32];
+  __shared__ __attribute__((aligned(16))) uint8_t buf[SPEC_BUF];
   __shared__ uint64_t xr[NT / WAVE];
   __shared__ uint32_t xf[NT / WAVE];
   __shared__ uint64_t lmw[NT];
@@ -1048,15 +1051,23 @@ constexpr uint32_t HV = HALO / SEGB;  // halo "threads" with nodes
 // of 5: the HBM stream of some workgroups overlaps the instruction-bound work of others
 // (C2 100M: 3.37 -> ~2.8 ms; C5: 3.77 -> ~2.4 ms).
 struct FastLds {
-  uint64_t lmw[NT + HV];   // live masks; then strong masks
-  uint64_t dmw[NT];        // undecided masks
-  uint16_t loff[NT + HV];  // first list index of each thread
-  uint32_t hmx[HALO / 16 + 1];  // halo masks per 16 bytes
-  uint16_t lpos[FCAP];
-  uint32_t lnd[FCAP > NT + 1 ? FCAP : NT + 1];  // nodes (first: the next-16-byte masks; last: the emit list)
-  uint8_t lal[FCAP];  // 0 dead, 1 strong, 2 undecided (leaves the image)
-  uint32_t lsucc[FCAP];  // successor offset of the nodes whose frame leaves the list (the claim of a
-                         // chain that ends in one: no header re-read from HBM at the tile's end)
+  union {
+    struct {
+      uint64_t lmw[NT + HV];   // live masks; then strong masks
+      uint64_t dmw[NT];        // undecided masks
+      uint16_t loff[NT + HV];  // first list index of each thread
+      uint32_t hmx[HALO / 16 + 1];  // halo masks per 16 bytes
+      uint16_t lpos[FCAP];
+      uint32_t lnd[FCAP > NT + 1 ? FCAP : NT + 1];  // nodes (first: the next-16-byte masks; last: the emit list)
+      uint8_t lal[FCAP];  // 0 dead, 1 strong, 2 undecided (leaves the image)
+      uint32_t lsucc[FCAP];  // successor offset of the nodes whose frame leaves the list (the claim of a
+                             // chain that ends in one: no header re-read from HBM at the tile's end)
+    };
+    // the per-frame records' image of the tile and its halo, staged from the registers of the tile
+    // load once the frames are listed (fast_records: everything above is dead by then)
+    __attribute__((aligned(16))) uint8_t img[IMG + 32];
+  };
+  uint32_t fls[NT];  // fast_records: the tile's delivered frames in chain order (offset | id << 14 | tailb << 16)
   uint32_t xw[8];
   uint32_t xf[2 * NT / WAVE], wl[NT / WAVE], fl[NT / WAVE];
   uint64_t xm[4];  // candidate masks (two waves): [w] strong, [2 + w] strong and far
@@ -1064,7 +1075,7 @@ struct FastLds {
   uint8_t pad[DRP_K1_PAD];  // (A/B only: caps the workgroups per CU through LDS)
 #endif
 };
-static_assert(sizeof(FastLds) <= IMG + 32, "spec_claims runs the edge form in its image buffer");
+static_assert(sizeof(FastLds) <= SPEC_BUF, "spec_claims runs the edge form in its image buffer");
 
 
 // claims_fast when the link rounds do not settle within DRP_FL_CAP rounds (two chains that never
@@ -1319,10 +1330,14 @@ __device__ __forceinline__ bool crec_frame(const uint32_t *w32, uint32_t o, uint
 
 // Records of the tile's delivered frames (after the claim; whole workgroup). E / nf: this thread's
 // settled entry and frame count (0 for a non-carrier), exactly as its per-thread record has them.
+// v / hv: this thread's 64 bytes of the tile and (threads < HALO / 16) 16 bytes of the halo, still
+// in the registers of the tile load: they become an LDS image of the tile (over the node tables,
+// dead once the frames are listed), so the field decode reads no memory (re-reading the tile from
+// the batch at this point, long after its load, cost claims_fast ~135 B per frame of fabric reads).
 __device__ __forceinline__ void fast_records(const DecodeParams &P, uint64_t t, FastLds &S, uint32_t E, uint32_t nf,
-                                             uint32_t s1r, uint32_t se_rel, const uint32_t *w32) {
+                                             uint32_t s1r, uint32_t se_rel, const uint4 (&v)[SEGB / 16],
+                                             const uint4 &hv) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-  uint16_t *fls = reinterpret_cast<uint16_t *>(S.lal);  // (free after the survival rounds)
   const uint32_t ip = wave_scan_dpp(nf);
   if (lane == 63) S.xw[4 + wid] = ip;
   bsync();
@@ -1336,7 +1351,7 @@ __device__ __forceinline__ void fast_records(const DecodeParams &P, uint64_t t, 
       const uint32_t nd = S.lnd[i], id = nd >> 30, c = nd & 0xFFFFu, q = (nd >> 16) & 0x3FFFu;
       if (id == 3u || c == NX_TAILC) break;
       if (id != 0u) {
-        if (cnt < nf) fls[slot + cnt] = (uint16_t)i;
+        if (cnt < nf) S.fls[slot + cnt] = (uint32_t)S.lpos[i] | (id << 14) | ((c == NX_TAILB ? 1u : 0u) << 16);
         cnt++;
       }
       if (c >= NX_TAILB || q >= s1r) break;  // (NX_TAILB, NX_TAILC, NX_NEAR, NX_FAR, NX_DEAD)
@@ -1344,13 +1359,19 @@ __device__ __forceinline__ void fast_records(const DecodeParams &P, uint64_t t, 
     }
     bad = cnt != nf;
   }
-  bsync();
+  bsync();  // (the node tables are dead: the image goes over them)
   if (DRP_CREC_STAGE == 0) return;
+  uint4 *im = reinterpret_cast<uint4 *>(S.img);
+#pragma unroll
+  for (uint32_t k = 0; k < SEGB / 16; k++) im[tid * (SEGB / 16) + k] = v[k];
+  if (tid < HALO / 16) im[TILE / 16 + tid] = hv;
+  if (tid < 2) im[IMG / 16 + tid] = make_uint4(0, 0, 0, 0);  // (the slack: no stale bytes)
+  bsync();
   if (tid < tot && !bad) {
-    const uint32_t i = fls[tid];
-    const uint32_t nd = S.lnd[i];
+    const uint32_t f = S.fls[tid];
     uint32_t w[CR_WORDS];
-    bad = !crec_frame(w32, S.lpos[i], se_rel, nd >> 30, (nd & 0xFFFFu) == NX_TAILB, w);
+    bad = !crec_frame(reinterpret_cast<const uint32_t *>(S.img), f & 0x3FFFu, min(se_rel, IMG), (f >> 14) & 3u,
+                      (f >> 16) & 1u, w);
     uint32_t *rr = P.rec + t * CR_TILE_WORDS + tid;
     if (DRP_CREC_STAGE == 1) {  // (A/B: keep the decode, store nothing)
       if ((w[0] ^ w[2] ^ w[3] ^ w[4] ^ w[5]) == 0x7FFFFFFFu && !bad) rr[0] = w[1];
@@ -1386,7 +1407,7 @@ __device__ __forceinline__ uint64_t range_bits(uint32_t base, uint32_t lo, uint3
 // stream's exact entry on, its end before), the last 3 positions before se always listed and
 // every header whose 16-byte window crosses se parsed by the exact grammar (a header cut by the
 // stream end is a tail, as parse_win has it); FC_DENSE lists nothing (the caller goes on).
-template <bool CF, bool EDGE>
+template <bool CF, bool EDGE, bool REC>
 __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const TileGeo &G, uint64_t t, FastLds &S,
                                                 uint32_t &eb_o, uint32_t &en_o, uint32_t &ecn_o, uint64_t &cl_o) {
   uint8_t *buf = nullptr;
@@ -1775,7 +1796,7 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
     P.claim[t] = cl;
     cl_o = cl;
   }
-  if (!EDGE && P.rec) fast_records(P, t, S, E, en_o, s1r, se_rel, w32);
+  if (!EDGE && REC) fast_records(P, t, S, E, en_o, s1r, se_rel, v, hv);
   return FC_OK;
 }
 
@@ -1787,8 +1808,11 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
 #ifndef DRP_K1_PERSIST
 #define DRP_K1_PERSIST 0  // (A/B: workgroups per CU of a persistent claims grid; 0: a workgroup per tile)
 #endif
-template <bool CF>
-__global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) {
+#ifndef DRP_K1_REC_WAVES
+#define DRP_K1_REC_WAVES 7  // min waves per SIMD for claims_fast with records (the tile's registers live to the end)
+#endif
+template <bool CF, bool REC>
+__global__ __launch_bounds__(NT, REC ? DRP_K1_REC_WAVES : DRP_K1_WAVES) void claims_fast(DecodeParams P) {
   __shared__ FastLds S;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
 #if DRP_K1_PERSIST  // (A/B: a persistent grid; measured slower, its loop spills registers)
@@ -1801,7 +1825,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
     }
     uint32_t eb, en, ecn;
     uint64_t cl;
-    (void)fast_claims<CF>(P, G, t, S, eb, en, ecn, cl);
+    (void)fast_claims<CF, false, REC>(P, G, t, S, eb, en, ecn, cl);
   }
 #else
   const uint64_t t = blockIdx.x;
@@ -1813,7 +1837,7 @@ __global__ __launch_bounds__(NT, DRP_K1_WAVES) void claims_fast(DecodeParams P) 
   }
   uint32_t eb, en, ecn;
   uint64_t cl;
-  (void)fast_claims<CF>(P, G, t, S, eb, en, ecn, cl);
+  (void)fast_claims<CF, false, REC>(P, G, t, S, eb, en, ecn, cl);
 #endif
 }
 
@@ -2727,79 +2751,82 @@ __device__ __forceinline__ void st_col(T *base, uint32_t i, T v) {
 // ---- record emission: columns from claims_fast's per-frame records (fast_records) -------------
 // The tiles verification lets it take (tile_recok = 1 + the slot of the tile's first row): rows
 // [tile_base, + tile_count) from slot tile_recok - 1 on. Reads 24 B per row and writes the columns;
-// the wire is not read again. Four tiles per workgroup in XCD-contiguous order (neighbouring
-// tiles' column lines meet in one L2); a small kernel (no LDS, few registers) so that many tiles'
-// loads are in flight per CU.
-constexpr uint32_t ER_WAVES = 4, ER_RPL = CR_CAP / WAVE;  // tiles (waves) per workgroup, rows per lane
-static_assert(CR_CAP % WAVE == 0, "a lane's rows are slots lane, lane + 64, ...");
-__device__ __forceinline__ void emit_rec_row(const RowCols &C, uint64_t A, uint32_t s, uint32_t w0, uint32_t pl,
+// the wire is not read again.
+// one row (i: relative to C's first row): its columns from the record words (the tile's first
+// byte at A)
+__device__ __forceinline__ void emit_rec_row(const RowCols &C, uint32_t i, uint64_t A, uint32_t w0, uint32_t pl,
                                              uint32_t w2, uint32_t n0, uint32_t n1, uint32_t n2) {
   const uint32_t id = (w0 >> 14) & 3u;
-  st_col(C.poff, s, A + (w0 & 0x3FFFu));
-  st_col(C.plen, s, pl);
-  st_col(C.type, s, (uint8_t)(id | (((w0 >> 16) & 1u) ? DRP_FRAME_PARTIAL : 0u)));
+  st_col(C.poff, i, A + (w0 & 0x3FFFu));
+  st_col(C.plen, i, pl);
+  st_col(C.type, i, (uint8_t)(id | (((w0 >> 16) & 1u) ? DRP_FRAME_PARTIAL : 0u)));
   if (id != 1u) return;
   const uint32_t hv = (w0 >> 17) & 1u, vo = hv ? w2 >> 16 : 0u;
-  st_col(C.ko, s, 1u + ((w0 >> 18) & 3u));
-  st_col(C.kl, s, w2 & 0xFFFFu);
-  st_col(C.so, s, 0u);
-  st_col(C.sl, s, 0u);
-  st_col(C.vo, s, vo);
-  st_col(C.vl, s, hv ? pl - vo : 0u);
-  st_col(C.ch, s, (uint64_t)n0);
-  st_col(C.fr, s, (uint64_t)n1);
-  st_col(C.to, s, (uint64_t)n2);
-  st_col(C.fl, s, (uint8_t)(hv ? DRP_F_VALUE : 0u));
+  st_col(C.ko, i, 1u + ((w0 >> 18) & 3u));
+  st_col(C.kl, i, w2 & 0xFFFFu);
+  st_col(C.so, i, 0u);
+  st_col(C.sl, i, 0u);
+  st_col(C.vo, i, vo);
+  st_col(C.vl, i, hv ? pl - vo : 0u);
+  st_col(C.ch, i, (uint64_t)n0);
+  st_col(C.fr, i, (uint64_t)n1);
+  st_col(C.to, i, (uint64_t)n2);
+  st_col(C.fl, i, (uint8_t)(hv ? DRP_F_VALUE : 0u));
 }
-// ER_TPW tiles per wave (their meta by scalar loads, issued together), every record word of the
-// lane's rows of all of them loaded before any column is stored: a wave has two round trips to
-// memory in all, and its bytes in flight cover them.
-#ifndef DRP_ER_TPW
-#define DRP_ER_TPW 2
-#endif
-constexpr uint32_t ER_TPW = DRP_ER_TPW;
+// Output rows in chunks of 64, each chunk's stores starting at a 64-row boundary of the columns
+// (scripts/probe_bw.hip: 62 B-per-row column stores run at 5.8 TB/s from 64-aligned chunks and at
+// 2.9 TB/s from chunks shifted off that boundary). chunk_tiles first marks, per chunk, the tile
+// holding its first row; the rows of a chunk then lie in that tile and the ones up to the next
+// chunk's. A wave per chunk: its lanes' rows, their tiles (the first or the next one in the fast
+// path, else a search over the tiles' first rows), and for a tile with records (tile_recok) the
+// row's record words, loaded before the row is stored. Rows of tiles without records are left to
+// emit_lean.
+__global__ __launch_bounds__(256) void chunk_tiles(DecodeParams P) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (t >= P.tile_prefix[P.nstreams]) return;
+  const uint64_t b = P.tile_base[t], n = P.tile_count[t];
+  if (!n || b >= P.cap) return;
+  const uint64_t e = umin64(b + n, P.cap);
+  for (uint64_t c = (b + 63) / 64; c * 64 < e; c++) P.chunk_tile[c] = (uint32_t)t;
+}
+
+constexpr uint32_t ER_WAVES = 4;  // chunks (waves) per workgroup
 __global__ __launch_bounds__(ER_WAVES * WAVE) void emit_recs(DecodeParams P) {
   if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
-  uint64_t b;
-  {
-    const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = blockIdx.x % 8u;
-    b = (uint64_t)x * q + min(x, r) + blockIdx.x / 8u;
-  }
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t t0 = (b * ER_WAVES + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * ER_TPW;
+  const uint64_t c = (uint64_t)blockIdx.x * ER_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t ntiles = ldc(P.tile_prefix + P.nstreams);
-  uint32_t rk[ER_TPW], lim[ER_TPW];
-  uint64_t base[ER_TPW];
-#pragma unroll
-  for (uint32_t i = 0; i < ER_TPW; i++) {
-    const uint64_t t = t0 + i;
-    rk[i] = t < ntiles ? ldc(P.tile_recok + t) : 0u;
-    const uint32_t n = t < ntiles ? (uint32_t)ldc(P.tile_count + t) : 0u;
-    base[i] = t < ntiles ? ldc(P.tile_base + t) : 0ull;
-    lim[i] = rk[i] ? min(n, base[i] >= P.cap ? 0u : (uint32_t)umin64(P.cap - base[i], 0xFFFFFFFFull)) : 0u;
-  }
-  uint32_t w[ER_TPW][ER_RPL][CR_WORDS];
-#pragma unroll
-  for (uint32_t i = 0; i < ER_TPW; i++) {
-    const uint32_t *rr = P.rec + (t0 + i) * CR_TILE_WORDS + (rk[i] - 1u);
-#pragma unroll
-    for (uint32_t j = 0; j < ER_RPL; j++) {
-      const uint32_t s = lane + j * WAVE;
-#pragma unroll
-      for (uint32_t k = 0; k < CR_WORDS; k++) w[i][j][k] = s < lim[i] ? rr[k * CR_CAP + s] : 0u;
+  if (!ntiles) return;
+  const uint64_t total = umin64(ldc(P.tile_base + ntiles - 1) + ldc(P.tile_count + ntiles - 1), P.cap);
+  if (c * 64 >= total) return;  // (whole wave)
+  const uint64_t r = c * 64 + lane;
+  const uint64_t t0 = ldc(P.chunk_tile + c);
+  const uint64_t t1 = (c + 1) * 64 < total ? (uint64_t)ldc(P.chunk_tile + c + 1) : ntiles - 1;
+  // this lane's tile: the last tile in [t0, t1] whose first row is <= r
+  uint64_t t = t0;
+  const uint64_t b1 = t1 > t0 ? ldc(P.tile_base + t0 + 1) : ~0ull;
+  if (t1 == t0 + 1 || t1 == t0) {  // (nearly always: tiles of more than 64 rows)
+    if (r >= b1) t = t0 + 1;
+  } else if (r >= b1) {  // (tiles of few rows, or runs of empty tiles: search)
+    uint64_t lo = t0 + 1, hi = t1;  // base[lo] <= r; find the last such
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi + 1) >> 1;
+      if (P.tile_base[mid] <= r) lo = mid;
+      else hi = mid - 1;
     }
+    t = lo;
   }
+  if (r >= total) return;
+  const uint32_t rk = P.tile_recok[t];
+  if (!rk) return;  // (emit_lean writes this row)
+  const uint64_t bt = P.tile_base[t];
+  const uint32_t *rr = P.rec + t * CR_TILE_WORDS + (uint32_t)(r - bt) + rk - 1u;
+  uint32_t w[CR_WORDS];
 #pragma unroll
-  for (uint32_t i = 0; i < ER_TPW; i++) {
-    if (!lim[i]) continue;
-    const uint64_t A = tile_geo(P, t0 + i).A;
-    const RowCols C = row_cols(P, base[i]);
-#pragma unroll
-    for (uint32_t j = 0; j < ER_RPL; j++) {
-      const uint32_t s = lane + j * WAVE;
-      if (s < lim[i]) emit_rec_row(C, A, s, w[i][j][0], w[i][j][1], w[i][j][2], w[i][j][3], w[i][j][4], w[i][j][5]);
-    }
-  }
+  for (uint32_t k = 0; k < CR_WORDS; k++) w[k] = rr[k * CR_CAP];
+  const uint64_t A = tile_geo(P, t).A;
+  const RowCols C = row_cols(P, c * 64);
+  emit_rec_row(C, lane, A, w[0], w[1], w[2], w[3], w[4], w[5]);
 }
 
 struct LeanLds {
@@ -3715,10 +3742,15 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
     drp_dbg_mark("claims_walk", st);
   } else {
     const uint64_t g = DRP_K1_PERSIST ? std::min<uint64_t>(nt_max, 256ull * DRP_K1_PERSIST) : nt_max;
-    if (Q.change_checks && !P->walk_rp)
-      hipLaunchKernelGGL(spec::claims_fast<true>, dim3((uint32_t)g), dim3(spec::NT), 0, st, Q);
+    const bool cf = Q.change_checks && !P->walk_rp;
+    if (cf && Q.rec)
+      hipLaunchKernelGGL((spec::claims_fast<true, true>), dim3((uint32_t)g), dim3(spec::NT), 0, st, Q);
+    else if (cf)
+      hipLaunchKernelGGL((spec::claims_fast<true, false>), dim3((uint32_t)g), dim3(spec::NT), 0, st, Q);
+    else if (Q.rec)
+      hipLaunchKernelGGL((spec::claims_fast<false, true>), dim3((uint32_t)g), dim3(spec::NT), 0, st, Q);
     else
-      hipLaunchKernelGGL(spec::claims_fast<false>, dim3((uint32_t)g), dim3(spec::NT), 0, st, Q);
+      hipLaunchKernelGGL((spec::claims_fast<false, false>), dim3((uint32_t)g), dim3(spec::NT), 0, st, Q);
   }
   drp_dbg_mark("claims_fast", st);
   const uint32_t gw = (uint32_t)(nt_max < 16384 ? nt_max : 16384);
@@ -3809,9 +3841,12 @@ extern "C" hipError_t drp_launch_spec_tail(const DecodeParams *P, uint64_t nt_ma
       Q.tile_sparse = nullptr;
     }
     if (Q.rec)  // (the tiles with records; emit_lean skips them)
-      hipLaunchKernelGGL(spec::emit_recs,
-                         dim3((uint32_t)((nt_max + spec::ER_WAVES * spec::ER_TPW - 1) / (spec::ER_WAVES * spec::ER_TPW))),
+    {
+      hipLaunchKernelGGL(spec::chunk_tiles, dim3((uint32_t)((nt_max + 255) / 256)), dim3(256), 0, st, Q);
+      const uint64_t nchunks = (Q.cap + 63) / 64;
+      hipLaunchKernelGGL(spec::emit_recs, dim3((uint32_t)((nchunks + spec::ER_WAVES - 1) / spec::ER_WAVES)),
                          dim3(spec::ER_WAVES * WAVE), 0, st, Q);
+    }
     hipLaunchKernelGGL(spec::emit_lean,
                        dim3((uint32_t)(Q.change_checks || Q.rec ? (nt_max + spec::EMIT_LONG_TPW - 1) / spec::EMIT_LONG_TPW
                                                                 : nt_max)),

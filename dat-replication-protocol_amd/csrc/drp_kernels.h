@@ -86,6 +86,7 @@ struct DecodeParams {
   uint32_t *rec;
   uint32_t *tile_rec;
   uint8_t *tile_recok;
+  uint32_t *chunk_tile;  // per 64 output rows: the tile holding the first (emit_recs' aligned row chunks)
   unsigned long long *stats;  // optional event counters (DRP_STATS=1), see drp_decode.hip
   unsigned long long *trace;  // optional per-tile timestamps (DRP_TRACE_FILE, with DRP_STATS)
 };

@@ -92,6 +92,9 @@ var NOTHING = { n: 0, errCode: 0, tailKind: 0, consumed: 0, blobRemaining: 0, fr
 //                    a BigInt, computed on the GPU (drp_keys.hip)
 //   device: k      - the GPU this stream decodes on (default: DRP_DEVICE or 0); independent
 //                    streams are spread over a node's GPUs this way (index.js: shard)
+//   codecErrors    - 'event': a Change the codec rejects destroys the stream with an 'error'
+//                    event; by default it is thrown, as the reference's Change.decode throws
+//                    (decode.js:210): out of write() or the handler callback that led to it
 //   highWaterMark  - the Writable's highWaterMark. Default MAX_BATCH (64 MiB), a deliberate
 //                    divergence from the reference (Node's default, 16 KiB): a producer that
 //                    honours write()'s return value stops at the highWaterMark, and the writes
@@ -102,6 +105,10 @@ function Decoder (opts) {
   if (!(this instanceof Decoder)) return new Decoder(opts)
   var hwm = opts && opts.highWaterMark !== undefined ? opts.highWaterMark : MAX_BATCH
   stream.Writable.call(this, { highWaterMark: hwm })
+  // a Change the codec rejects: thrown, as the reference's Change.decode throws (default), or
+  // emitted as an 'error' event that destroys the stream (opts.codecErrors === 'event')
+  this._codecEvents = !!(opts && opts.codecErrors === 'event')
+  this._broken = false
   this._keyPost = !!(opts && opts.keyHash)
 
   this.destroyed = false
@@ -382,6 +389,7 @@ Decoder.prototype._gather = function (batch, a, b) {
 // Deliver frames of the front batch while no callback is outstanding, up to the end of the
 // write being consumed; then acknowledge that write (decode.js:144-169).
 Decoder.prototype._deliver = function () {
+  if (this._broken) return // (a codec exception was thrown: see _replay)
   while (!this.destroyed && this._pending <= 0) {
     var batch = this._batches[0]
     var slot = this._slots[0]
@@ -515,7 +523,18 @@ Decoder.prototype._replay = function (batch, lim) {
   }
   if (i < n) return true // (the rest completes in later writes)
   if (res.errCode && this._errPos(batch) < lim) {
-    this.destroy(new Error(ERRORS[res.errCode](res.errDetail)))
+    var err = new Error(ERRORS[res.errCode](res.errDetail))
+    if ((res.errCode === 4 || res.errCode === 5) && !this._codecEvents) {
+      // a Change the codec rejects: messages.Change.decode throws inside the reference's
+      // _onchangeend (decode.js:205-214), so the exception leaves whatever drove the delivery
+      // (the write() that handed the bytes over, or the handler's callback that resumed it; here
+      // also the GPU batch's completion) and the stream is left as it was: nothing more is
+      // delivered and no event is emitted (tests/golden/ref_throws.json, recorded from the reference)
+      this._halt = true
+      this._broken = true
+      throw err
+    }
+    this.destroy(err)
     return false
   }
   if (batch.tooBig && batch.size <= lim) {

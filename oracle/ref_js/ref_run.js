@@ -12,6 +12,8 @@
 //              {op:'blob', len, writes:[hex,...]} | {op:'finalize'}]
 //   node ref_run.js acks <wire file> <write sizes> <burst|paced>
 //        -> the callback order of tests/js/ack_driver.js (write acknowledgements vs async handlers)
+//   node ref_run.js throws <wire file> <write sizes> <burst|paced>   (DRP_REF_CODEC=strict)
+//        -> how a rejected Change surfaces (tests/js/throw_driver.js)
 //   node ref_run.js bench <wire file> <chunk> <seconds>   (DRP_REF_CODEC=full)
 //        -> JSON {frames_per_s, bytes_per_s, frames, reps}
 'use strict'
@@ -133,6 +135,12 @@ if (cmd === 'decode') {
 } else if (cmd === 'acks') { // node ref_run.js acks <wire file> <write sizes> <burst|paced>
   require(path.join(__dirname, '..', '..', 'tests', 'js', 'ack_driver.js'))(protocol, fs.readFileSync(process.argv[3]),
     process.argv[4].split(',').map(Number), process.argv[5], function (log) { process.stdout.write(JSON.stringify(log) + '\n') })
+} else if (cmd === 'throws') { // node ref_run.js throws <wire file> <write sizes> <burst|paced> (DRP_REF_CODEC=strict)
+  require(path.join(__dirname, '..', '..', 'tests', 'js', 'throw_driver.js'))(protocol, fs.readFileSync(process.argv[3]),
+    process.argv[4].split(',').map(Number), process.argv[5], function (log) {
+      process.stdout.write(JSON.stringify(log) + '\n')
+      process.exit(0)
+    })
 } else if (cmd === 'bench') {
   bench(fs.readFileSync(process.argv[3]), Number(process.argv[4]), Number(process.argv[5]))
 } else {

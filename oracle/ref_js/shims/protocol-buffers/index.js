@@ -8,6 +8,8 @@
 //   full                  - a restatement of the generated proto2 decoder (switch on tag,
 //                           unknown fields skipped by wire type, last wins), used to time the
 //                           reference path for the calibration ratio.
+//   strict                - passthrough results, but it throws as the generated decoder does for
+//                           a payload missing a required field (the codec-throw fixtures).
 // Change.encode (both modes) writes present fields in field-number order, as the generated
 // encoder does.
 'use strict'
@@ -76,8 +78,28 @@ function decodePassthrough (buf) {
   return { payload: Buffer.from(buf) }
 }
 
+// strict: decodeFull, then the generated decoder's required-field check (protocol-buffers@2 throws
+// Error('Decoded message is not valid') when a required field is missing): used to record how the
+// reference's FRAMING surfaces a codec throw (tests/golden/make_throw_fixtures.py)
+function decodeStrict (buf) {
+  var seen = {}
+  var off = 0
+  while (off < buf.length) {
+    var prefix = varint.decode(buf, off)
+    if (varint.decode.bytes === 0) throw new Error('Decoded message is not valid')
+    off += varint.decode.bytes
+    var tag = prefix >> 3
+    seen[tag] = true
+    var l = (prefix & 7) === 2 ? varint.decode(buf, off) : 0
+    if ((prefix & 7) === 2) off += varint.decode.bytes + l
+    else { varint.decode(buf, off); off += varint.decode.bytes }
+  }
+  if (!seen[2] || !seen[3] || !seen[4] || !seen[5]) throw new Error('Decoded message is not valid')
+  return decodePassthrough(buf)
+}
+
 module.exports = function (schema) {
   checkSchema(schema)
-  var full = process.env.DRP_REF_CODEC === 'full'
-  return { Change: { encode: encode, decode: full ? decodeFull : decodePassthrough } }
+  var mode = process.env.DRP_REF_CODEC
+  return { Change: { encode: encode, decode: mode === 'full' ? decodeFull : mode === 'strict' ? decodeStrict : decodePassthrough } }
 }

@@ -26,8 +26,8 @@ struct Cols {
   uint64_t *poff; uint32_t *plen; uint8_t *type; uint32_t *ko, *kl, *so, *sl, *vo, *vl; uint64_t *ch, *fr, *to; uint8_t *fl;
   const uint32_t *rec;  // 6 words per row, word-major per 128-row tile (null: no reads)
 };
-__global__ void cols(Cols c, uint64_t n) {
-  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+__global__ void cols(Cols c, uint64_t n, uint32_t shift) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x + shift;  // (shift: rows not 64-aligned per wave)
   if (i >= n) return;
   uint32_t w[6] = {(uint32_t)i, 84, 10u | (22u << 16), 7, 8, 9};
   if (c.rec) {
@@ -90,8 +90,10 @@ int main() {
   c.sl = (uint32_t *)take(N * 4); c.vo = (uint32_t *)take(N * 4); c.vl = (uint32_t *)take(N * 4);
   c.ch = (uint64_t *)take(N * 8); c.fr = (uint64_t *)take(N * 8); c.to = (uint64_t *)take(N * 8); c.fl = take(N);
   c.rec = nullptr;
-  timeit("cols", N * 62.0, [&] { hipLaunchKernelGGL(cols, dim3((uint32_t)(N / 256)), dim3(256), 0, 0, c, N); });
+  timeit("cols", N * 62.0, [&] { hipLaunchKernelGGL(cols, dim3((uint32_t)(N / 256)), dim3(256), 0, 0, c, N, 0u); });
+  timeit("cols_mis", N * 62.0, [&] { hipLaunchKernelGGL(cols, dim3((uint32_t)(N / 256) - 1), dim3(256), 0, 0, c, N, 37u); });
   c.rec = (const uint32_t *)a;
-  timeit("cols_rd", N * 86.0, [&] { hipLaunchKernelGGL(cols, dim3((uint32_t)(N / 256)), dim3(256), 0, 0, c, N); });
+  timeit("cols_rd", N * 86.0, [&] { hipLaunchKernelGGL(cols, dim3((uint32_t)(N / 256)), dim3(256), 0, 0, c, N, 0u); });
+  timeit("cols_rd_mis", N * 86.0, [&] { hipLaunchKernelGGL(cols, dim3((uint32_t)(N / 256) - 1), dim3(256), 0, 0, c, N, 37u); });
   return 0;
 }

@@ -576,3 +576,54 @@ def test_high_water_mark_option():
     assert out["retained"] == 0, out
     assert out["queueLength"] < 130, out
     assert out["changes"] > 300 * 1000, out
+
+
+def _throw_cases():
+    with open(os.path.join(ROOT, "tests", "golden", "ref_throws.json")) as f:
+        return json.load(f)["cases"]
+
+
+def run_throws(case, mock):
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(bytes.fromhex(case["wire"]))
+        path = f.name
+    env = dict(os.environ)
+    if mock:
+        env["DRP_MOCK_NATIVE"] = "1"
+    try:
+        return json.loads(subprocess.check_output(
+            [NODE, os.path.join(JS, "throw_order.js"), path, ",".join(map(str, case["sizes"])), case["pattern"]],
+            text=True, timeout=120, env=env).strip().splitlines()[-1])
+    finally:
+        os.unlink(path)
+
+
+def _same_surfacing(got, want, name):
+    """Equal logs, except that where the reference throws out of write() (the write whose bytes hold
+    the rejected Change was decoded synchronously inside it), the package's exception leaves the
+    GPU batch's completion callback instead: a write's bytes are decoded after write() returns."""
+    assert len(got) == len(want), (name, got, want)
+    for g, w in zip(got, want):
+        if w.startswith("throw") and not w.startswith("throw-end") and g.startswith("uncaught:"):
+            assert g.split(":", 1)[1] == w.split(":", 1)[1], (name, g, w)
+        else:
+            assert g == w, (name, got, want)
+
+
+@needs_node
+def test_codec_throw_surfaces_as_in_the_reference_cpu():
+    """A Change the codec rejects (a missing required field) surfaces as the reference's
+    Change.decode throw does (tests/golden/ref_throws.json, recorded from the reference with a
+    strict codec shim): the same frames delivered and acknowledged before it, the same message,
+    thrown out of the handler callback that resumed delivery, no 'error' or 'close' event, nothing
+    delivered after it. JS layer over the CPU stand-in addon."""
+    for case in _throw_cases():
+        _same_surfacing(run_throws(case, mock=True), case["log"], case["name"])
+
+
+@pytest.mark.gpu
+@needs_node
+def test_codec_throw_surfaces_as_in_the_reference():
+    """As test_codec_throw_surfaces_as_in_the_reference_cpu, through the addon and the GPU."""
+    for case in _throw_cases():
+        _same_surfacing(run_throws(case, mock=False), case["log"], case["name"])
