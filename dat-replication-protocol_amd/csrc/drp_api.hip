@@ -1038,8 +1038,8 @@ static uint64_t stage_cap(const drp_ctx *c, uint64_t m) {
   return (uint64_t)((double)m * dens) + 1024;
 }
 
-constexpr uint64_t kGatherSeg = 16ull << 20, kGatherMin = 16ull << 20;  // (h2d_range's parallel gather)
-constexpr unsigned kGatherThreads = 8;
+constexpr uint64_t kGatherSeg = 4ull << 20, kGatherMin = 4ull << 20;  // (h2d_range's parallel gather)
+constexpr unsigned kGatherThreads = 4;
 // Batch bytes [a, a + len) into device memory at dst (asynchronously on st). A chunked batch's
 // range is gathered into the ctx's page-locked buffer first (*copied counts those host bytes),
 // so the copy into HBM runs by DMA and only the staged ranges are ever copied on the host.

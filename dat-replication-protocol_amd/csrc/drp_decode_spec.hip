@@ -1805,9 +1805,6 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
 // for its first), and large batches take the hop walkers instead when walk_density's sample says
 // the stream is sparse; dense streams (C2) are predicted as well without it, and its code costs
 // them ~4% (DESIGN.md "Long frames").
-#ifndef DRP_K1_PERSIST
-#define DRP_K1_PERSIST 0  // (A/B: workgroups per CU of a persistent claims grid; 0: a workgroup per tile)
-#endif
 #ifndef DRP_K1_REC_WAVES
 #define DRP_K1_REC_WAVES 7  // min waves per SIMD for claims_fast with records (the tile's registers live to the end)
 #endif
@@ -1815,20 +1812,8 @@ template <bool CF, bool REC>
 __global__ __launch_bounds__(NT, REC ? DRP_K1_REC_WAVES : DRP_K1_WAVES) void claims_fast(DecodeParams P) {
   __shared__ FastLds S;
   const uint64_t ntiles = P.tile_prefix[P.nstreams];
-#if DRP_K1_PERSIST  // (A/B: a persistent grid; measured slower, its loop spills registers)
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    bsync();  // (the previous tile's LDS reads are done)
-    const TileGeo G = tile_geo(P, t);
-    if (G.A < G.so || G.A + IMG > G.se) {  // edge tile: the general kernel
-      push_work(P, t);
-      continue;
-    }
-    uint32_t eb, en, ecn;
-    uint64_t cl;
-    (void)fast_claims<CF, false, REC>(P, G, t, S, eb, en, ecn, cl);
-  }
-#else
   const uint64_t t = blockIdx.x;
+  if (REC && t == 0 && threadIdx.x == 0) P.counter[13] = 1u;  // (records may exist: emit_recs runs)
   const TileGeo G = tile_geo(P, t);
   if (t >= ntiles) return;  // (whole workgroup)
   if (G.A < G.so || G.A + IMG > G.se) {  // edge tile: the general kernel
@@ -1838,7 +1823,6 @@ __global__ __launch_bounds__(NT, REC ? DRP_K1_REC_WAVES : DRP_K1_WAVES) void cla
   uint32_t eb, en, ecn;
   uint64_t cl;
   (void)fast_claims<CF, false, REC>(P, G, t, S, eb, en, ecn, cl);
-#endif
 }
 
 // ==== kernel 2: exact entries, verification, frame counts =====================================
@@ -2782,6 +2766,7 @@ __device__ __forceinline__ void emit_rec_row(const RowCols &C, uint32_t i, uint6
 // row's record words, loaded before the row is stored. Rows of tiles without records are left to
 // emit_lean.
 __global__ __launch_bounds__(256) void chunk_tiles(DecodeParams P) {
+  if (!P.counter[13]) return;  // (claims_fast wrote no records: the hop walkers' claims)
   const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (t >= P.tile_prefix[P.nstreams]) return;
   const uint64_t b = P.tile_base[t], n = P.tile_count[t];
@@ -2793,6 +2778,7 @@ __global__ __launch_bounds__(256) void chunk_tiles(DecodeParams P) {
 constexpr uint32_t ER_WAVES = 4;  // chunks (waves) per workgroup
 __global__ __launch_bounds__(ER_WAVES * WAVE) void emit_recs(DecodeParams P) {
   if (*P.overflow & (F_MISS | F_WAIT)) return;  // (a failed prediction: emitted after its repair)
+  if (!P.counter[13]) return;                     // (claims_fast wrote no records)
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t c = (uint64_t)blockIdx.x * ER_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t ntiles = ldc(P.tile_prefix + P.nstreams);
@@ -3741,7 +3727,7 @@ extern "C" hipError_t drp_launch_spec_head(const DecodeParams *P, uint64_t nt_ma
     if (e != hipSuccess) return e;
     drp_dbg_mark("claims_walk", st);
   } else {
-    const uint64_t g = DRP_K1_PERSIST ? std::min<uint64_t>(nt_max, 256ull * DRP_K1_PERSIST) : nt_max;
+    const uint64_t g = nt_max;
     const bool cf = Q.change_checks && !P->walk_rp;
     if (cf && Q.rec)
       hipLaunchKernelGGL((spec::claims_fast<true, true>), dim3((uint32_t)g), dim3(spec::NT), 0, st, Q);
