@@ -10,7 +10,6 @@
 #include <cstring>
 #include <ctime>
 #include <algorithm>
-#include <atomic>
 #include <chrono>
 #include <thread>
 #include <unistd.h>
@@ -1038,8 +1037,6 @@ static uint64_t stage_cap(const drp_ctx *c, uint64_t m) {
   return (uint64_t)((double)m * dens) + 1024;
 }
 
-constexpr uint64_t kGatherSeg = 4ull << 20, kGatherMin = 4ull << 20;  // (h2d_range's parallel gather)
-constexpr unsigned kGatherThreads = 4;
 // Batch bytes [a, a + len) into device memory at dst (asynchronously on st). A chunked batch's
 // range is gathered into the ctx's page-locked buffer first (*copied counts those host bytes),
 // so the copy into HBM runs by DMA and only the staged ranges are ever copied on the host.
@@ -1053,48 +1050,14 @@ static int h2d_range(drp_ctx *c, const HostSrc &H, uint64_t a, uint64_t len, voi
   if (!c->gather.ensure(len)) return DRP_E_NOMEM;
   CHK(hipStreamSynchronize(st));  // (the buffer's previous range has left)
   uint8_t *g = static_cast<uint8_t *>(c->gather.p);
-  // bytes [x, x + n) of the batch into g at x - a, chunk by chunk
-  auto gather = [&](uint64_t x, uint64_t n) {
-    uint64_t k = (uint64_t)(std::upper_bound(H.start.begin(), H.start.end(), x) - H.start.begin()) - 1;
-    for (uint64_t at = x, end = x + n; at < end; k++) {
-      const uint64_t s0 = H.start[k], take = std::min(end, s0 + H.ch[k].n) - at;
-      memcpy(g + (at - a), H.ch[k].bytes + (at - s0), take);
-      at += take;
-    }
-  };
+  uint64_t k = (uint64_t)(std::upper_bound(H.start.begin(), H.start.end(), a) - H.start.begin()) - 1;
+  for (uint64_t at = a, end = a + len; at < end; k++) {
+    const uint64_t s0 = H.start[k], take = std::min(end, s0 + H.ch[k].n) - at;
+    memcpy(g + (at - a), H.ch[k].bytes + (at - s0), take);
+    at += take;
+  }
   *copied += len;
-  // A large range: kGatherThreads threads copy a slice of each kGatherSeg segment each, and the DMA
-  // of a segment is queued as soon as its slices are in, while the next one is gathered (one
-  // thread's memcpy into pinned memory ran at ~13 GB/s: the Node path's 64 KiB writes, 344 MB in
-  // 25 ms).
-  const uint64_t nseg = (len + kGatherSeg - 1) / kGatherSeg;
-  const unsigned nthr = len >= kGatherMin ? kGatherThreads : 1u;
-  if (nthr == 1) {
-    gather(a, len);
-    CHK(hipMemcpyAsync(dst, g, len, hipMemcpyHostToDevice, st));
-    return DRP_OK;
-  }
-  std::vector<std::atomic<unsigned>> done(nseg);
-  for (auto &d : done) d.store(0, std::memory_order_relaxed);
-  std::vector<std::thread> pool;
-  pool.reserve(nthr);
-  for (unsigned w = 0; w < nthr; w++)
-    pool.emplace_back([&, w]() {
-      for (uint64_t s = 0; s < nseg; s++) {
-        const uint64_t s0 = a + s * kGatherSeg, sn = std::min(kGatherSeg, a + len - s0);
-        const uint64_t lo = s0 + sn * w / nthr, hi = s0 + sn * (w + 1) / nthr;
-        if (hi > lo) gather(lo, hi - lo);
-        done[s].fetch_add(1, std::memory_order_release);
-      }
-    });
-  hipError_t e = hipSuccess;
-  for (uint64_t s = 0; s < nseg; s++) {
-    while (done[s].load(std::memory_order_acquire) < nthr) std::this_thread::yield();
-    const uint64_t o = s * kGatherSeg, sn = std::min(kGatherSeg, len - o);
-    if (e == hipSuccess) e = hipMemcpyAsync(static_cast<uint8_t *>(dst) + o, g + o, sn, hipMemcpyHostToDevice, st);
-  }
-  for (auto &th : pool) th.join();
-  CHK(e);
+  CHK(hipMemcpyAsync(dst, g, len, hipMemcpyHostToDevice, st));
   return DRP_OK;
 }
 
