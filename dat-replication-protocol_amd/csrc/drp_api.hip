@@ -197,6 +197,8 @@ struct drp_ctx {
   PinBuf gather;  // chunked host batches: the staged ranges, gathered (drp_decode_stage_v)
   DevBuf dec_cols;  // device columns of the staged host-batch decode (drp_decode_stage)
   DevBuf fetch_tmp; // drp_decode_fetch_block: the caller's block layout, packed on the device
+  DevBuf keybuf;    // drp_decode_fetch_keys: per-row key lengths and positions
+  DevBuf keytext;   // drp_decode_fetch_keys: the key text
   double frames_per_byte = 0;  // density of the last staged batch (sizes the next one's columns)
   int blob_skip = DRP_BLOB_SKIP_AUTO;
   bool blob_heavy = false;     // the last host batch was mostly blob payload (AUTO: stage in pieces)
@@ -210,6 +212,7 @@ struct drp_ctx {
   struct Staged {
     uint64_t rows = 0, nf0 = 0, cap = 0;
     std::vector<std::pair<uint64_t, uint64_t>> pieces;
+    const uint8_t *dev = nullptr;  // the last piece's bytes on the device (a one-piece batch: all of it)
     uint64_t off0 = 0;
     uint32_t len0 = 0;
     uint8_t ty0 = 0;
@@ -299,6 +302,9 @@ void drp_close(drp_ctx *c) {
   c->aux.release();
   c->dec_cols.release();
   c->recbuf.release();
+  c->fetch_tmp.release();
+  c->keybuf.release();
+  c->keytext.release();
   if (c->dstats) (void)hipFree(c->dstats);
   if (c->ctile) (void)hipFree(c->ctile);
   for (auto &e : c->ev) (void)hipEventDestroy(e);
@@ -1165,6 +1171,7 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
       if (hipEventElapsedTime(&ms, c->hev[0], c->hev[1]) == hipSuccess) h2d_ms += ms;
     }
     S.pieces.emplace_back(rows, ps);
+    S.dev = static_cast<const uint8_t *>(c->in_stage.p);
     const uint64_t bad = (r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0;
     if (r.err_code || pe == n) {  // the batch's end or its error: this piece's tail is the batch's
       if (r.err_code) {
@@ -1339,6 +1346,7 @@ static int stage_decode(drp_ctx *c, const HostSrc &H, drp_carry *carry, uint64_t
   c->frames_per_byte = m ? (double)r.frames / (double)m : 0.0;
   const uint64_t bad = (r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0;
   S.pieces.emplace_back(0, a);
+  S.dev = dbytes;
   S.rows = S.nf0 + r.frames + bad;
   *n_frames = S.nf0 + r.frames;
   if (r.err_code) {
@@ -1504,6 +1512,82 @@ int drp_decode_fetch_block_ex(drp_ctx *c, void *block, uint64_t block_bytes, con
   }
   c->timing.d2h_ms = (float)(now_ms() - t0);
   return DRP_OK;
+}
+
+// drp_decode_fetch_keys: per row the length of its ASCII key (0 for every other row), an
+// exclusive scan of those (drp_launch_tile_scan over rows: one "tile" per row), then every key
+// copied from the staged bytes to its position and the positions narrowed to u32
+__global__ __launch_bounds__(256) void key_len_kernel(const uint8_t *type, const uint8_t *flags, const uint32_t *kl,
+                                                      uint64_t n, uint64_t *len, uint64_t *prefix) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (g == 0) {
+    prefix[0] = 0;
+    prefix[1] = n;
+  }
+  if (g >= n) return;
+  const bool on = (type[g] & 0x3f) == DRP_TYPE_CHANGE && (flags[g] & (DRP_F_KEY_ASCII | DRP_F_BAD)) == DRP_F_KEY_ASCII;
+  len[g] = on ? kl[g] : 0u;
+}
+__global__ __launch_bounds__(256) void key_copy_kernel(const uint8_t *bytes, const uint64_t *poff, const uint32_t *ko,
+                                                       const uint64_t *len, const uint64_t *pos, uint64_t n,
+                                                       uint32_t *kp, uint8_t *text, uint64_t *total) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (g >= n) return;
+  const uint64_t p = pos[g], m = len[g];
+  kp[g] = (uint32_t)p;
+  if (g == n - 1) *total = p + m;
+  const uint8_t *src = bytes + poff[g] + ko[g];
+  for (uint64_t x = 0; x < m; x++) text[p + x] = src[x];
+}
+
+int drp_decode_fetch_keys(drp_ctx *c, uint64_t first, uint64_t rows, uint32_t *kp, char *text, uint64_t text_cap,
+                          uint64_t *text_len) {
+  if (!c || !kp || !text_len || (!text && text_cap)) return DRP_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  auto &S = c->staged;
+  if (first > S.rows || rows > S.rows - first) return DRP_E_INVAL;
+  if (S.pieces.size() != 1 || !S.dev || c->key_post == DRP_KEY_POST_OFF) return DRP_E_INVAL;
+  *text_len = 0;
+  if (!rows) return DRP_OK;
+  const uint64_t dst = first == 0 && S.nf0 ? 1 : 0;  // (a carried blob row: no key)
+  const uint64_t g0 = first + dst - S.nf0, ng = rows - dst;
+  if (dst) kp[0] = 0;
+  if (!ng) return DRP_OK;
+  hipStream_t st = c->st;
+  // scratch: lengths, positions, the scan's tile bounds and block sums, u32 positions, the total
+  const uint64_t nb = (ng + 4095) / 4096 + 2;
+  const size_t o_len = 0, o_pos = o_len + ng * 8, o_pre = o_pos + ng * 8, o_tmp = o_pre + 16, o_kp = o_tmp + nb * 8,
+               o_tot = (o_kp + ng * 4 + 15) & ~(size_t)15, o_end = o_tot + 16;
+  if (!c->keybuf.ensure(o_end)) return DRP_E_NOMEM;
+  uint8_t *K = static_cast<uint8_t *>(c->keybuf.p);
+  uint64_t *len = reinterpret_cast<uint64_t *>(K + o_len), *pos = reinterpret_cast<uint64_t *>(K + o_pos);
+  uint64_t *pre = reinterpret_cast<uint64_t *>(K + o_pre), *tmp = reinterpret_cast<uint64_t *>(K + o_tmp);
+  uint32_t *dkp = reinterpret_cast<uint32_t *>(K + o_kp);
+  uint64_t *tot = reinterpret_cast<uint64_t *>(K + o_tot);
+  const uint32_t grid = (uint32_t)((ng + 255) / 256);
+  hipLaunchKernelGGL(key_len_kernel, dim3(grid), dim3(256), 0, st, S.fr.type + g0, S.co.flags + g0, S.co.key_len + g0,
+                     ng, len, pre);
+  CHK(hipGetLastError());
+  CHK(drp_launch_tile_scan(len, pre, 1, ng, tmp, pos, ~0ull, nullptr, st));
+  // the total first (the text's size), then the text
+  uint64_t total = 0;
+  {
+    uint64_t lastp = 0, lastl = 0;
+    CHK(hipMemcpyAsync(&lastp, pos + ng - 1, 8, hipMemcpyDeviceToHost, st));
+    CHK(hipMemcpyAsync(&lastl, len + ng - 1, 8, hipMemcpyDeviceToHost, st));
+    CHK(hipStreamSynchronize(st));
+    total = lastp + lastl;
+  }
+  if (!c->keytext.ensure(total + 64)) return DRP_E_NOMEM;
+  uint8_t *T = static_cast<uint8_t *>(c->keytext.p);
+  hipLaunchKernelGGL(key_copy_kernel, dim3(grid), dim3(256), 0, st, S.dev, S.fr.payload_off + g0, S.co.key_off + g0, len,
+                     pos, ng, dkp, T, tot);
+  CHK(hipGetLastError());
+  CHK(hipMemcpyAsync(kp + dst, dkp, ng * 4, hipMemcpyDeviceToHost, st));
+  if (text && total && total <= text_cap) CHK(hipMemcpyAsync(text, T, total, hipMemcpyDeviceToHost, st));
+  CHK(hipStreamSynchronize(st));
+  *text_len = total;
+  return total > text_cap && text ? DRP_E_CAPACITY : DRP_OK;
 }
 
 int drp_decode_stage(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *carry, uint64_t *n_frames,

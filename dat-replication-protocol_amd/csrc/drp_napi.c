@@ -264,7 +264,9 @@ typedef struct {
   void *khash;
   uint32_t *kp;   /* each row's key position in `keys` (rows with an ASCII key) */
   char *keys;     /* the batch's ASCII keys end to end (malloc'd; a latin1 string on the JS thread) */
+  colblock *kblk; /* or those keys built on the device (drp_decode_fetch_keys) in a pinned block */
   uint64_t nkeys; /* its length; ~0: too long for one string (the JS layer decodes keys one by one) */
+  int keys_done;  /* the key text (or its absence) is settled: the device built it */
   double t_h2d, t_gpu, t_d2h, t_convert; /* ms: batch to HBM, decode kernels, columns back,
                                             u64 -> Number + the key text */
   double h2d_bytes, h2d_skipped, host_copied; /* bytes staged into HBM / blob payload bytes left in host
@@ -273,6 +275,8 @@ typedef struct {
 
 static void free_cols(dec_job *j) {
   if (j->blk) col_put(j->blk); /* (never handed to JS) */
+  if (j->kblk) col_put(j->kblk);
+  j->kblk = NULL;
   free(j->mem);
   free(j->keys);
   j->blk = NULL;
@@ -378,6 +382,33 @@ static void dec_run(dec_job *j) {
       /* payload_off, change, from, to as doubles (JS Numbers), converted on the device */
       j->rc = drp_decode_fetch_block_ex(j->box->c, base, j->bytes, off, 0, j->rows, DRP_FETCH_F64);
     }
+    /* the key text on the device, into a pinned block (a batch staged in blob-skipping pieces has
+       its earlier pieces off the device: DRP_E_INVAL, the host builds it below) */
+    if (j->rc == DRP_OK && j->st && j->rows) {
+      const double tk = now_ms();
+      uint64_t tl = 0;
+      j->kblk = col_get(j->st, (size_t)j->rows * 40 + 4096);
+      int r = j->kblk ? drp_decode_fetch_keys(j->box->c, 0, j->rows, j->kp, (char *)j->kblk->p, j->kblk->cap, &tl)
+                      : DRP_E_NOMEM;
+      if (r == DRP_E_CAPACITY && tl <= KEYS_MAX) { /* (keys longer than the guess: once more) */
+        col_put(j->kblk);
+        j->kblk = col_get(j->st, (size_t)tl + 64);
+        r = j->kblk ? drp_decode_fetch_keys(j->box->c, 0, j->rows, j->kp, (char *)j->kblk->p, j->kblk->cap, &tl)
+                    : DRP_E_NOMEM;
+      }
+      if (r == DRP_OK || (r == DRP_E_CAPACITY && tl > KEYS_MAX)) {
+        j->nkeys = tl > KEYS_MAX ? ~(uint64_t)0 : tl; /* (too long for one string: keys one by one) */
+        if (j->nkeys == ~(uint64_t)0 && j->kblk) {
+          col_put(j->kblk);
+          j->kblk = NULL;
+        }
+        j->keys_done = 1;
+      } else if (j->kblk) {
+        col_put(j->kblk);
+        j->kblk = NULL;
+      }
+      j->t_convert = now_ms() - tk;
+    }
   }
   drp_timing tm;
   if (drp_last_timing(j->box->c, &tm) == DRP_OK) {
@@ -393,6 +424,7 @@ static void dec_run(dec_job *j) {
     free_cols(j);
     return;
   }
+  if (j->keys_done) return; /* (the key text came from the device) */
   const double t0 = now_ms();
   if ((j->rc = key_text(j)) != DRP_OK) {
     free_cols(j);
@@ -427,7 +459,11 @@ static napi_value dec_result(napi_env env, dec_job *j) {
   set_num(env, res, "blobRemaining", (double)j->carry.blob_remaining);
   set_num(env, res, "frameBytes", (double)j->carry.frame_bytes);
   napi_value t, kt;
-  if (j->keys) {
+  if (j->kblk && j->nkeys != ~(uint64_t)0) {
+    if (napi_create_string_latin1(env, (const char *)j->kblk->p, j->nkeys, &kt) != napi_ok) return NULL;
+    col_put(j->kblk);
+    j->kblk = NULL;
+  } else if (j->keys) {
     if (napi_create_string_latin1(env, j->keys, j->nkeys, &kt) != napi_ok) return NULL;
     free(j->keys);
     j->keys = NULL;

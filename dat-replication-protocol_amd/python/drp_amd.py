@@ -26,7 +26,7 @@ EXPORTS = [
     "drp_last_timing", "drp_set_tile", "drp_set_strict", "drp_set_exact", "drp_set_key_post",
     "drp_set_blob_skip", "drp_decode_scratch_bytes",
     "drp_decode_device", "drp_decode_batch", "drp_decode_stage", "drp_decode_stage_v", "drp_decode_fetch", "drp_decode_fetch_block",
-    "drp_decode_fetch_block_ex",
+    "drp_decode_fetch_block_ex", "drp_decode_fetch_keys",
     "drp_encode_size", "drp_encode_device",
     "drp_encode_batch", "drp_index_scan", "drp_stream_stats_from_results", "drp_device",
     "drp_comm_id", "drp_comm_init_rank", "drp_comm_init_all", "drp_comm_destroy",
@@ -119,6 +119,7 @@ def lib():
         L.drp_decode_fetch.argtypes = [P, C.POINTER(Frames), C.POINTER(Changes), U64, U64]
         L.drp_decode_fetch_block.argtypes = [P, P, U64, C.POINTER(U64), U64, U64]
         L.drp_decode_fetch_block_ex.argtypes = [P, P, U64, C.POINTER(U64), U64, U64, U32]
+        L.drp_decode_fetch_keys.argtypes = [P, U64, U64, P, P, U64, C.POINTER(U64)]
         L.drp_encode_size.argtypes = [P, C.POINTER(ChangeSrc), U64, C.POINTER(U64)]
         L.drp_encode_device.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, P, U64]
         L.drp_encode_batch.argtypes = [P, C.POINTER(ChangeSrc), P, U64, U64, P, U64,
@@ -287,16 +288,19 @@ class Ctx:
                    frame_bytes=int(carry.frame_bytes))
         return res
 
-    def decode_staged(self, wire, blob_remaining=0, pieces=1, key_hash=False, block=False, f64=False):
+    def decode_staged(self, wire, blob_remaining=0, pieces=1, key_hash=False, block=False, f64=False, keys=False):
         """drp_decode_stage, then drp_decode_fetch of the rows in `pieces` consecutive
         fetches into host columns sized from the frame count (the N-API addon's path). `wire`
         as a list of byte strings: the batch is those chunks end to end (drp_decode_stage_v).
         block=True: one drp_decode_fetch_block of every row into one host block instead (the
         columns at 64-byte aligned offsets, as the addon lays them out); f64=True: with
-        drp_decode_fetch_block_ex(DRP_FETCH_F64), payload_off / change / from / to as float64."""
+        drp_decode_fetch_block_ex(DRP_FETCH_F64), payload_off / change / from / to as float64.
+        keys=True: the key flags too, and drp_decode_fetch_keys' "kp" (u32 per row) and "key_text"
+        (bytes; None when the batch was staged in pieces: DRP_E_INVAL)."""
         carry = Carry(blob_remaining, 0, 0, 0, 0)
         nf, ef, ec, ed = U64(), U64(), U32(), U32()
-        _chk("drp_set_key_post", self.L.drp_set_key_post(self.h, KEY_POST_HASH if key_hash else KEY_POST_OFF))
+        kpost = KEY_POST_HASH if key_hash else (KEY_POST_FLAGS if keys else KEY_POST_OFF)
+        _chk("drp_set_key_post", self.L.drp_set_key_post(self.h, kpost))
         if isinstance(wire, (list, tuple)):
             arrs = [np.frombuffer(bytes(c), np.uint8) if len(c) else np.zeros(1, np.uint8) for c in wire]
             ch = (Chunk * max(1, len(arrs)))(*[Chunk(_p(a), len(c)) for a, c in zip(arrs, wire)])
@@ -334,6 +338,18 @@ class Ctx:
             part = {k: v[a:] for k, v in o.items()}
             fr, co = _structs(part, _p)
             _chk("drp_decode_fetch", self.L.drp_decode_fetch(self.h, C.byref(fr), C.byref(co), int(a), int(b - a)))
+        if keys:
+            kp = np.zeros(max(rows, 1), np.uint32)
+            tl = U64()
+            rc = self.L.drp_decode_fetch_keys(self.h, 0, rows, _p(kp), None, 0, C.byref(tl))
+            if rc == -1:  # DRP_E_INVAL: staged in pieces
+                o.update(kp=None, key_text=None)
+            else:
+                _chk("drp_decode_fetch_keys", rc)
+                text = np.zeros(max(int(tl.value), 1), np.uint8)
+                _chk("drp_decode_fetch_keys", self.L.drp_decode_fetch_keys(self.h, 0, rows, _p(kp), _p(text),
+                                                                           int(tl.value), C.byref(tl)))
+                o.update(kp=kp[:rows], key_text=text[:int(tl.value)].tobytes())
         o.update(nframes=int(nf.value), err_frame=int(ef.value), err_code=int(ec.value), err_detail=int(ed.value),
                  consumed=int(carry.consumed), tail=int(carry.tail_kind), blob_remaining=int(carry.blob_remaining),
                  frame_bytes=int(carry.frame_bytes))

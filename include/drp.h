@@ -270,6 +270,17 @@ int drp_decode_fetch_block(drp_ctx *ctx, void *block, uint64_t block_bytes, cons
 #define DRP_FETCH_F64 1u
 int drp_decode_fetch_block_ex(drp_ctx *ctx, void *block, uint64_t block_bytes, const uint64_t *col_off,
                               uint64_t first, uint64_t rows, uint32_t flags);
+/* The keys of the staged rows [first, first + rows) whose key the key post-processing flagged
+ * ASCII (drp_set_key_post; Change rows without DRP_F_BAD), end to end: kp[r] = the text length
+ * before row r (every row), text = those keys (at most text_cap bytes), *text_len = its length.
+ * Built on the device from the staged batch (a JavaScript host makes one string of it and cuts
+ * each key as a substring, the same string the key bytes' UTF-8 decode would give). text = NULL:
+ * only kp and *text_len. DRP_E_CAPACITY: the text is longer than text_cap (kp and *text_len are
+ * still written). DRP_E_INVAL when the batch was staged in more than one piece (blob skipping:
+ * its earlier pieces are no longer on the device) or the keys were not flagged. Replaces the key
+ * string of messages.Change.decode (decode.js:205-214). */
+int drp_decode_fetch_keys(drp_ctx *ctx, uint64_t first, uint64_t rows, uint32_t *kp, char *text, uint64_t text_cap,
+                          uint64_t *text_len);
 /* drp_decode_stage over a batch the caller holds as chunks (its queued writes), laid end to end:
  * the caller never concatenates them. The ranges the decode stages into HBM (all of the batch,
  * or with blob skipping everything but the blob payloads) are gathered from the chunks into

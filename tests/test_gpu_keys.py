@@ -87,3 +87,41 @@ def test_key_post_off_by_default(ctx):
     g = ctx.decode_batch(wire)
     ch = (g["type"] & 0x3F) == 1  # (blob rows' Change columns are unspecified)
     assert int(np.max(g["flags"][ch])) < 0x10
+
+
+def _key_text(wire, r, rows):
+    """The oracle's ASCII keys of the Change rows end to end, and each row's position (as the
+    addon's key text: rows whose key is ASCII and whose Change is well formed)."""
+    kp, parts, tot = np.zeros(rows, np.uint32), [], 0
+    for k in range(rows):
+        kp[k] = tot
+        if k >= r["nframes"] or r["type"][k] & 0x3F != 1 or r["flags"][k] & 4:
+            continue
+        po = int(r["payload_off"][k])
+        key = wire[po + int(r["key_off"][k]):po + int(r["key_off"][k]) + int(r["key_len"][k])]
+        if key.isascii():
+            parts.append(key)
+            tot += len(key)
+    return kp, b"".join(parts)
+
+
+@pytest.mark.parametrize("chunked", [False, True])
+def test_fetch_keys_builds_the_key_text_on_the_device(ctx, chunked):
+    """drp_decode_fetch_keys (the N-API addon's key text): every ASCII key end to end, built on
+    the device from the staged batch, equals the oracle's; positions per row too."""
+    from _gpu import drp_amd
+    wire = _stream(random.Random(23), 4000)
+    r = O.decode_batch(wire)
+    arg = [wire[i:i + 65536] for i in range(0, len(wire), 65536)] if chunked else wire
+    ctx.set_blob_skip(drp_amd.BLOB_SKIP_OFF)  # (one piece: the whole batch stays on the device)
+    try:
+        o = ctx.decode_staged(arg, keys=True)
+        assert o["nframes"] == r["nframes"]
+        kp, text = _key_text(wire, r, o["nframes"])
+        assert o["key_text"] == text
+        np.testing.assert_array_equal(o["kp"], kp)
+        ctx.set_blob_skip(drp_amd.BLOB_SKIP_ALWAYS)  # pieces: the caller builds the text on the host
+        o = ctx.decode_staged(arg, keys=True)
+        assert o["nframes"] == r["nframes"] and (o["key_text"] is None or o["key_text"] == text)
+    finally:
+        ctx.set_blob_skip(drp_amd.BLOB_SKIP_AUTO)
