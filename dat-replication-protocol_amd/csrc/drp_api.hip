@@ -1530,12 +1530,11 @@ __global__ __launch_bounds__(256) void key_len_kernel(const uint8_t *type, const
 }
 __global__ __launch_bounds__(256) void key_copy_kernel(const uint8_t *bytes, const uint64_t *poff, const uint32_t *ko,
                                                        const uint64_t *len, const uint64_t *pos, uint64_t n,
-                                                       uint32_t *kp, uint8_t *text, uint64_t *total) {
+                                                       uint32_t *kp, uint8_t *text) {
   const uint64_t g = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (g >= n) return;
   const uint64_t p = pos[g], m = len[g];
-  kp[g] = (uint32_t)p;
-  if (g == n - 1) *total = p + m;
+  kp[g] = (uint32_t)p;  // (the text's length is checked against 256 MiB by the caller)
   const uint8_t *src = bytes + poff[g] + ko[g];
   for (uint64_t x = 0; x < m; x++) text[p + x] = src[x];
 }
@@ -1554,16 +1553,15 @@ int drp_decode_fetch_keys(drp_ctx *c, uint64_t first, uint64_t rows, uint32_t *k
   if (dst) kp[0] = 0;
   if (!ng) return DRP_OK;
   hipStream_t st = c->st;
-  // scratch: lengths, positions, the scan's tile bounds and block sums, u32 positions, the total
+  // scratch: lengths, positions, the scan's tile bounds and block sums, u32 positions
   const uint64_t nb = (ng + 4095) / 4096 + 2;
   const size_t o_len = 0, o_pos = o_len + ng * 8, o_pre = o_pos + ng * 8, o_tmp = o_pre + 16, o_kp = o_tmp + nb * 8,
-               o_tot = (o_kp + ng * 4 + 15) & ~(size_t)15, o_end = o_tot + 16;
+               o_end = o_kp + ng * 4 + 16;
   if (!c->keybuf.ensure(o_end)) return DRP_E_NOMEM;
   uint8_t *K = static_cast<uint8_t *>(c->keybuf.p);
   uint64_t *len = reinterpret_cast<uint64_t *>(K + o_len), *pos = reinterpret_cast<uint64_t *>(K + o_pos);
   uint64_t *pre = reinterpret_cast<uint64_t *>(K + o_pre), *tmp = reinterpret_cast<uint64_t *>(K + o_tmp);
   uint32_t *dkp = reinterpret_cast<uint32_t *>(K + o_kp);
-  uint64_t *tot = reinterpret_cast<uint64_t *>(K + o_tot);
   const uint32_t grid = (uint32_t)((ng + 255) / 256);
   hipLaunchKernelGGL(key_len_kernel, dim3(grid), dim3(256), 0, st, S.fr.type + g0, S.co.flags + g0, S.co.key_len + g0,
                      ng, len, pre);
@@ -1581,7 +1579,7 @@ int drp_decode_fetch_keys(drp_ctx *c, uint64_t first, uint64_t rows, uint32_t *k
   if (!c->keytext.ensure(total + 64)) return DRP_E_NOMEM;
   uint8_t *T = static_cast<uint8_t *>(c->keytext.p);
   hipLaunchKernelGGL(key_copy_kernel, dim3(grid), dim3(256), 0, st, S.dev, S.fr.payload_off + g0, S.co.key_off + g0, len,
-                     pos, ng, dkp, T, tot);
+                     pos, ng, dkp, T);
   CHK(hipGetLastError());
   CHK(hipMemcpyAsync(kp + dst, dkp, ng * 4, hipMemcpyDeviceToHost, st));
   if (text && total && total <= text_cap) CHK(hipMemcpyAsync(text, T, total, hipMemcpyDeviceToHost, st));

@@ -234,8 +234,9 @@ void link(const Img &m, uint64_t s1, uint64_t g, uint64_t e_first, uint64_t &E,
 
 // Wave scans and reductions on DPP (row shifts, then row broadcasts): __shfl_xor reductions cost
 // ~5 VALU and a ds_bpermute per step. The compiler leaves update_dpp + op uncombined in the claims
-// kernels (three VALU per step); DRP_DPP_ASM=1 writes one DPP op per step in inline asm. Every use
-// runs with all 64 lanes active (block-level code). s_nop 4 first: the five wait states between an SALU write of EXEC
+// kernels (three VALU per step), so the prefix sum is one DPP op per step in inline asm (C2 claims
+// ~30 VALU per wave fewer; 5.35 -> 5.32 ms per decode). Every use of it runs with all 64 lanes
+// active (block-level code). s_nop 4 first: the five wait states between an SALU write of EXEC
 // (the end of the branch before) and a DPP op; s_nop 1: the two between a VALU write and a DPP read.
 #define DRP_DPP_STEPS(op)                                                                    \
   "s_nop 4\n\t" op " %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"     \
@@ -246,12 +247,7 @@ void link(const Img &m, uint64_t s1, uint64_t g, uint64_t e_first, uint64_t &E,
   "s_nop 1\n\t" op " %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
 // inclusive prefix sum over the wave
 __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  asm volatile(DRP_DPP_STEPS("v_add_u32_dpp") : "+v"(v));
   return v;
 }
 // wave-uniform sum / maximum (lane 63 of the inclusive scan)
@@ -1481,7 +1477,8 @@ __device__ __forceinline__ uint32_t fast_claims(const DecodeParams &P, const Til
   const uint32_t cnt = (uint32_t)__builtin_popcountll(live);
   const uint32_t cpre = wave_scan_dpp(cnt);
   const uint32_t hcnt = (uint32_t)__builtin_popcountll(hlive);
-  const uint32_t hpre = wave_scan_dpp(hcnt);
+  uint32_t hpre = 0;
+  if (wid == 0) hpre = wave_scan_dpp(hcnt);  // (the halo's threads are wave 0's: wave-uniform)
   if (lane == 63) xw[wid] = cpre;
   if (tid == 63) xw[2] = hpre;
   lmw[tid] = live;
