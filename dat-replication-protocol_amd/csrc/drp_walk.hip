@@ -732,8 +732,14 @@ extern "C" hipError_t drp_launch_claims_walk(const DecodeParams *P, uint64_t nt_
   hipLaunchKernelGGL(spec::walk_sync, dim3((uint32_t)((maxr * spec::SY_LANES + 255) / 256)), dim3(256), 0, st, *P);
   const size_t nrec = (size_t)nt_max * spec::NT;  // (one record byte per 64-byte segment)
   hipError_t e = hipMemsetAsync(P->ent, 0xFF, nrec, st);
-  if (e == hipSuccess) e = hipMemsetAsync(P->ent_n, 0, nrec, st);
-  if (e == hipSuccess) e = hipMemsetAsync(P->ent_c, 0, nrec, st);
+  if (e == hipSuccess) {  // (ent_c follows ent_n in the scratch: one fill for both)
+    if (P->ent_c == P->ent_n + nrec) {
+      e = hipMemsetAsync(P->ent_n, 0, 2 * nrec, st);
+    } else {
+      e = hipMemsetAsync(P->ent_n, 0, nrec, st);
+      if (e == hipSuccess) e = hipMemsetAsync(P->ent_c, 0, nrec, st);
+    }
+  }
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(spec::claims_hop, dim3((uint32_t)((maxr + 255) / 256)), dim3(256), 0, st, *P);
   return hipGetLastError();
