@@ -151,6 +151,16 @@ bool is_device_ptr(const void *p) {
   return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+// page-locked host memory (the DMA engine reads it directly, without a staging copy)
+bool is_pinned_host(const void *p) {
+  hipPointerAttribute_t a;
+  if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
 size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
 double now_ms() {
@@ -166,6 +176,10 @@ struct drp_ctx {
   hipStream_t st = nullptr;
   hipEvent_t ev[4] = {};
   hipEvent_t hev[2] = {};  // a staged piece's H2D
+  // pipelined staging (stage_pieces): the copy stream and one event per chunk (created on first use)
+  hipStream_t cst = nullptr;
+  hipEvent_t pev[32] = {};
+  uint64_t pipe_chunk = 64ull << 20;  // DRP_PIPE_CHUNK (MiB; 0: no pipelining)
   uint32_t B = 128;
   int strict = 0;
   int exact = 0;  // 1: always the exact kernel (decode_tiles), never the speculative one
@@ -205,6 +219,11 @@ struct drp_ctx {
   uint64_t blob_run = 0;       // bytes from a piece's start to its blob's payload, last seen
   uint64_t piece_span = 0;     // batch bytes one blob-skipping piece covered on average, last seen
   drp_timing timing = {};
+  // drp_decode_batch's host columns while it stages (pipelined pieces fetch their rows into them
+  // during the copy; dfetched: rows already there)
+  const drp_frames *dfr = nullptr;
+  const drp_changes *dco = nullptr;
+  uint64_t dcap = 0, dfetched = 0;
   std::vector<uint64_t> host_tmp;
   // the staged host-batch decode: row 0 is a host-built blob continuation when nf0 == 1; GPU
   // rows follow, each piece's payload_off relative to the batch offset where that piece was
@@ -268,6 +287,11 @@ int drp_open(int device, drp_ctx **out) {
   }
   for (auto &e : c->ev) (void)hipEventCreate(&e);
   for (auto &e : c->hev) (void)hipEventCreate(&e);
+  if (hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipStreamDestroy(c->st);
+    delete c;
+    return DRP_E_HIP;
+  }
   if (const char *t = getenv("DRP_TILE")) {
     uint32_t tb = (uint32_t)atoi(t);
     if (tb == 4096 || tb == 8192) c->B = tb / 64;
@@ -282,6 +306,7 @@ int drp_open(int device, drp_ctx **out) {
   if (const char *e = getenv("DRP_CASCADE_MIN")) c->cascade_min = (uint32_t)strtoul(e, nullptr, 10);
   if (const char *e = getenv("DRP_JUMP_MIN")) c->jump_min = strtoll(e, nullptr, 10);
   if (const char *e = getenv("DRP_WALK_MIN")) c->walk_min = strtoull(e, nullptr, 10);
+  if (const char *e = getenv("DRP_PIPE_CHUNK")) c->pipe_chunk = strtoull(e, nullptr, 10) << 20;
   if (const char *e = getenv("DRP_CREC")) c->crec = atoi(e);
   if (const char *e = getenv("DRP_CLAIMS")) c->claims_mode = strcmp(e, "fast") == 0 ? 2 : strcmp(e, "hop") == 0 ? 3 : 0;
   if (const char *e = getenv("DRP_DIRTY_CAP")) c->dirty_cap = strtoull(e, nullptr, 10);
@@ -309,6 +334,10 @@ void drp_close(drp_ctx *c) {
   if (c->ctile) (void)hipFree(c->ctile);
   for (auto &e : c->ev) (void)hipEventDestroy(e);
   for (auto &e : c->hev) (void)hipEventDestroy(e);
+  for (auto &e : c->pev)
+    if (e) (void)hipEventDestroy(e);
+  (void)hipStreamSynchronize(c->cst);
+  (void)hipStreamDestroy(c->cst);
   (void)hipStreamDestroy(c->st);
   delete c;
 }
@@ -1035,6 +1064,18 @@ constexpr uint64_t kPiecesMin = 1 << 20;     // batches below this are staged wh
 // blob payload on the host into the pinned gather buffer.
 constexpr uint64_t kPieceBudget = 8;
 constexpr uint64_t kPieceProbe = 4;  // pieces of a batch before its own span is trusted
+// A flat batch in page-locked memory that is staged whole (or its rest, above) is decoded as it
+// lands: the DMA engine copies it in chunks of at least kPipeChunk on the ctx's copy stream while
+// the compute stream decodes a piece per chunk (each piece waits for its chunk's event), so only
+// the last chunk's decode follows the copy (C3: 18.7 ms of PCIe per GiB, 2.7 ms of decode).
+constexpr uint64_t kPipeChunk = 64 << 20;  // (drp_ctx::pipe_chunk's default)
+constexpr uint64_t kPipeEvents = 32;  // chunks at most (drp_ctx::pev)
+
+// payload offsets of a pipelined piece's rows: piece-relative -> relative to the pipelined range
+__global__ void piece_shift_kernel(uint64_t *payload_off, uint64_t n, uint64_t d) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u)
+    payload_off[i] += d;
+}
 
 // The staged rows' capacity for m bytes: from the density of the ctx's previous batch (a
 // stream's batches are alike), 1/32 per byte at first.
@@ -1087,9 +1128,48 @@ __global__ void piece_tail_kernel(const drp_stream_result *r, const uint64_t *pa
   *boff = r->frames ? payload_off[r->frames - 1] : 0;
 }
 
-static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *carry,
+static int fetch_staged(drp_ctx *c, const drp_frames *frames, const drp_changes *cols, uint64_t first,
+                        uint64_t rows);
+
+// staged rows [first, first + rows) into host columns from their row `first` on (fetch_staged
+// writes from row 0)
+static int fetch_staged_at(drp_ctx *c, const drp_frames *frames, const drp_changes *cols, uint64_t first,
+                           uint64_t rows) {
+  drp_frames f = *frames;
+  drp_changes o = *cols;
+  f.payload_off += first;
+  f.payload_len += first;
+  f.type += first;
+  o.key_off += first;
+  o.key_len += first;
+  o.subset_off += first;
+  o.subset_len += first;
+  o.value_off += first;
+  o.value_len += first;
+  o.change += first;
+  o.from += first;
+  o.to += first;
+  o.flags += first;
+  if (o.key_hash) o.key_hash += first;
+  return fetch_staged(c, &f, &o, first, rows);
+}
+
+static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, bool pipe, drp_carry *carry,
                         uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail) {
   hipStream_t st = c->st;
+  // pipelined (pipe): [pbase, n) goes to in_stage (offset 0) by DMA on c->cst, chunk k ending at
+  // pend[k] and signalled by c->pev[k]; each piece ends at a chunk's end. The copy stream is
+  // drained on every way out (its DMAs write into in_stage).
+  uint64_t pbase = 0, jumped = 0;
+  std::vector<uint64_t> pend;
+  size_t pk = 0;
+  struct Drain {
+    drp_ctx *c;
+    const std::vector<uint64_t> &pend;
+    ~Drain() {
+      if (!pend.empty()) (void)hipStreamSynchronize(c->cst);
+    }
+  } drain{c, pend};
   auto &S = c->staged;
   const size_t stage_meta = 256;
   if (!c->aux.ensure(stage_meta + sizeof(drp_stream_result) + 64)) return DRP_E_NOMEM;
@@ -1121,19 +1201,59 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
   } hr;
   drp_stream_result &r = hr.r;
   for (;;) {
-    if (H.flat && c->blob_skip == DRP_BLOB_SKIP_AUTO) {  // dense blobs in a flat batch: the rest in one piece
+    if (!pipe && H.flat && c->blob_skip == DRP_BLOB_SKIP_AUTO) {  // dense blobs in a flat batch: the rest in one piece
       const uint64_t span = npieces >= kPieceProbe ? span_now : c->piece_span;
-      if (span && (n - pos) / span > kPieceBudget) want = n - pos;
+      if (span && (n - pos) / span > kPieceBudget) {
+        want = n - pos;
+        pipe = c->pipe_chunk && n - pos >= 2 * c->pipe_chunk && is_pinned_host(H.flat);
+      }
     }
-    const uint64_t pe = std::min(n, pos + want), ps = pos & ~15ull, mp = pe - ps;
+    if (pipe && pend.empty()) {  // (the compute stream is idle here: every piece ends in a wait)
+      pbase = pos & ~15ull;
+      const uint64_t m = n - pbase;
+      if (!c->in_stage.ensure(m + 64)) return DRP_E_NOMEM;
+      const uint64_t chunk = (std::max(c->pipe_chunk, (m + kPipeEvents - 1) / kPipeEvents) + 0xFFFF) & ~0xFFFFull;
+      for (uint64_t e = pbase + chunk; e < n; e += chunk) pend.push_back(e);
+      pend.push_back(n);
+      CHK(hipEventRecord(c->hev[0], c->cst));
+      for (size_t k = 0; k < pend.size(); k++) {
+        if (!c->pev[k]) CHK(hipEventCreateWithFlags(&c->pev[k], hipEventDisableTiming));
+        const uint64_t lo = k ? pend[k - 1] : pbase;
+        CHK(hipMemcpyAsync(c->in_stage.at<uint8_t>(lo - pbase), H.flat + lo, pend[k] - lo, hipMemcpyHostToDevice,
+                           c->cst));
+        CHK(hipEventRecord(c->pev[k], c->cst));
+      }
+      CHK(hipEventRecord(c->hev[1], c->cst));
+      staged += m;
+      S.pieces.emplace_back(rows, pbase);
+    }
+    uint64_t pe, ps, mp;
+    const uint8_t *dp;
+    if (pipe) {  // to the end of the first chunk past pos (and past the last piece's end)
+      while (pk < pend.size() && pend[pk] <= pos) pk++;
+      if (pk == pend.size()) return DRP_E_HIP;  // (unreachable: pos < n)
+      pe = pend[pk];
+      ps = pos & ~15ull;
+      mp = pe - ps;
+      dp = c->in_stage.at<uint8_t>(ps - pbase);
+      CHK(hipStreamWaitEvent(st, c->pev[pk], 0));
+      pk++;
+      hipLaunchKernelGGL(piece_meta_kernel, dim3(1), dim3(1), 0, st, soff, ent, mp, pos - ps);
+      CHK(hipGetLastError());
+    } else {
+      pe = std::min(n, pos + want);
+      ps = pos & ~15ull;
+      mp = pe - ps;
+      if (!c->in_stage.ensure(mp + 64)) return DRP_E_NOMEM;
+      dp = static_cast<const uint8_t *>(c->in_stage.p);
+      CHK(hipEventRecord(c->hev[0], st));
+      if (const int rc = h2d_range(c, H, ps, mp, c->in_stage.p, st, &copied)) return rc;
+      hipLaunchKernelGGL(piece_meta_kernel, dim3(1), dim3(1), 0, st, soff, ent, mp, pos - ps);
+      CHK(hipGetLastError());
+      CHK(hipEventRecord(c->hev[1], st));
+      staged += mp;
+    }
     npieces++;
-    if (!c->in_stage.ensure(mp + 64)) return DRP_E_NOMEM;
-    CHK(hipEventRecord(c->hev[0], st));
-    if (const int rc = h2d_range(c, H, ps, mp, c->in_stage.p, st, &copied)) return rc;
-    hipLaunchKernelGGL(piece_meta_kernel, dim3(1), dim3(1), 0, st, soff, ent, mp, pos - ps);
-    CHK(hipGetLastError());
-    CHK(hipEventRecord(c->hev[1], st));
-    staged += mp;
     drp_frames fr;
     drp_changes co;
     fr.payload_off = S.fr.payload_off + rows;
@@ -1150,7 +1270,7 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
     co.to = S.co.to + rows;
     co.flags = S.co.flags + rows;
     co.key_hash = S.co.key_hash ? S.co.key_hash + rows : nullptr;
-    const int rc = run_decode(c, (const uint8_t *)c->in_stage.p, mp, soff, ent, 1, &fr, &co, cap - rows, dres);
+    const int rc = run_decode(c, dp, mp, soff, ent, 1, &fr, &co, cap - rows, dres);
     if (rc == DRP_E_CAPACITY) return DRP_E_RETRY;
     if (rc != DRP_OK) return rc;
     // (run_decode describes one launch sequence: the call's timing is the sum over its pieces)
@@ -1166,12 +1286,20 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
     CHK(hipMemcpyAsync(&hr, dres, sizeof(hr), hipMemcpyDeviceToHost, st));
     CHK(hipStreamSynchronize(st));
     const uint64_t boff = hr.boff;
-    {
+    if (pipe) {  // the pipelined range is one piece: its rows' payload offsets from pbase
+      const uint64_t nr = r.frames + ((r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0);
+      if (nr && ps > pbase) {
+        const uint32_t g = (uint32_t)std::min<uint64_t>((nr + 255) / 256, 1024);
+        hipLaunchKernelGGL(piece_shift_kernel, dim3(g), dim3(256), 0, st, fr.payload_off, nr, ps - pbase);
+        CHK(hipGetLastError());
+      }
+      S.dev = static_cast<const uint8_t *>(c->in_stage.p);
+    } else {
       float ms = 0;
       if (hipEventElapsedTime(&ms, c->hev[0], c->hev[1]) == hipSuccess) h2d_ms += ms;
+      S.pieces.emplace_back(rows, ps);
+      S.dev = static_cast<const uint8_t *>(c->in_stage.p);
     }
-    S.pieces.emplace_back(rows, ps);
-    S.dev = static_cast<const uint8_t *>(c->in_stage.p);
     const uint64_t bad = (r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0;
     if (r.err_code || pe == n) {  // the batch's end or its error: this piece's tail is the batch's
       if (r.err_code) {
@@ -1193,7 +1321,7 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
       want = std::max(kPieceMin, c->blob_run + kPieceMargin);
       if (bend <= n) {  // the batch holds the whole blob: its row is not partial
         CHK(hipMemsetAsync(S.fr.type + rows - 1, DRP_TYPE_BLOB, 1, st));
-        skipped += bend - pe;
+        (pipe ? jumped : skipped) += bend - pe;
         pos = bend;
         span_now = (pos - pos0) / npieces;
         if (pos == n) {
@@ -1203,7 +1331,7 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
           break;
         }
       } else {  // the blob continues past the batch: the carry says how far
-        skipped += n - pe;
+        (pipe ? jumped : skipped) += n - pe;
         carry->blob_remaining = bend - n;
         carry->consumed = n;
         carry->tail_kind = DRP_TAIL_BLOB;
@@ -1216,14 +1344,27 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, drp_carry *c
       if (np > pos) pos = np;
       span_now = (pos - pos0) / npieces;
     }
+    if (pipe && c->dfr) {  // the rows so far into drp_decode_batch's host columns, while the copy runs
+      const uint64_t upto = std::min(S.nf0 + rows, c->dcap);
+      if (upto > c->dfetched) {
+        S.rows = S.nf0 + rows;
+        if (const int rc = fetch_staged_at(c, c->dfr, c->dco, c->dfetched, upto - c->dfetched)) return rc;
+        c->dfetched = upto;
+      }
+    }
   }
   c->timing = sum;
   if (span_now) c->piece_span = span_now;
+  if (!pend.empty()) {
+    CHK(hipStreamSynchronize(c->cst));
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->hev[0], c->hev[1]) == hipSuccess) h2d_ms += ms;
+  }
   c->timing.h2d_ms = h2d_ms;
   c->timing.h2d_bytes = staged;
   c->timing.h2d_skipped = skipped;
   c->timing.host_copied = copied;
-  c->blob_heavy = skipped * 4 >= n;  // (AUTO: keep skipping while it pays)
+  c->blob_heavy = (skipped + jumped) * 4 >= n;  // (AUTO: keep skipping while it pays)
   c->frames_per_byte = (double)rows / (double)(n - S.pieces[0].second);
   S.rows = S.nf0 + rows;
   *n_frames = S.nf0 + rows - ((*err_code == DRP_ERR_CHANGE || *err_code == DRP_ERR_REQUIRED) ? 1 : 0);
@@ -1265,14 +1406,19 @@ static int stage_decode(drp_ctx *c, const HostSrc &H, drp_carry *carry, uint64_t
     }
   }
   const bool host_in = !bytes || !is_device_ptr(bytes) || ((uintptr_t)bytes & 15);
-  if (host_in && n - brem >= kPiecesMin &&
-      (c->blob_skip == DRP_BLOB_SKIP_ALWAYS ||
-       (c->blob_skip == DRP_BLOB_SKIP_AUTO && (c->blob_heavy || c->frames_per_byte == 0)))) {
+  const bool pieces = host_in && n - brem >= kPiecesMin &&
+                      (c->blob_skip == DRP_BLOB_SKIP_ALWAYS ||
+                       (c->blob_skip == DRP_BLOB_SKIP_AUTO && (c->blob_heavy || c->frames_per_byte == 0)));
+  // a large flat batch in page-locked memory staged whole: decoded as it lands (kPipeChunk)
+  const bool pipe =
+      !pieces && host_in && H.flat && c->pipe_chunk && n - brem >= 2 * c->pipe_chunk && is_pinned_host(H.flat);
+  if (pieces || pipe) {
     // (AUTO: a ctx's first batch probes in pieces too; pieces grow geometrically while no blob
     // is met, so a batch without blobs costs a few more launches once)
     const drp_carry in = *carry;
-    const int rc = stage_pieces(c, H, brem, carry, n_frames, err_frame, err_code, err_detail);
+    const int rc = stage_pieces(c, H, brem, pipe, carry, n_frames, err_frame, err_code, err_detail);
     if (rc != DRP_E_RETRY) return rc;
+    c->dfetched = 0;
     *carry = in;  // (capacity: staged whole below)
     *err_frame = ~0ull;
     *err_code = DRP_ERR_NONE;
@@ -1642,11 +1788,17 @@ int drp_decode_batch(drp_ctx *c, const uint8_t *bytes, uint64_t n, drp_carry *ca
   HostSrc H;
   H.flat = bytes;
   H.n = n;
+  c->dfr = frames;
+  c->dco = cols;
+  c->dcap = cap;
+  c->dfetched = 0;
   int rc = stage_decode(c, H, carry, n_frames, err_frame, err_code, err_detail);
+  c->dfr = nullptr;
+  c->dco = nullptr;
   c->key_post = key_post;
   if (rc != DRP_OK) return rc;
-  const uint64_t rows = c->staged.rows;
-  rc = fetch_staged(c, frames, cols, 0, rows < cap ? rows : cap);
+  const uint64_t rows = c->staged.rows, upto = rows < cap ? rows : cap;
+  rc = fetch_staged_at(c, frames, cols, c->dfetched, upto > c->dfetched ? upto - c->dfetched : 0);
   if (rc != DRP_OK) return rc;
   return rows > cap ? DRP_E_CAPACITY : DRP_OK;
 }

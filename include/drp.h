@@ -161,7 +161,7 @@ typedef struct drp_timing {
   uint32_t reserved;
   /* host-batch calls (drp_decode_stage / drp_decode_fetch / drp_decode_batch), wall clock: */
   float h2d_ms;   /* staging the batch into HBM */
-  float d2h_ms;   /* copying the columns back (drp_decode_fetch) */
+  float d2h_ms;   /* copying the columns back (drp_decode_fetch; a pipelined batch: the rows left after its copy) */
   uint64_t h2d_bytes;   /* bytes of the last host batch staged into HBM */
   uint64_t h2d_skipped; /* its blob payload bytes never staged (pass-through, drp_set_blob_skip) */
   uint64_t host_copied; /* bytes of a chunked batch gathered on the host (drp_decode_stage_v) */
