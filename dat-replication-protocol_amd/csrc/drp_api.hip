@@ -179,7 +179,7 @@ struct drp_ctx {
   // pipelined staging (stage_pieces): the copy stream and one event per chunk (created on first use)
   hipStream_t cst = nullptr;
   hipEvent_t pev[32] = {};
-  uint64_t pipe_chunk = 64ull << 20;  // DRP_PIPE_CHUNK (MiB; 0: no pipelining)
+  uint64_t pipe_chunk = 128ull << 20;  // DRP_PIPE_CHUNK (MiB; 0: no pipelining)
   uint32_t B = 128;
   int strict = 0;
   int exact = 0;  // 1: always the exact kernel (decode_tiles), never the speculative one
@@ -1065,10 +1065,11 @@ constexpr uint64_t kPiecesMin = 1 << 20;     // batches below this are staged wh
 constexpr uint64_t kPieceBudget = 8;
 constexpr uint64_t kPieceProbe = 4;  // pieces of a batch before its own span is trusted
 // A flat batch in page-locked memory that is staged whole (or its rest, above) is decoded as it
-// lands: the DMA engine copies it in chunks of at least kPipeChunk on the ctx's copy stream while
-// the compute stream decodes a piece per chunk (each piece waits for its chunk's event), so only
-// the last chunk's decode follows the copy (C3: 18.7 ms of PCIe per GiB, 2.7 ms of decode).
-constexpr uint64_t kPipeChunk = 64 << 20;  // (drp_ctx::pipe_chunk's default)
+// lands: the DMA engine copies it in chunks of at least drp_ctx::pipe_chunk (128 MiB; 64 and 256
+// measured 0.3 and 0.2 ms slower on C3) on the ctx's copy stream while the compute stream decodes a
+// piece per chunk (each piece waits for its chunk's event) and fetches its rows into
+// drp_decode_batch's host columns, so only the last chunk's decode and fetch follow the copy (C3:
+// 19 ms of PCIe per GiB, 2.8 ms of decode and 1.3 ms of fetch).
 constexpr uint64_t kPipeEvents = 32;  // chunks at most (drp_ctx::pev)
 
 // payload offsets of a pipelined piece's rows: piece-relative -> relative to the pipelined range
@@ -1409,7 +1410,7 @@ static int stage_decode(drp_ctx *c, const HostSrc &H, drp_carry *carry, uint64_t
   const bool pieces = host_in && n - brem >= kPiecesMin &&
                       (c->blob_skip == DRP_BLOB_SKIP_ALWAYS ||
                        (c->blob_skip == DRP_BLOB_SKIP_AUTO && (c->blob_heavy || c->frames_per_byte == 0)));
-  // a large flat batch in page-locked memory staged whole: decoded as it lands (kPipeChunk)
+  // a large flat batch in page-locked memory staged whole: decoded as it lands (pipe_chunk)
   const bool pipe =
       !pieces && host_in && H.flat && c->pipe_chunk && n - brem >= 2 * c->pipe_chunk && is_pinned_host(H.flat);
   if (pieces || pipe) {

@@ -1,5 +1,5 @@
-"""GPU: pipelined staging of large flat batches in page-locked memory (drp_api.hip kPipeChunk).
-The DMA engine copies the batch in 64 MiB chunks on the ctx's copy stream while the compute
+"""GPU: pipelined staging of large flat batches in page-locked memory (drp_api.hip, drp_ctx::pipe_chunk).
+The DMA engine copies the batch in 128 MiB chunks on the ctx's copy stream while the compute
 stream decodes one piece per chunk; pieces resume at the frame a chunk edge cut and jump the
 blobs they end inside (decode.js:179-202: blob payloads are only sliced). Every frame, the carry
 and the error must equal the oracle's whole-batch decode, and the staged rows stay one piece
@@ -17,10 +17,14 @@ pytestmark = pytest.mark.gpu
 MiB = 1 << 20
 
 
-@pytest.fixture()
-def ctx():
+@pytest.fixture(params=["32", "128"])
+def ctx(request, monkeypatch):
+    """A ctx pipelining in 32 MiB chunks (many piece edges) or in the default 128 MiB ones
+    (DRP_PIPE_CHUNK is read when the ctx opens)."""
     from _gpu import drp_amd
+    monkeypatch.setenv("DRP_PIPE_CHUNK", request.param)
     c = drp_amd.Ctx(0)
+    c.pipe_chunk = int(request.param) << 20
     yield c
     c.close()
 
@@ -52,14 +56,15 @@ def _key_text(wire, r, rows):
 
 
 def test_pipelined_c3_batches(ctx):
-    """A 226 MB C3-shaped batch (1000 C2 frames + one 1 MiB blob per unit) from pinned memory:
+    """A 283 MB C3-shaped batch (1000 C2 frames + one 1 MiB blob per unit) from pinned memory:
     the first decode probes in blob-skipping pieces and pipelines the rest, the next ones
     pipeline the whole batch; all equal the oracle, and the key text built on the device too."""
     from _gpu import assert_same
-    wire = S.c3_stream(random.Random(31), 200, frames_per_unit=1000)
-    nexp = 200 * 1001
+    wire = S.c3_stream(random.Random(31), 250, frames_per_unit=1000)
+    nexp = 250 * 1001
     ref = O.decode_batch(wire, cap=nexp + 16)
     assert ref["nframes"] == nexp and ref["err_code"] == 0
+    assert len(wire) >= 2 * ctx.pipe_chunk
     t, a = _pinned(wire)
     for k in range(3):
         g = ctx.decode_batch(a, cap=nexp + 16)
@@ -100,7 +105,7 @@ def test_pipelined_long_frames_carry_and_errors(ctx, case):
         wire = wire + S.varint(5) + b"\x07abcd" + S.c2_stream(1000, seed=5).tobytes()
     elif case == "bad_change":
         wire = wire + S.frame(b"\xff\xff\xff", 1) + S.c2_stream(1000, seed=6).tobytes()
-    assert len(wire) >= 256 * MiB
+    assert len(wire) >= 2 * ctx.pipe_chunk
     ref = O.decode_batch(wire, blob_remaining=brem, cap=2_000_000)
     assert ref["nframes"] < 1_999_000
     t, a = _pinned(wire)
