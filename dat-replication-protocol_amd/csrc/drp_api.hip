@@ -179,6 +179,11 @@ struct drp_ctx {
   // pipelined staging (stage_pieces): the copy stream and one event per chunk (created on first use)
   hipStream_t cst = nullptr;
   hipEvent_t pev[32] = {};
+  // their early fetches: a fetch stream, the event behind a piece's last row writes, and a pinned
+  // bounce buffer the rows land in before a worker thread copies them into the caller's columns
+  hipStream_t fst = nullptr;
+  hipEvent_t fev = nullptr;
+  PinBuf fbounce;
   uint64_t pipe_chunk = 128ull << 20;  // DRP_PIPE_CHUNK (MiB; 0: no pipelining)
   uint32_t B = 128;
   int strict = 0;
@@ -287,7 +292,11 @@ int drp_open(int device, drp_ctx **out) {
   }
   for (auto &e : c->ev) (void)hipEventCreate(&e);
   for (auto &e : c->hev) (void)hipEventCreate(&e);
-  if (hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->fst, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->fev, hipEventDisableTiming) != hipSuccess) {
+    if (c->cst) (void)hipStreamDestroy(c->cst);
+    if (c->fst) (void)hipStreamDestroy(c->fst);
     (void)hipStreamDestroy(c->st);
     delete c;
     return DRP_E_HIP;
@@ -338,6 +347,10 @@ void drp_close(drp_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamSynchronize(c->cst);
   (void)hipStreamDestroy(c->cst);
+  (void)hipStreamSynchronize(c->fst);
+  (void)hipStreamDestroy(c->fst);
+  (void)hipEventDestroy(c->fev);
+  c->fbounce.release();
   (void)hipStreamDestroy(c->st);
   delete c;
 }
@@ -617,6 +630,23 @@ constexpr int kSpecRepairPasses = 16;
 constexpr int kChain = 3;  // dirty-list repair passes queued per host read
 constexpr int kSegRepairAfter = 3;  // verify passes before the segmented repair of the streams still missing
 
+// A repair pass's clears in one launch (six fills cost ~50 us of launch gaps per pass): the entry
+// words, the flag word, the first-miss words, the verify list's count and this pass's dirty-list
+// count and overflow word.
+__global__ __launch_bounds__(256) void pass_clear_kernel(uint64_t *incl_e, uint64_t nt, uint64_t *first_miss,
+                                                         uint64_t ns, uint32_t *overflow, uint32_t *vlist_n,
+                                                         uint32_t *dl_n, uint32_t *dl_ovf) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256u, i0 = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  for (uint64_t i = i0; i < nt; i += stride) incl_e[i] = 0;
+  for (uint64_t i = i0; i < ns; i += stride) first_miss[i] = ~0ull;
+  if (i0 == 0) {
+    *overflow = 0;
+    *vlist_n = 0;
+    *dl_n = 0;
+    *dl_ovf = 0;
+  }
+}
+
 int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uint64_t *stream_off,
                     const uint64_t *entry, uint64_t ns, const drp_frames *fr, const drp_changes *co,
                     uint64_t cap, drp_stream_result *res) {
@@ -803,13 +833,11 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
       // (a pass whose input list is empty launches nothing but the memsets)
       const int chain = full ? 1 : std::min(kChain, kSpecRepairPasses - pass);
       for (int cp = 0; cp < chain; cp++) {
-        CHK(hipMemsetAsync(P.incl_e, 0, NT * 8, st));
-        CHK(hipMemsetAsync(P.overflow, 0, 4, st));
-        CHK(hipMemsetAsync(P.first_miss, 0xFF, ns * 8, st));
-        CHK(hipMemsetAsync(P.vlist_n, 0, 4, st));
         const uint32_t kn = k ^ 1u;  // this pass's dirty list
-        CHK(hipMemsetAsync(ctrl + 8 + kn, 0, 4, st));
-        CHK(hipMemsetAsync(ctrl + 10 + kn, 0, 4, st));
+        const uint32_t cg = (uint32_t)std::min<uint64_t>(1024, (std::max<uint64_t>(NT, ns) + 255) / 256);
+        hipLaunchKernelGGL(pass_clear_kernel, dim3(cg), dim3(256), 0, st, P.incl_e, NT, P.first_miss, ns, P.overflow,
+                           P.vlist_n, ctrl + 8 + kn, ctrl + 10 + kn);
+        CHK(hipGetLastError());
         DecodeParams V = P;
         V.dlist = dl[kn];
         V.dlist_n = ctrl + 8 + kn;
@@ -1155,6 +1183,57 @@ static int fetch_staged_at(drp_ctx *c, const drp_frames *frames, const drp_chang
   return fetch_staged(c, &f, &o, first, rows);
 }
 
+// An early fetch of pipelined pieces (worker thread): staged GPU rows [g0, g0 + ng) into the host
+// columns from row `dst` on, by DMA into the pinned bounce buffer on the fetch stream (behind
+// c->fev, recorded after the rows' last writes) and a host copy from there; payload offsets made
+// batch offsets per piece as fetch_staged does. The caller sized c->fbounce (fetch_bounce_bytes).
+struct FetchCol {
+  const void *src;
+  void *dst;
+  uint32_t w;
+};
+static int fetch_cols(const drp_ctx *c, const drp_frames *F, const drp_changes *O, FetchCol *col) {
+  const auto &S = c->staged;
+  const void *src[14] = {S.fr.payload_off, S.fr.payload_len, S.fr.type, S.co.key_off, S.co.key_len,
+                         S.co.subset_off, S.co.subset_len, S.co.value_off, S.co.value_len, S.co.change,
+                         S.co.from, S.co.to, S.co.flags, S.co.key_hash};
+  void *dst[14] = {F->payload_off, F->payload_len, F->type, O->key_off, O->key_len, O->subset_off, O->subset_len,
+                   O->value_off, O->value_len, O->change, O->from, O->to, O->flags, O->key_hash};
+  static const uint32_t W[14] = {8, 4, 1, 4, 4, 4, 4, 4, 4, 8, 8, 8, 1, 8};
+  int n = 0;
+  for (int k = 0; k < 14; k++)
+    if (src[k] && dst[k]) col[n++] = {src[k], dst[k], W[k]};
+  return n;
+}
+constexpr uint64_t kBounceRows = 1 << 20;  // rows per bounce round (14 columns: <= 112 MiB pinned)
+static uint64_t fetch_bounce_bytes(uint64_t ng) { return 14 * al(std::min(ng, kBounceRows) * 8); }
+static int fetch_bounce(drp_ctx *c, uint64_t dst, uint64_t g0, uint64_t ng) {
+  if (hipSetDevice(c->device) != hipSuccess) return DRP_E_HIP;
+  FetchCol col[14];
+  const int n = fetch_cols(c, c->dfr, c->dco, col);
+  uint8_t *b = static_cast<uint8_t *>(c->fbounce.p);
+  CHK(hipStreamWaitEvent(c->fst, c->fev, 0));
+  for (uint64_t r = 0; r < ng; r += kBounceRows) {
+    const uint64_t m = std::min(kBounceRows, ng - r);
+    uint64_t o = 0;
+    for (int k = 0; k < n; o += al(m * col[k].w), k++)
+      CHK(hipMemcpyAsync(b + o, static_cast<const uint8_t *>(col[k].src) + (g0 + r) * col[k].w, m * col[k].w,
+                         hipMemcpyDeviceToHost, c->fst));
+    CHK(hipStreamSynchronize(c->fst));
+    o = 0;
+    for (int k = 0; k < n; o += al(m * col[k].w), k++)
+      memcpy(static_cast<uint8_t *>(col[k].dst) + (dst + r) * col[k].w, b + o, m * col[k].w);
+  }
+  const auto &S = c->staged;
+  for (size_t k = 0; k < S.pieces.size(); k++) {
+    const uint64_t r0 = S.pieces[k].first, r1 = k + 1 < S.pieces.size() ? S.pieces[k + 1].first : ~0ull;
+    const uint64_t sh = S.pieces[k].second, lo = std::max(r0, g0), hi = std::min(r1, g0 + ng);
+    if (sh)
+      for (uint64_t g = lo; g < hi; g++) c->dfr->payload_off[dst + (g - g0)] += sh;
+  }
+  return DRP_OK;
+}
+
 static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, bool pipe, drp_carry *carry,
                         uint64_t *n_frames, uint64_t *err_frame, uint32_t *err_code, uint32_t *err_detail) {
   hipStream_t st = c->st;
@@ -1162,6 +1241,17 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, bool pipe, d
   // pend[k] and signalled by c->pev[k]; each piece ends at a chunk's end. The copy stream is
   // drained on every way out (its DMAs write into in_stage).
   uint64_t pbase = 0, jumped = 0;
+  double tf = 0, tw = 0, tb = now_ms();  // (DRP_TRACE: early-fetch and piece-wait host time)
+  int nfetch = 0;
+  // the early fetches (pipe, drp_decode_batch's host columns): one worker thread at a time
+  std::thread fetcher;
+  int fetch_rc = DRP_OK;
+  struct Join {
+    std::thread &t;
+    ~Join() {
+      if (t.joinable()) t.join();
+    }
+  } join{fetcher};
   std::vector<uint64_t> pend;
   size_t pk = 0;
   struct Drain {
@@ -1213,8 +1303,14 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, bool pipe, d
       pbase = pos & ~15ull;
       const uint64_t m = n - pbase;
       if (!c->in_stage.ensure(m + 64)) return DRP_E_NOMEM;
-      const uint64_t chunk = (std::max(c->pipe_chunk, (m + kPipeEvents - 1) / kPipeEvents) + 0xFFFF) & ~0xFFFFull;
-      for (uint64_t e = pbase + chunk; e < n; e += chunk) pend.push_back(e);
+      // uniform chunks, then a half and a quarter chunk: the decode and fetch left after the copy
+      // are a quarter chunk's (each piece's decode hides behind the next, shorter copy)
+      const uint64_t chunk =
+          (std::max(c->pipe_chunk, (m + kPipeEvents - 3) / (kPipeEvents - 2)) + 0xFFFF) & ~0xFFFFull;
+      const uint64_t t2 = (n - chunk / 4) & ~0xFFFFull, t1 = (n - 3 * chunk / 4) & ~0xFFFFull;
+      for (uint64_t e = pbase + chunk; e < t1; e += chunk) pend.push_back(e);
+      if (t1 > pbase) pend.push_back(t1);
+      if (t2 > t1) pend.push_back(t2);
       pend.push_back(n);
       CHK(hipEventRecord(c->hev[0], c->cst));
       for (size_t k = 0; k < pend.size(); k++) {
@@ -1225,6 +1321,8 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, bool pipe, d
         CHK(hipEventRecord(c->pev[k], c->cst));
       }
       CHK(hipEventRecord(c->hev[1], c->cst));
+      TRACE("stage: pipelined from %llu in %zu chunks of %llu B", (unsigned long long)pbase, pend.size(),
+            (unsigned long long)chunk);
       staged += m;
       S.pieces.emplace_back(rows, pbase);
     }
@@ -1285,7 +1383,11 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, bool pipe, d
     hipLaunchKernelGGL(piece_tail_kernel, dim3(1), dim3(1), 0, st, dres, fr.payload_off, dboff);
     CHK(hipGetLastError());
     CHK(hipMemcpyAsync(&hr, dres, sizeof(hr), hipMemcpyDeviceToHost, st));
-    CHK(hipStreamSynchronize(st));
+    {
+      const double t0 = now_ms();
+      CHK(hipStreamSynchronize(st));
+      tw += now_ms() - t0;
+    }
     const uint64_t boff = hr.boff;
     if (pipe) {  // the pipelined range is one piece: its rows' payload offsets from pbase
       const uint64_t nr = r.frames + ((r.err_code == DRP_ERR_CHANGE || r.err_code == DRP_ERR_REQUIRED) ? 1 : 0);
@@ -1348,12 +1450,38 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, bool pipe, d
     if (pipe && c->dfr) {  // the rows so far into drp_decode_batch's host columns, while the copy runs
       const uint64_t upto = std::min(S.nf0 + rows, c->dcap);
       if (upto > c->dfetched) {
-        S.rows = S.nf0 + rows;
-        if (const int rc = fetch_staged_at(c, c->dfr, c->dco, c->dfetched, upto - c->dfetched)) return rc;
+        const double t0 = now_ms();
+        if (fetcher.joinable()) fetcher.join();
+        tf += now_ms() - t0;
+        if (fetch_rc) return fetch_rc;
+        uint64_t a = c->dfetched;
+        if (a == 0 && S.nf0) {  // (the carried blob's row, built on the host)
+          c->dfr->payload_off[0] = S.off0;
+          c->dfr->payload_len[0] = S.len0;
+          c->dfr->type[0] = S.ty0;
+          a = 1;
+        }
+        if (upto > a) {
+          const uint64_t g0 = a - S.nf0, ng = upto - a;
+          if (c->fbounce.ensure(fetch_bounce_bytes(ng))) {
+            CHK(hipEventRecord(c->fev, st));
+            fetcher = std::thread([c, a, g0, ng, &fetch_rc] { fetch_rc = fetch_bounce(c, a, g0, ng); });
+          } else {  // (no pinned bounce buffer: a direct fetch here)
+            S.rows = S.nf0 + rows;
+            if (const int rc = fetch_staged_at(c, c->dfr, c->dco, a, ng)) return rc;
+          }
+          nfetch++;
+        }
         c->dfetched = upto;
       }
     }
   }
+  if (fetcher.joinable()) {
+    const double t0 = now_ms();
+    fetcher.join();
+    tf += now_ms() - t0;
+  }
+  if (fetch_rc) return fetch_rc;
   c->timing = sum;
   if (span_now) c->piece_span = span_now;
   if (!pend.empty()) {
@@ -1362,6 +1490,8 @@ static int stage_pieces(drp_ctx *c, const HostSrc &H, uint64_t pos, bool pipe, d
     if (hipEventElapsedTime(&ms, c->hev[0], c->hev[1]) == hipSuccess) h2d_ms += ms;
   }
   c->timing.h2d_ms = h2d_ms;
+  TRACE("stage: %llu pieces in %.2f ms (h2d %.2f): %d early fetches (%.2f ms waited for), result waits %.2f ms",
+        (unsigned long long)npieces, now_ms() - tb, h2d_ms, nfetch, tf, tw);
   c->timing.h2d_bytes = staged;
   c->timing.h2d_skipped = skipped;
   c->timing.host_copied = copied;
@@ -1413,6 +1543,8 @@ static int stage_decode(drp_ctx *c, const HostSrc &H, drp_carry *carry, uint64_t
   // a large flat batch in page-locked memory staged whole: decoded as it lands (pipe_chunk)
   const bool pipe =
       !pieces && host_in && H.flat && c->pipe_chunk && n - brem >= 2 * c->pipe_chunk && is_pinned_host(H.flat);
+  TRACE("stage: %llu B, host %d flat %d pinned %d pieces %d pipe %d", (unsigned long long)n, (int)host_in,
+        H.flat != nullptr, (int)(H.flat && is_pinned_host(H.flat)), (int)pieces, (int)pipe);
   if (pieces || pipe) {
     // (AUTO: a ctx's first batch probes in pieces too; pieces grow geometrically while no blob
     // is met, so a batch without blobs costs a few more launches once)
