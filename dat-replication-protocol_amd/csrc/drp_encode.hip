@@ -257,11 +257,17 @@ __global__ __launch_bounds__(256) void enc_write_kernel(EncodeParams P) {
 #ifndef DRP_ENC_OS
 #define DRP_ENC_OS 1  // 0: the per-frame writer for every frame (A/B)
 #endif
+#ifndef DRP_ENC_DPP
+#define DRP_ENC_DPP 1  // a lane's second source block from the next lane (wave shift) where it can
+#endif                  // (C5 encode 2.02 -> 1.87 ms; 0: two loads per lane, A/B)
+#ifndef DRP_ENC_U
+#define DRP_ENC_U 4
+#endif
 #ifndef DRP_ENC_BS
 #define DRP_ENC_BS 65536  // output block bytes (a multiple of 16 KiB, at most 1 MiB)
 #endif
 constexpr uint32_t ENC_BS = DRP_ENC_BS, ENC_CPB = ENC_BS / 16, ENC_OS_T = 256, ENC_FMAX = 128;
-constexpr uint32_t ENC_U = 4, ENC_NB = ENC_CPB / (ENC_OS_T * ENC_U);  // chunks per lane: ENC_NB batches of ENC_U
+constexpr uint32_t ENC_U = DRP_ENC_U, ENC_NB = ENC_CPB / (ENC_OS_T * ENC_U);  // chunks per lane: ENC_NB batches of ENC_U
 static_assert(ENC_NB >= 1 && ENC_NB * ENC_U <= 32 && ENC_CPB % (ENC_OS_T * ENC_U) == 0, "ENC_BS");
 constexpr uint32_t LIT0 = 0, LIT2 = 24, LIT4 = 32, LITB = 72;  // prefix byte slots per frame
 // Mixed chunks (not inside one copy segment) per block: at most 3 + 2 + 4 per frame (the chunks the
@@ -480,6 +486,34 @@ __global__ __launch_bounds__(ENC_OS_T) void enc_write_os(EncodeParams P) {
       }
     }
     uint4 v0[ENC_U], v1[ENC_U];
+#if DRP_ENC_DPP
+    // a lane's second block is the next lane's first when that lane copies the next 16 source
+    // bytes (one copy segment across the two chunks): taken from it by a wave shift (DPP) instead
+    // of loaded again; the lanes at segment ends and lane 63 load it
+    bool own1[ENC_U];
+#pragma unroll
+    for (uint32_t u = 0; u < ENC_U; u++) {
+      const uintptr_t a = fast[u] ? (uintptr_t)sa[u] : 0;
+      const uint32_t nlo = (uint32_t)__builtin_amdgcn_update_dpp(0u, (uint32_t)a, 0x130, 0xF, 0xF, false);
+      const uint32_t nhi = (uint32_t)__builtin_amdgcn_update_dpp(0u, (uint32_t)(a >> 32), 0x130, 0xF, 0xF, false);
+      const uintptr_t na = ((uintptr_t)nhi << 32) | nlo;
+      own1[u] = fast[u] && shv[u] && na != a + 16;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < ENC_U; u++) {
+      v0[u] = v1[u] = make_uint4(0, 0, 0, 0);
+      if (fast[u]) v0[u] = sa[u][0];
+      if (own1[u]) v1[u] = sa[u][1];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < ENC_U; u++) {
+      const uint4 n = make_uint4((uint32_t)__builtin_amdgcn_update_dpp(0u, v0[u].x, 0x130, 0xF, 0xF, false),
+                                 (uint32_t)__builtin_amdgcn_update_dpp(0u, v0[u].y, 0x130, 0xF, 0xF, false),
+                                 (uint32_t)__builtin_amdgcn_update_dpp(0u, v0[u].z, 0x130, 0xF, 0xF, false),
+                                 (uint32_t)__builtin_amdgcn_update_dpp(0u, v0[u].w, 0x130, 0xF, 0xF, false));
+      if (!own1[u]) v1[u] = n;
+    }
+#else
 #pragma unroll
     for (uint32_t u = 0; u < ENC_U; u++) {
       v0[u] = v1[u] = make_uint4(0, 0, 0, 0);
@@ -488,6 +522,7 @@ __global__ __launch_bounds__(ENC_OS_T) void enc_write_os(EncodeParams P) {
         if (shv[u]) v1[u] = sa[u][1];
       }
     }
+#endif
 #pragma unroll
     for (uint32_t u = 0; u < ENC_U; u++)
       if (fast[u]) {
