@@ -1,3 +1,4 @@
+# A/B: C3 through the pipelined staging at several DRP_PIPE_CHUNK (MiB; 0 = staged whole) / DRP_WALK_MIN values
 set -o pipefail
 mkdir -p gpurun_out/ab
 for cfg in "64 32768" "64 4096" "128 8192" "128 32768" "256 32768" "0 32768"; do
