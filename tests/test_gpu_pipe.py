@@ -120,3 +120,36 @@ def test_pipelined_long_frames_carry_and_errors(ctx, case):
     finally:
         ctx.set_blob_skip(drp_amd.BLOB_SKIP_AUTO)
     del t
+
+
+@pytest.mark.parametrize("block", [False, True])
+def test_pipelined_stage_then_fetch(ctx, block):
+    """drp_decode_stage of a pipelined batch, then the staged rows fetched later: in three
+    drp_decode_fetch calls, or as one drp_decode_fetch_block_ex with f64 columns; the key text
+    (drp_decode_fetch_keys) when the rows are one staged range (a fresh ctx's first batch probes in
+    pieces first: then it may decline, as for any batch staged in pieces)."""
+    wire = S.c3_stream(random.Random(37), 250, frames_per_unit=1000)
+    nexp = 250 * 1001
+    ref = O.decode_batch(wire, cap=nexp + 16)
+    t, a = _pinned(wire)
+    for k in range(2):
+        o = ctx.decode_staged(a, pieces=3, block=block, f64=block, keys=True)
+        assert (o["nframes"], o["err_code"], o["consumed"]) == (nexp, 0, len(wire))
+        for c in ["payload_off", "payload_len", "type"]:
+            np.testing.assert_array_equal(o[c].astype(np.float64 if block and c == "payload_off" else ref[c].dtype),
+                                          ref[c].astype(np.float64) if block and c == "payload_off" else ref[c],
+                                          err_msg=f"#{k}:{c}")
+        ch = ref["type"] == 1
+        for c in O.COLS32:
+            np.testing.assert_array_equal(o[c][ch], ref[c][ch], err_msg=f"#{k}:{c}")
+        # (keys=True adds the key flags, DRP_F_KEY_ASCII | DRP_F_KEY_UTF8: C2 keys are ASCII)
+        np.testing.assert_array_equal(o["flags"][ch] & 0x0F, ref["flags"][ch], err_msg=f"#{k}:flags")
+        assert np.all(o["flags"][ch] & 0x30 == 0x30)
+        for c in O.COLS64:
+            np.testing.assert_array_equal(o[c][ch].astype(np.float64) if block else o[c][ch],
+                                          ref[c][ch].astype(np.float64) if block else ref[c][ch], err_msg=f"#{k}:{c}")
+        if k == 1 or o["key_text"] is not None:
+            kp, text = _key_text(wire, ref, nexp)
+            assert o["key_text"] == text
+            np.testing.assert_array_equal(o["kp"], kp)
+    del t
