@@ -234,7 +234,12 @@ int drp_decode_device(drp_ctx *ctx, const uint8_t *bytes, uint64_t nbytes,
  * carry->blob_remaining in: leading blob continuation; out: carry for the next batch.
  * Returns frames delivered in *n_frames, first failing frame in *err_frame
  * (UINT64_MAX if none) with *err_code and *err_detail. A leading blob continuation is
- * reported as frame 0 with type DRP_TYPE_BLOB|0x40 (continuation). */
+ * reported as frame 0 with type DRP_TYPE_BLOB|0x40 (continuation).
+ * A host batch of 256 MiB or more in page-locked memory is decoded as it is copied (128 MiB DMA
+ * chunks on a second stream of the ctx, one piece decoded per chunk; the rows of each piece are
+ * copied into the host columns by a ctx-internal worker thread during the next chunk's copy):
+ * the results are those of one whole-batch decode, and the call still returns only when every
+ * row is in the columns. A ctx stays single-threaded for its callers. */
 #define DRP_FRAME_CONT 0x40
 int drp_decode_batch(drp_ctx *ctx, const uint8_t *bytes, uint64_t n, drp_carry *carry,
                      const drp_frames *frames, const drp_changes *cols, uint64_t cap,
