@@ -741,7 +741,12 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
   if (dstats) P.stats = dstats;
   {  // tile_prefix and every per-decode clear in one launch
     ClearSet cs = {};
+    hipError_t ce = hipSuccess;
     auto add = [&](void *p, uint64_t bytes, uint32_t v) {
+      if (cs.n == ClearSet::CAP) {  // (not reached: CAP covers every fill of a decode)
+        if (ce == hipSuccess) ce = hipMemsetAsync(p, (int)(v & 0xFF), bytes, st);
+        return;
+      }
       cs.ptr[cs.n] = p;
       cs.bytes[cs.n] = bytes;
       cs.value[cs.n++] = v;
@@ -755,6 +760,7 @@ int run_decode_spec(drp_ctx *c, const uint8_t *bytes, uint64_t nbytes, const uin
     if (P.tile_rec) add(P.tile_rec, NT * 4, 0xFF);
     if (P.walk_dense) add(P.walk_dense, 16, 0);
     if (dstats) add(dstats, 64 * 8, 0);
+    CHK(ce);
     CHK(drp_launch_prologue(B, stream_off, ns, tile_prefix, &cs, st));
   }
   c->timing.seg_repairs = 0;

@@ -114,9 +114,10 @@ struct EncodeParams {
 extern "C" {
 // regions a decode's prologue fills (drp_launch_prologue): byte value, 4-byte multiples
 struct ClearSet {
-  void *ptr[8];
-  uint64_t bytes[8];
-  uint32_t value[8];
+  static constexpr uint32_t CAP = 12;  // (a decode fills up to 9: with records, the density sample and DRP_STATS)
+  void *ptr[CAP];
+  uint64_t bytes[CAP];
+  uint32_t value[CAP];
   uint32_t n;
 };
 hipError_t drp_launch_prologue(uint32_t B, const uint64_t *stream_off, uint64_t nstreams, uint64_t *tile_prefix,
